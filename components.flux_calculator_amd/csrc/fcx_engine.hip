@@ -1,0 +1,957 @@
+// fcx_engine.hip -- host side of libfcx: the C ABI of include/fcx.h.
+//
+// The engine mirrors the reference data model (local_field(0:10,3)%var(35), basic:86-103):
+// every bound slot points at a caller array; identical pointers are aliases and share one
+// device buffer (the reference's pointer aliasing, basic:334-358 / prepare:36-38).  At
+// fcx_commit the planner validates the bindings against the flux_calculator_prepare.F90
+// rules, allocates one device mirror per distinct host array (one pooled hipMalloc, 256-B
+// aligned sub-buffers), and builds device parameter blocks for the fused launches.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cctype>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <set>
+#include <string>
+#include <vector>
+
+#include "fcx_internal.h"
+
+using namespace fcx;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char *fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                  \
+  do {                                                                                 \
+    hipError_t e_ = (expr);                                                            \
+    if (e_ != hipSuccess) return fail(FCX_E_HIP, "%s: %s", #expr, hipGetErrorString(e_)); \
+  } while (0)
+
+const char *kVarNames[kNumVars] = {
+    "ALBE", "ALBA", "AMOI", "AMOM", "FARE", "FICE", "PATM", "PSUR", "QATM", "TATM", "TSUR", "UATM",
+    "VATM", "U10M", "V10M", "CMOM", "CMOI", "CHEA", "QSUR", "HLAT", "HSEN", "MEVA", "MPRE", "MRAI",
+    "MSNO", "RBBR", "RLWD", "RLWU", "RSID", "RSIU", "RSIN", "RSDD", "RSDR", "UMOM", "VMOM"};
+
+struct Buffer {
+  double *host = nullptr;  // caller array (nullptr for device-bound)
+  double *dev = nullptr;   // device memory (engine pool or caller's)
+  int64_t n = 0;
+  bool external = false;   // caller-owned device memory
+};
+
+struct Csr {
+  bool set = false;
+  int64_t n_dst = 0;
+  std::vector<int32_t> row_ptr, col;
+  std::vector<double> w;
+  int32_t *d_row = nullptr, *d_col = nullptr;
+  double *d_w = nullptr;
+};
+
+struct Plan {
+  Params host{};
+  Params *dev = nullptr;
+  std::vector<int> reads, writes;  // buffer ids
+};
+
+int var0(int var) { return var - 1; }
+
+}  // namespace
+
+struct fcx_engine {
+  int device = 0;
+  int T = 0;
+  int64_t n[3] = {0, 0, 0};
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  int8_t method[FCX_NUM_FLUXES][kMaxTypes] = {};
+  int slot[kMaxTypes + 1][3][kNumVars];
+  bool allocated[kMaxTypes + 1][3][kNumVars] = {};
+  uint8_t put_to[kMaxTypes + 1][3][kNumVars] = {};
+  std::vector<Buffer> bufs;
+  std::map<const double *, int> by_ptr;
+  bool committed = false;
+  bool any_regrid = false;
+  bool aligned16 = true;
+  // bias corrections (bias_corrections.F90)
+  bool lcorr = false;
+  int32_t init_date = 0;
+  std::vector<double> corr_mm;  // [12][n_t]
+  double *corr_dev = nullptr;
+  Csr rg[4];
+  std::vector<std::pair<int, std::pair<int, int>>> averages;  // (phase, (grid, var))
+  std::map<std::pair<uint32_t, int>, Plan> plans;               // (stages, avg phase mask)
+  void *pool = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  bool timed = false;
+
+  fcx_engine() {
+    for (auto &a : slot)
+      for (auto &b : a)
+        for (auto &c : b) c = -1;
+  }
+  int buf(int s, int g, int var) const { return slot[s][g - 1][var0(var)]; }
+  double *dptr(int s, int g, int var) const {
+    int b = buf(s, g, var);
+    return b < 0 ? nullptr : bufs[b].dev;
+  }
+};
+
+// ------------------------------------------------------------------ utilities
+
+extern "C" const char *fcx_last_error(void) { return g_err.c_str(); }
+extern "C" int fcx_version(void) { return FCX_VERSION; }
+
+extern "C" int fcx_method_from_string(const char *s, size_t len) {
+  if (!s) return -1;
+  size_t e = len;
+  while (e > 0 && (s[e - 1] == ' ' || s[e - 1] == '\0')) --e;  // trim()
+  std::string m(s, e);
+  static const char *names[] = {"none", "zero", "copy", "CCLM", "MOM5", "RCO", "water", "ice", "StBo"};
+  for (int i = 0; i < 9; ++i)
+    if (m == names[i]) return i;
+  return -1;
+}
+
+// datetime_helpers.py:4-13 (proleptic Gregorian civil-date arithmetic)
+static int64_t days_from_civil(int64_t y, int m, int d) {
+  y -= m <= 2;
+  const int64_t era = (y >= 0 ? y : y - 399) / 400;
+  const int64_t yoe = y - era * 400;
+  const int64_t doy = (153 * (m + (m > 2 ? -3 : 9)) + 2) / 5 + d - 1;
+  const int64_t doe = yoe * 365 + yoe / 4 - yoe / 100 + doy;
+  return era * 146097 + doe - 719468;
+}
+
+extern "C" int fcx_current_month(int32_t init_date, int64_t seconds, int32_t *month) {
+  if (!month) return fail(FCX_E_ARG, "month is NULL");
+  const int64_t y = init_date / 10000;
+  const int m = (init_date / 100) % 100, d = init_date % 100;
+  if (y < 1 || m < 1 || m > 12 || d < 1 || d > 31)
+    return fail(FCX_E_ARG, "init_date %d is not YYYYMMDD", (int)init_date);
+  int64_t q = seconds / 86400;
+  if (seconds % 86400 != 0 && seconds < 0) q -= 1;
+  const int64_t z = days_from_civil(y, m, d) + q + 719468;
+  const int64_t era = (z >= 0 ? z : z - 146096) / 146097;
+  const int64_t doe = z - era * 146097;
+  const int64_t yoe = (doe - doe / 1460 + doe / 36524 - doe / 146096) / 365;
+  const int64_t doy = doe - (365 * yoe + yoe / 4 - yoe / 100);
+  const int64_t mp = (5 * doy + 2) / 153;
+  *month = (int32_t)(mp < 10 ? mp + 3 : mp - 9);
+  return FCX_OK;
+}
+
+// ------------------------------------------------------------------ set-up
+
+extern "C" int fcx_create(int device, int num_surface_types, const int32_t grid_size[3],
+                          fcx_engine **out) {
+  if (!out || !grid_size) return fail(FCX_E_ARG, "NULL argument");
+  *out = nullptr;
+  if (num_surface_types < 1 || num_surface_types > kMaxTypes)
+    return fail(FCX_E_ARG, "num_surface_types=%d outside 1..%d", num_surface_types, kMaxTypes);
+  for (int g = 0; g < 3; ++g)
+    if (grid_size[g] < 0) return fail(FCX_E_ARG, "grid_size(%d)=%d < 0", g + 1, grid_size[g]);
+  HIP_TRY(hipSetDevice(device));
+  auto *e = new fcx_engine();
+  e->device = device;
+  e->T = num_surface_types;
+  for (int g = 0; g < 3; ++g) e->n[g] = grid_size[g];
+  hipError_t err = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
+  if (err != hipSuccess) {
+    delete e;
+    return fail(FCX_E_HIP, "hipStreamCreate: %s", hipGetErrorString(err));
+  }
+  e->own_stream = true;
+  if (hipEventCreate(&e->ev0) != hipSuccess || hipEventCreate(&e->ev1) != hipSuccess) {
+    delete e;
+    return fail(FCX_E_HIP, "hipEventCreate failed");
+  }
+  *out = e;
+  return FCX_OK;
+}
+
+extern "C" int fcx_destroy(fcx_engine *e) {
+  if (!e) return FCX_OK;
+  (void)hipSetDevice(e->device);
+  if (e->stream) (void)hipStreamSynchronize(e->stream);
+  for (auto &kv : e->plans) (void)hipFree(kv.second.dev);
+  for (auto &r : e->rg) {
+    (void)hipFree(r.d_row);
+    (void)hipFree(r.d_col);
+    (void)hipFree(r.d_w);
+  }
+  (void)hipFree(e->corr_dev);
+  (void)hipFree(e->pool);
+  if (e->ev0) (void)hipEventDestroy(e->ev0);
+  if (e->ev1) (void)hipEventDestroy(e->ev1);
+  if (e->own_stream && e->stream) (void)hipStreamDestroy(e->stream);
+  delete e;
+  return FCX_OK;
+}
+
+extern "C" int fcx_set_stream(fcx_engine *e, void *stream) {
+  if (!e) return fail(FCX_E_ARG, "NULL engine");
+  if (e->own_stream && e->stream) {
+    (void)hipStreamSynchronize(e->stream);
+    (void)hipStreamDestroy(e->stream);
+  }
+  e->stream = reinterpret_cast<hipStream_t>(stream);
+  e->own_stream = false;
+  return FCX_OK;
+}
+
+extern "C" int fcx_set_method(fcx_engine *e, int flux, int s, int method) {
+  if (!e) return fail(FCX_E_ARG, "NULL engine");
+  if (e->committed) return fail(FCX_E_STATE, "engine already committed");
+  if (flux < 0 || flux >= FCX_NUM_FLUXES) return fail(FCX_E_ARG, "flux %d unknown", flux);
+  if (s < 1 || s > e->T) return fail(FCX_E_ARG, "surface_type %d outside 1..%d", s, e->T);
+  if (method < FCX_NONE || method > FCX_STBO) return fail(FCX_E_ARG, "method %d unknown", method);
+  e->method[flux][s - 1] = (int8_t)method;
+  return FCX_OK;
+}
+
+extern "C" int fcx_bind_field(fcx_engine *e, int s, int g, int var, double *ptr, int64_t n,
+                              int flags) {
+  if (!e) return fail(FCX_E_ARG, "NULL engine");
+  if (e->committed) return fail(FCX_E_STATE, "engine already committed");
+  if (s < 0 || s > kMaxTypes || g < 1 || g > 3 || var < 1 || var > kNumVars)
+    return fail(FCX_E_ARG, "slot (%d,%d,%d) out of range", s, g, var);
+  if (!ptr) {
+    e->slot[s][g - 1][var0(var)] = -1;
+    return FCX_OK;
+  }
+  if (n < e->n[g - 1])
+    return fail(FCX_E_ARG, "%s(%d,%s): array of %lld cells shorter than grid_size %lld",
+                kVarNames[var0(var)], s, g == 1 ? "t" : g == 2 ? "u" : "v", (long long)n,
+                (long long)e->n[g - 1]);
+  const bool on_dev = flags & FCX_MEM_DEVICE;
+  auto it = e->by_ptr.find(ptr);
+  int b;
+  if (it == e->by_ptr.end()) {
+    Buffer bf;
+    bf.n = n;
+    if (on_dev) {
+      bf.dev = ptr;
+      bf.external = true;
+      if (reinterpret_cast<uintptr_t>(ptr) % 16) e->aligned16 = false;
+    } else {
+      bf.host = ptr;
+    }
+    b = (int)e->bufs.size();
+    e->bufs.push_back(bf);
+    e->by_ptr[ptr] = b;
+  } else {
+    b = it->second;
+    if (e->bufs[b].external != on_dev)
+      return fail(FCX_E_ARG, "pointer bound both as host and as device memory");
+    e->bufs[b].n = std::max(e->bufs[b].n, n);
+  }
+  e->slot[s][g - 1][var0(var)] = b;
+  e->allocated[s][g - 1][var0(var)] = (flags & FCX_ALLOCATED) != 0;
+  return FCX_OK;
+}
+
+extern "C" int fcx_set_corrections(fcx_engine *e, int enabled, int32_t init_date, const double *corr,
+                                   int64_t n, int layout) {
+  if (!e) return fail(FCX_E_ARG, "NULL engine");
+  if (e->committed) return fail(FCX_E_STATE, "engine already committed");
+  e->lcorr = enabled != 0;
+  e->init_date = init_date;
+  if (!e->lcorr) return FCX_OK;
+  int32_t mth;
+  if (fcx_current_month(init_date, 0, &mth) != FCX_OK) return FCX_E_ARG;
+  if (!corr || n < e->n[0]) return fail(FCX_E_ARG, "corrections: need %lld cells", (long long)e->n[0]);
+  const int64_t nt = e->n[0];
+  e->corr_mm.assign((size_t)12 * nt, 0.0);
+  // device layout [month][cell]: one coalesced month slice per step (the Fortran
+  // corrections(1,12,n) puts the 12 months of a cell together, bias:191)
+  for (int m = 0; m < 12; ++m)
+    for (int64_t j = 0; j < nt; ++j)
+      e->corr_mm[(size_t)m * nt + j] =
+          layout == FCX_CORR_CELL_MAJOR ? corr[(size_t)j * 12 + m] : corr[(size_t)m * n + j];
+  return FCX_OK;
+}
+
+extern "C" int fcx_set_regrid_matrix(fcx_engine *e, int which, int64_t nnz, const int32_t *src,
+                                     const int32_t *dst, const double *w) {
+  if (!e) return fail(FCX_E_ARG, "NULL engine");
+  if (e->committed) return fail(FCX_E_STATE, "engine already committed");
+  if (which < 0 || which > 3) return fail(FCX_E_ARG, "regrid matrix %d unknown", which);
+  static const int from_g[4] = {2, 3, 1, 1}, to_g[4] = {1, 1, 2, 3};
+  const int64_t n_src = e->n[from_g[which] - 1], n_dst = e->n[to_g[which] - 1];
+  Csr &c = e->rg[which];
+  c.set = true;
+  c.n_dst = n_dst;
+  c.row_ptr.assign((size_t)n_dst + 1, 0);
+  for (int64_t k = 0; k < nnz; ++k) {
+    if (src[k] < 1 || src[k] > n_src || dst[k] < 1 || dst[k] > n_dst)
+      return fail(FCX_E_ARG, "regrid link %lld (%d -> %d) outside the local grids (io:183-191)",
+                  (long long)k + 1, src[k], dst[k]);
+    c.row_ptr[(size_t)dst[k]]++;
+  }
+  for (int64_t d = 0; d < n_dst; ++d) c.row_ptr[(size_t)d + 1] += c.row_ptr[(size_t)d];
+  c.col.assign((size_t)nnz, 0);
+  c.w.assign((size_t)nnz, 0.0);
+  std::vector<int32_t> fill(c.row_ptr.begin(), c.row_ptr.end() - 1);
+  for (int64_t k = 0; k < nnz; ++k) {  // stable: link order kept inside each row
+    const int32_t at = fill[(size_t)dst[k] - 1]++;
+    c.col[(size_t)at] = src[k] - 1;
+    c.w[(size_t)at] = w[k];
+  }
+  return FCX_OK;
+}
+
+extern "C" int fcx_set_put_to(fcx_engine *e, int s, int g, int var, int mask) {
+  if (!e) return fail(FCX_E_ARG, "NULL engine");
+  if (e->committed) return fail(FCX_E_STATE, "engine already committed");
+  if (s < 0 || s > kMaxTypes || g < 1 || g > 3 || var < 1 || var > kNumVars || mask < 0 || mask > 7)
+    return fail(FCX_E_ARG, "bad put_to arguments");
+  e->put_to[s][g - 1][var0(var)] = (uint8_t)mask;
+  if (mask) e->any_regrid = true;
+  return FCX_OK;
+}
+
+extern "C" int fcx_add_average(fcx_engine *e, int phase, int g, int var) {
+  if (!e) return fail(FCX_E_ARG, "NULL engine");
+  if (e->committed) return fail(FCX_E_STATE, "engine already committed");
+  if ((phase != FCX_PHASE_EARLY && phase != FCX_PHASE_NORMAL) || g < 1 || g > 3 || var < 1 ||
+      var > kNumVars)
+    return fail(FCX_E_ARG, "bad average arguments");
+  e->averages.push_back({phase, {g, var}});
+  return FCX_OK;
+}
+
+// ------------------------------------------------------------------ validation
+
+// flux_calculator_prepare.F90: every method's inputs must be ASSOCIATED and its output
+// allocated; 'copy' needs the type-1 array.
+static int validate(fcx_engine *e) {
+  auto need = [&](int s, int g, int var, const char *what) -> int {
+    if (e->buf(s, g, var) < 0)
+      return fail(FCX_E_MISSING, "Error calculating %s for surface_type %d on the grid %s_grid: "
+                                 "lacking %s", what, s, g == 1 ? "t" : g == 2 ? "u" : "v",
+                  kVarNames[var0(var)]);
+    return FCX_OK;
+  };
+#define NEED(s, g, v, w)                      \
+  do {                                         \
+    if (int r_ = need(s, g, v, w)) return r_;  \
+  } while (0)
+  for (int s = 1; s <= e->T; ++s) {
+    for (int k = 0; k < 3; ++k) {
+      const int m = e->method[FCX_SPEC_VAPOR_SURFACE_T + k][s - 1];
+      const int g = k + 1;
+      if (m == FCX_CCLM) {
+        NEED(s, g, FCX_FICE, "QSUR"); NEED(s, g, FCX_PSUR, "QSUR"); NEED(s, g, FCX_TSUR, "QSUR");
+        NEED(s, g, FCX_QSUR, "QSUR");
+      } else if (m == FCX_COPY) {
+        NEED(1, g, FCX_QSUR, "QSUR");
+      } else if (m != FCX_NONE) {
+        return fail(FCX_E_ARG, "QSUR method %d not known", m);
+      }
+    }
+    int m = e->method[FCX_FLUX_MASS_EVAP][s - 1];
+    if (m == FCX_CCLM || m == FCX_MOM5) {
+      NEED(s, 1, m == FCX_CCLM ? FCX_AMOI : FCX_CMOI, "MEVA");
+      for (int v : {FCX_PSUR, FCX_QATM, FCX_QSUR, FCX_TATM, FCX_UATM, FCX_VATM}) NEED(s, 1, v, "MEVA");
+    } else if (m == FCX_RCO) {
+      for (int v : {FCX_QATM, FCX_TSUR, FCX_UATM, FCX_VATM}) NEED(s, 1, v, "MEVA");
+    } else if (m != FCX_NONE && m != FCX_ZERO && m != FCX_COPY) {
+      return fail(FCX_E_ARG, "MEVA method %d not known", m);
+    }
+    if (m != FCX_NONE) NEED(s, 1, FCX_MEVA, "MEVA");
+    if (m == FCX_COPY && e->lcorr) {
+      const int m1 = e->method[FCX_FLUX_MASS_EVAP][0];
+      if (!(m1 == FCX_ZERO || m1 == FCX_CCLM || m1 == FCX_MOM5 || m1 == FCX_RCO))
+        return fail(FCX_E_UNSUPPORTED,
+                    "MEVA 'copy' with bias corrections needs surface type 1 to compute MEVA");
+      if (e->buf(s, 1, FCX_MEVA) != e->buf(1, 1, FCX_MEVA))
+        return fail(FCX_E_ARG, "MEVA 'copy' of type %d must alias the type-1 array", s);
+    }
+    m = e->method[FCX_FLUX_HEAT_LATENT][s - 1];
+    if (m == FCX_WATER || m == FCX_ICE) NEED(s, 1, FCX_MEVA, "HLAT");
+    else if (m != FCX_NONE && m != FCX_ZERO && m != FCX_COPY)
+      return fail(FCX_E_ARG, "HLAT method %d not known", m);
+    if (m != FCX_NONE) NEED(s, 1, FCX_HLAT, "HLAT");
+    m = e->method[FCX_FLUX_HEAT_SENSIBLE][s - 1];
+    if (m == FCX_CCLM || m == FCX_MOM5) {
+      NEED(s, 1, m == FCX_CCLM ? FCX_AMOI : FCX_CHEA, "HSEN");
+      for (int v : {FCX_PATM, FCX_PSUR, FCX_QATM, FCX_TATM, FCX_TSUR, FCX_UATM, FCX_VATM})
+        NEED(s, 1, v, "HSEN");
+    } else if (m == FCX_RCO) {
+      for (int v : {FCX_TATM, FCX_TSUR, FCX_UATM, FCX_VATM}) NEED(s, 1, v, "HSEN");
+    } else if (m != FCX_NONE && m != FCX_ZERO && m != FCX_COPY) {
+      return fail(FCX_E_ARG, "HSEN method %d not known", m);
+    }
+    if (m != FCX_NONE) NEED(s, 1, FCX_HSEN, "HSEN");
+    m = e->method[FCX_FLUX_MOMENTUM][s - 1];
+    for (int g = 2; g <= 3; ++g) {
+      if (m == FCX_CCLM || m == FCX_MOM5) {
+        NEED(s, g, m == FCX_CCLM ? FCX_AMOM : FCX_CMOM, "UMOM/VMOM");
+        for (int v : {FCX_PSUR, FCX_QSUR, FCX_TSUR, FCX_UATM, FCX_VATM}) NEED(s, g, v, "UMOM/VMOM");
+      } else if (m == FCX_RCO) {
+        for (int v : {FCX_UATM, FCX_VATM}) NEED(s, g, v, "UMOM/VMOM");
+      } else if (m != FCX_NONE && m != FCX_ZERO && m != FCX_COPY) {
+        return fail(FCX_E_ARG, "momentum method %d not known", m);
+      }
+      if (m != FCX_NONE) NEED(s, g, g == 2 ? FCX_UMOM : FCX_VMOM, "UMOM/VMOM");
+    }
+    m = e->method[FCX_FLUX_RADIATION_BLACKBODY][s - 1];
+    if (m == FCX_STBO) NEED(s, 1, FCX_TSUR, "RBBR");
+    else if (m != FCX_NONE && m != FCX_ZERO && m != FCX_COPY)
+      return fail(FCX_E_ARG, "RBBR method %d not known", m);
+    if (m != FCX_NONE) NEED(s, 1, FCX_RBBR, "RBBR");
+  }
+#undef NEED
+  return FCX_OK;
+}
+
+// P7 trigger of flux_calculator.F90:913-914/1003-1004 + calc:376
+static bool average_applies(const fcx_engine *e, int g, int var) {
+  return e->buf(0, g, var) >= 0 && e->T >= 2 && e->buf(2, g, var) >= 0 &&
+         e->allocated[0][g - 1][var0(var)];
+}
+
+// ------------------------------------------------------------------ planning
+
+static bool is_compute(int m) { return m == FCX_ZERO || m == FCX_CCLM || m == FCX_MOM5 || m == FCX_RCO; }
+
+// Can u/v work be done from the t-grid loads?  (n equal, same buffers, same QSUR methods)
+static bool merge_ok(const fcx_engine *e) {
+  if (e->n[0] != e->n[1] || e->n[0] != e->n[2]) return false;
+  for (int s = 1; s <= e->T; ++s) {
+    if (e->method[FCX_SPEC_VAPOR_SURFACE_U][s - 1] != e->method[FCX_SPEC_VAPOR_SURFACE_T][s - 1] ||
+        e->method[FCX_SPEC_VAPOR_SURFACE_V][s - 1] != e->method[FCX_SPEC_VAPOR_SURFACE_T][s - 1])
+      return false;
+    for (int v : {FCX_TSUR, FCX_FICE, FCX_PSUR, FCX_UATM, FCX_VATM, FCX_QSUR})
+      for (int g = 2; g <= 3; ++g)
+        if (e->buf(s, g, v) >= 0 && e->buf(s, g, v) != e->buf(s, 1, v)) return false;
+    for (int v : {FCX_AMOM, FCX_CMOM})
+      if (e->buf(s, 3, v) != e->buf(s, 2, v)) return false;
+  }
+  return true;
+}
+
+static int build_plan(fcx_engine *e, uint32_t stages, int avg_phases, Plan &pl) {
+  Params &P = pl.host;
+  std::memset(&P, 0, sizeof P);
+  std::set<int> reads, writes;
+  for (int g = 0; g < 3; ++g) P.n[g] = e->n[g];
+  P.num_types = e->T;
+  P.stages = stages;
+  const bool uv_stages = stages & (S_QSUR_U | S_QSUR_V | S_UMOM | S_VMOM);
+  P.merged_uv = uv_stages && merge_ok(e);
+  int64_t n_max = 0;
+  if (stages & (S_RBBR | S_QSUR_T | S_MEVA | S_HLAT | S_HSEN | S_RSDR)) n_max = e->n[0];
+  if (stages & (S_QSUR_U | S_UMOM)) n_max = std::max(n_max, e->n[1]);
+  if (stages & (S_QSUR_V | S_VMOM)) n_max = std::max(n_max, e->n[2]);
+
+  auto in = [&](int s, int g, int var) -> const double * {
+    const int b = e->buf(s, g, var);
+    if (b < 0) return nullptr;
+    reads.insert(b);
+    return e->bufs[b].dev;
+  };
+  auto out = [&](int s, int g, int var) -> double * {
+    const int b = e->buf(s, g, var);
+    if (b < 0) return nullptr;
+    writes.insert(b);
+    return e->bufs[b].dev;
+  };
+
+  for (int s = 1; s <= e->T; ++s) {
+    TypeParams &tp = P.type[s - 1];
+    for (int k = 0; k < 3; ++k) tp.m_qsur[k] = e->method[FCX_SPEC_VAPOR_SURFACE_T + k][s - 1];
+    tp.m_meva = e->method[FCX_FLUX_MASS_EVAP][s - 1];
+    tp.m_hlat = e->method[FCX_FLUX_HEAT_LATENT][s - 1];
+    tp.m_hsen = e->method[FCX_FLUX_HEAT_SENSIBLE][s - 1];
+    tp.m_mom = e->method[FCX_FLUX_MOMENTUM][s - 1];
+    tp.m_rbbr = e->method[FCX_FLUX_RADIATION_BLACKBODY][s - 1];
+    TGridPtrs &t = tp.t;
+    bool ts = false, fi = false, ps = false, pa = false, qa = false, ta = false, uv = false,
+         amoi = false, cmoi = false, chea = false, q_needed = false, me_needed = false;
+    const bool q_in_reg = (stages & S_QSUR_T) && tp.m_qsur[0] == FCX_CCLM;
+    if (stages & S_RBBR) {
+      if (tp.m_rbbr == FCX_STBO) ts = true;
+      if (tp.m_rbbr == FCX_STBO || tp.m_rbbr == FCX_ZERO) t.rbbr = out(s, 1, FCX_RBBR);
+    }
+    if (q_in_reg) {
+      fi = ps = ts = true;
+      t.qsur = out(s, 1, FCX_QSUR);
+    }
+    const bool me_in_reg = (stages & S_MEVA) && is_compute(tp.m_meva);
+    if (stages & S_MEVA) {
+      const int m = tp.m_meva;
+      if (m == FCX_CCLM || m == FCX_MOM5) {
+        (m == FCX_CCLM ? amoi : cmoi) = true;
+        ps = qa = ta = uv = q_needed = true;
+      } else if (m == FCX_RCO) {
+        qa = ts = uv = true;
+      }
+      if (is_compute(m)) {
+        t.meva = out(s, 1, FCX_MEVA);
+        tp.bias_adds = e->lcorr ? 1 : 0;
+      }
+    }
+    if ((stages & S_HLAT) && (tp.m_hlat == FCX_WATER || tp.m_hlat == FCX_ICE || tp.m_hlat == FCX_ZERO)) {
+      t.hlat = out(s, 1, FCX_HLAT);
+      if (tp.m_hlat != FCX_ZERO) me_needed = true;
+    }
+    if (stages & S_HSEN) {
+      const int m = tp.m_hsen;
+      if (m == FCX_CCLM || m == FCX_MOM5) {
+        (m == FCX_CCLM ? amoi : chea) = true;
+        pa = ps = qa = ta = ts = uv = true;
+      } else if (m == FCX_RCO) {
+        ta = ts = uv = true;
+      }
+      if (is_compute(m)) t.hsen = out(s, 1, FCX_HSEN);
+    }
+    if ((stages & S_RSDR) && e->buf(0, 1, FCX_RSDD) >= 0) {
+      bool all = true;
+      for (int i = 1; i <= e->T; ++i) all = all && e->buf(i, 1, FCX_RSDR) >= 0;
+      if (all) {
+        t.rsdr = out(s, 1, FCX_RSDR);
+        P.rsdd0 = in(0, 1, FCX_RSDD);
+      }
+    }
+    // u / v grids
+    bool mq[2] = {false, false}, mm[2] = {false, false};
+    for (int k = 0; k < 2; ++k) {
+      const int g = 2 + k;
+      UVGridPtrs &gp = tp.uv[k];
+      const uint32_t s_q = k == 0 ? S_QSUR_U : S_QSUR_V, s_m = k == 0 ? S_UMOM : S_VMOM;
+      mq[k] = (stages & s_q) && tp.m_qsur[1 + k] == FCX_CCLM;
+      mm[k] = (stages & s_m) && is_compute(tp.m_mom);
+      const bool cclm = tp.m_mom == FCX_CCLM || tp.m_mom == FCX_MOM5;
+      if (mq[k]) gp.qsur = out(s, g, FCX_QSUR);
+      if (mm[k]) gp.mom = out(s, g, k == 0 ? FCX_UMOM : FCX_VMOM);
+      if (P.merged_uv) {
+        if (mq[k]) {
+          fi = ps = ts = true;
+          if (gp.qsur == t.qsur && t.qsur) gp.qsur = nullptr;  // same buffer: stored once
+        }
+        if (mm[k] && tp.m_mom != FCX_ZERO) {
+          uv = true;
+          if (cclm) {
+            ps = ts = q_needed = true;
+            if (tp.m_mom == FCX_CCLM) gp.amom = in(s, g, FCX_AMOM);
+            else gp.cmom = in(s, g, FCX_CMOM);
+          }
+        }
+      } else {
+        if (mq[k]) {
+          gp.fice = in(s, g, FCX_FICE);
+          gp.psur = in(s, g, FCX_PSUR);
+          gp.tsur = in(s, g, FCX_TSUR);
+        }
+        if (mm[k] && tp.m_mom != FCX_ZERO) {
+          gp.uatm = in(s, g, FCX_UATM);
+          gp.vatm = in(s, g, FCX_VATM);
+          if (cclm) {
+            gp.psur = in(s, g, FCX_PSUR);
+            gp.tsur = in(s, g, FCX_TSUR);
+            if (tp.m_mom == FCX_CCLM) gp.amom = in(s, g, FCX_AMOM);
+            else gp.cmom = in(s, g, FCX_CMOM);
+            if (!mq[k]) gp.qsur_in = in(s, g, FCX_QSUR);
+          }
+        }
+      }
+    }
+    // merged: a momentum stage whose QSUR is not produced in this launch reads QSUR(t)
+    const bool q_reg_any = q_in_reg || (P.merged_uv && (mq[0] || mq[1]));
+    if (q_needed && !q_reg_any) t.qsur_in = in(s, 1, FCX_QSUR);
+    if (q_needed && q_reg_any && !q_in_reg && (stages & S_MEVA) && is_compute(tp.m_meva) &&
+        (tp.m_meva == FCX_CCLM || tp.m_meva == FCX_MOM5)) {
+      // MEVA runs before QSUR(u/v) in the reference: it must see QSUR(t) as stored
+      t.qsur_in = in(s, 1, FCX_QSUR);
+    }
+    if (me_needed && !me_in_reg) t.meva_in = in(s, 1, FCX_MEVA);
+    if (ts) t.tsur = in(s, 1, FCX_TSUR);
+    if (fi) t.fice = in(s, 1, FCX_FICE);
+    if (ps) t.psur = in(s, 1, FCX_PSUR);
+    if (pa) t.patm = in(s, 1, FCX_PATM);
+    if (qa) t.qatm = in(s, 1, FCX_QATM);
+    if (ta) t.tatm = in(s, 1, FCX_TATM);
+    if (uv) {
+      t.uatm = in(s, 1, FCX_UATM);
+      t.vatm = in(s, 1, FCX_VATM);
+    }
+    if (amoi) t.amoi = in(s, 1, FCX_AMOI);
+    if (cmoi) t.cmoi = in(s, 1, FCX_CMOI);
+    if (chea) t.chea = in(s, 1, FCX_CHEA);
+  }
+  // bias: a 'copy' type adds corr once more to the aliased type-1 array (calc:112-116),
+  // which in flux-major order happens before any HLAT reads it
+  if (stages & S_MEVA && e->lcorr)
+    for (int s = 2; s <= e->T; ++s)
+      if (e->method[FCX_FLUX_MASS_EVAP][s - 1] == FCX_COPY) P.type[0].bias_adds++;
+
+  // type-0 averages
+  if (stages & S_AVG) {
+    std::vector<std::pair<int, int>> list;
+    if (avg_phases >= 1000) {  // explicit average_across_surface_types(g, var) call
+      const int g = (avg_phases - 1000) / 100, var = (avg_phases - 1000) % 100;
+      if (e->allocated[0][g - 1][var0(var)]) list.push_back({g, var});  // calc:376
+    } else {
+      for (auto &a : e->averages)
+        if ((a.first & avg_phases) && average_applies(e, a.second.first, a.second.second))
+          list.push_back(a.second);
+    }
+    for (auto &a : list) {
+      const int g = a.first, var = a.second;
+      if (P.num_avg >= kMaxAvg) return fail(FCX_E_UNSUPPORTED, "more than %d averaged outputs", kMaxAvg);
+      AvgEntry &ae = P.avg[P.num_avg++];
+      ae.grid = g - 1;
+      ae.x0 = out(0, g, var);
+      for (int s = 1; s <= e->T; ++s) {
+        if (e->buf(s, g, var) < 0 || e->buf(s, g, FCX_FARE) < 0)
+          return fail(FCX_E_MISSING, "average of %s: surface type %d lacks %s or FARE",
+                      kVarNames[var0(var)], s, kVarNames[var0(var)]);
+        // values produced in this launch are re-read by the same thread (in order)
+        ae.x[s - 1] = e->dptr(s, g, var);
+        if (!writes.count(e->buf(s, g, var))) reads.insert(e->buf(s, g, var));
+        ae.fare[s - 1] = in(s, g, FCX_FARE);
+      }
+      n_max = std::max(n_max, e->n[g - 1]);
+    }
+  }
+  P.n_max = n_max;
+  pl.reads.assign(reads.begin(), reads.end());
+  pl.writes.assign(writes.begin(), writes.end());
+  // buffers that are both read and written in the launch are produced there: not inputs
+  std::vector<int> pure;
+  for (int b : pl.reads)
+    if (!writes.count(b)) pure.push_back(b);
+  pl.reads.swap(pure);
+  HIP_TRY(hipMalloc(&pl.dev, sizeof(Params)));
+  HIP_TRY(hipMemcpy(pl.dev, &P, sizeof(Params), hipMemcpyHostToDevice));
+  return FCX_OK;
+}
+
+static int get_plan(fcx_engine *e, uint32_t stages, int avg_phases, Plan **pl) {
+  auto key = std::make_pair(stages, avg_phases);
+  auto it = e->plans.find(key);
+  if (it == e->plans.end()) {
+    Plan p;
+    if (int r = build_plan(e, stages, avg_phases, p)) return r;
+    it = e->plans.emplace(key, p).first;
+  }
+  *pl = &it->second;
+  return FCX_OK;
+}
+
+extern "C" int fcx_commit(fcx_engine *e) {
+  if (!e) return fail(FCX_E_ARG, "NULL engine");
+  if (e->committed) return FCX_OK;
+  HIP_TRY(hipSetDevice(e->device));
+  if (int r = validate(e)) return r;
+  // one pooled allocation for all host-bound mirrors, 256-B aligned sub-buffers
+  size_t total = 0;
+  std::vector<size_t> off(e->bufs.size(), 0);
+  for (size_t b = 0; b < e->bufs.size(); ++b) {
+    if (e->bufs[b].external) continue;
+    off[b] = total;
+    total += ((size_t)e->bufs[b].n * sizeof(double) + 255) / 256 * 256;
+  }
+  if (total) {
+    hipError_t err = hipMalloc(&e->pool, total);
+    if (err != hipSuccess)
+      return fail(FCX_E_NOMEM, "hipMalloc(%zu) for the field mirrors: %s", total, hipGetErrorString(err));
+    for (size_t b = 0; b < e->bufs.size(); ++b)
+      if (!e->bufs[b].external) e->bufs[b].dev = reinterpret_cast<double *>((char *)e->pool + off[b]);
+  }
+  if (e->lcorr) {
+    HIP_TRY(hipMalloc(&e->corr_dev, std::max<size_t>(e->corr_mm.size(), 1) * sizeof(double)));
+    HIP_TRY(hipMemcpy(e->corr_dev, e->corr_mm.data(), e->corr_mm.size() * sizeof(double),
+                      hipMemcpyHostToDevice));
+  }
+  for (auto &c : e->rg) {
+    if (!c.set) continue;
+    HIP_TRY(hipMalloc(&c.d_row, c.row_ptr.size() * sizeof(int32_t)));
+    HIP_TRY(hipMalloc(&c.d_col, std::max<size_t>(c.col.size(), 1) * sizeof(int32_t)));
+    HIP_TRY(hipMalloc(&c.d_w, std::max<size_t>(c.w.size(), 1) * sizeof(double)));
+    HIP_TRY(hipMemcpy(c.d_row, c.row_ptr.data(), c.row_ptr.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    if (!c.col.empty()) {
+      HIP_TRY(hipMemcpy(c.d_col, c.col.data(), c.col.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+      HIP_TRY(hipMemcpy(c.d_w, c.w.data(), c.w.size() * sizeof(double), hipMemcpyHostToDevice));
+    }
+  }
+  e->committed = true;
+  return FCX_OK;
+}
+
+// ------------------------------------------------------------------ execution
+
+static const uint32_t kEarly = S_RBBR;
+static const uint32_t kNormal = S_QSUR_T | S_QSUR_U | S_QSUR_V | S_MEVA | S_HLAT | S_HSEN | S_UMOM |
+                                S_VMOM | S_RSDR;
+
+static int check(fcx_engine *e) {
+  if (!e) return fail(FCX_E_ARG, "NULL engine");
+  if (!e->committed) return fail(FCX_E_STATE, "fcx_commit has not been called");
+  return FCX_OK;
+}
+
+static const double *month_slice(fcx_engine *e, int32_t t, int *rc) {
+  *rc = FCX_OK;
+  if (!e->lcorr) return nullptr;
+  int32_t m = 0;
+  if ((*rc = fcx_current_month(e->init_date, t, &m)) != FCX_OK) return nullptr;
+  return e->corr_dev + (size_t)(m - 1) * e->n[0];
+}
+
+static int copy_bufs(fcx_engine *e, const std::vector<int> &ids, bool h2d) {
+  for (int b : ids) {
+    const Buffer &bf = e->bufs[b];
+    if (bf.external || bf.n == 0) continue;
+    if (h2d)
+      HIP_TRY(hipMemcpyAsync(bf.dev, bf.host, bf.n * sizeof(double), hipMemcpyHostToDevice, e->stream));
+    else
+      HIP_TRY(hipMemcpyAsync(bf.host, bf.dev, bf.n * sizeof(double), hipMemcpyDeviceToHost, e->stream));
+  }
+  return FCX_OK;
+}
+
+static int launch_plan(fcx_engine *e, Plan *pl, const double *corr_m) {
+  if (pl->host.n_max <= 0) return FCX_OK;
+  const int cpt = e->aligned16 ? 2 : 1;
+  const int r = launch_cells(&pl->host, pl->dev, corr_m, cpt, e->stream);
+  if (r) return fail(FCX_E_HIP, "cells_kernel launch: %s", hipGetErrorString((hipError_t)r));
+  return FCX_OK;
+}
+
+static int regrid_var(fcx_engine *e, int var, int surface_type);
+
+// the reference step order with do_regridding after each calc (flux_calculator.F90:972-991)
+static int staged_sequence(int phase, std::vector<std::pair<uint32_t, int>> &seq) {
+  if (phase & FCX_PHASE_EARLY) seq.push_back({S_RBBR, FCX_RBBR});
+  if (phase & FCX_PHASE_NORMAL) {
+    seq.push_back({S_QSUR_T | S_QSUR_U | S_QSUR_V, FCX_QSUR});
+    seq.push_back({S_MEVA, FCX_MEVA});
+    seq.push_back({S_HLAT, FCX_HLAT});
+    seq.push_back({S_HSEN, FCX_HSEN});
+    seq.push_back({S_UMOM, FCX_UMOM});
+    seq.push_back({S_VMOM, FCX_VMOM});
+    seq.push_back({S_RSDR, 0});
+  }
+  return FCX_OK;
+}
+
+static uint32_t phase_stages(int phase) {
+  uint32_t st = S_AVG;
+  if (phase & FCX_PHASE_EARLY) st |= kEarly;
+  if (phase & FCX_PHASE_NORMAL) st |= kNormal;
+  return st;
+}
+
+extern "C" int fcx_upload(fcx_engine *e, int phase) {
+  if (int r = check(e)) return r;
+  if (phase < 1 || phase > 3) return fail(FCX_E_ARG, "phase %d unknown", phase);
+  Plan *pl;
+  if (int r = get_plan(e, phase_stages(phase), phase, &pl)) return r;
+  return copy_bufs(e, pl->reads, true);
+}
+
+extern "C" int fcx_download(fcx_engine *e, int phase) {
+  if (int r = check(e)) return r;
+  if (phase < 1 || phase > 3) return fail(FCX_E_ARG, "phase %d unknown", phase);
+  Plan *pl;
+  if (int r = get_plan(e, phase_stages(phase), phase, &pl)) return r;
+  if (int r = copy_bufs(e, pl->writes, false)) return r;
+  if (e->any_regrid) {  // device-side regrid destinations of the fields this phase computes
+    std::vector<int> extra;
+    std::vector<int> vars;
+    if (phase & FCX_PHASE_EARLY) vars = {FCX_RBBR};
+    if (phase & FCX_PHASE_NORMAL)
+      for (int v : {FCX_QSUR, FCX_MEVA, FCX_HLAT, FCX_HSEN, FCX_UMOM, FCX_VMOM}) vars.push_back(v);
+    for (int s = 1; s <= e->T; ++s)
+      for (int g = 1; g <= 3; ++g)
+        for (int v : vars)
+          if (e->put_to[s][g - 1][v - 1])
+            for (int k = 0; k < 3; ++k)
+              if ((e->put_to[s][g - 1][v - 1] >> k) & 1)
+                if (e->buf(s, k + 1, v) >= 0) extra.push_back(e->buf(s, k + 1, v));
+    std::sort(extra.begin(), extra.end());
+    extra.erase(std::unique(extra.begin(), extra.end()), extra.end());
+    if (int r = copy_bufs(e, extra, false)) return r;
+  }
+  return FCX_OK;
+}
+
+extern "C" int fcx_run(fcx_engine *e, int phase, int32_t t) {
+  if (int r = check(e)) return r;
+  if (phase < 1 || phase > 3) return fail(FCX_E_ARG, "phase %d unknown", phase);
+  int rc;
+  const double *corr_m = month_slice(e, t, &rc);
+  if (rc) return rc;
+  HIP_TRY(hipEventRecord(e->ev0, e->stream));
+  if (!e->any_regrid) {
+    Plan *pl;
+    if (int r = get_plan(e, phase_stages(phase), phase, &pl)) return r;
+    if (int r = launch_plan(e, pl, corr_m)) return r;
+  } else {
+    std::vector<std::pair<uint32_t, int>> seq;
+    staged_sequence(phase, seq);
+    for (auto &st : seq) {
+      Plan *pl;
+      if (int r = get_plan(e, st.first, 0, &pl)) return r;
+      if (int r = launch_plan(e, pl, corr_m)) return r;
+      if (st.second)
+        if (int r = regrid_var(e, st.second, 0)) return r;
+    }
+    Plan *pl;
+    if (int r = get_plan(e, S_AVG, phase, &pl)) return r;
+    if (int r = launch_plan(e, pl, nullptr)) return r;
+  }
+  HIP_TRY(hipEventRecord(e->ev1, e->stream));
+  e->timed = true;
+  return FCX_OK;
+}
+
+extern "C" int fcx_step(fcx_engine *e, int phase, int32_t t) {
+  if (int r = fcx_upload(e, phase)) return r;
+  if (int r = fcx_run(e, phase, t)) return r;
+  if (int r = fcx_download(e, phase)) return r;
+  return fcx_synchronize(e);
+}
+
+extern "C" int fcx_synchronize(fcx_engine *e) {
+  if (!e) return fail(FCX_E_ARG, "NULL engine");
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  return FCX_OK;
+}
+
+// one reference subroutine: upload what it reads, run, download what it writes
+static int per_call(fcx_engine *e, uint32_t stages, int avg_phases, int32_t t) {
+  if (int r = check(e)) return r;
+  Plan *pl;
+  if (int r = get_plan(e, stages, avg_phases, &pl)) return r;
+  int rc;
+  const double *corr_m = (stages & S_MEVA) ? month_slice(e, t, &rc) : nullptr;
+  if ((stages & S_MEVA) && rc) return rc;
+  if (int r = copy_bufs(e, pl->reads, true)) return r;
+  HIP_TRY(hipEventRecord(e->ev0, e->stream));
+  if (int r = launch_plan(e, pl, corr_m)) return r;
+  HIP_TRY(hipEventRecord(e->ev1, e->stream));
+  e->timed = true;
+  if (int r = copy_bufs(e, pl->writes, false)) return r;
+  return fcx_synchronize(e);
+}
+
+extern "C" int fcx_calc_spec_vapor_surface(fcx_engine *e, int g) {
+  if (g < 1 || g > 3) return fail(FCX_E_ARG, "which_grid %d", g);
+  return per_call(e, g == 1 ? S_QSUR_T : g == 2 ? S_QSUR_U : S_QSUR_V, 0, 0);
+}
+extern "C" int fcx_calc_flux_mass_evap(fcx_engine *e, int32_t t) { return per_call(e, S_MEVA, 0, t); }
+extern "C" int fcx_calc_flux_heat_latent(fcx_engine *e) { return per_call(e, S_HLAT, 0, 0); }
+extern "C" int fcx_calc_flux_heat_sensible(fcx_engine *e) { return per_call(e, S_HSEN, 0, 0); }
+extern "C" int fcx_calc_flux_momentum_east(fcx_engine *e, int g) {
+  if (g != 2) return fail(FCX_E_UNSUPPORTED, "eastward momentum is computed on the u grid (2), got %d", g);
+  return per_call(e, S_UMOM, 0, 0);
+}
+extern "C" int fcx_calc_flux_momentum_north(fcx_engine *e, int g) {
+  if (g != 3) return fail(FCX_E_UNSUPPORTED, "northward momentum is computed on the v grid (3), got %d", g);
+  return per_call(e, S_VMOM, 0, 0);
+}
+extern "C" int fcx_calc_flux_radiation_blackbody(fcx_engine *e) { return per_call(e, S_RBBR, 0, 0); }
+extern "C" int fcx_distribute_shortwave_radiation_flux(fcx_engine *e) { return per_call(e, S_RSDR, 0, 0); }
+
+extern "C" int fcx_average_across_surface_types(fcx_engine *e, int g, int var) {
+  if (g < 1 || g > 3 || var < 1 || var > kNumVars) return fail(FCX_E_ARG, "bad average arguments");
+  return per_call(e, S_AVG, 1000 + 100 * g + var, 0);
+}
+
+// basic:463-522 on the device buffers (dst zeroed, CSR rows in link order)
+static int regrid_var(fcx_engine *e, int var, int surface_type) {
+  static const int from_g[4] = {2, 3, 1, 1}, to_g[4] = {1, 1, 2, 3}, bit[4] = {1, 1, 2, 4};
+  for (int s = 1; s <= kMaxTypes; ++s) {
+    if (!(s == surface_type || surface_type == 0)) continue;
+    for (int k = 0; k < 4; ++k) {
+      if (!(e->put_to[s][from_g[k] - 1][var0(var)] & bit[k])) continue;
+      const Csr &c = e->rg[k];
+      double *dst = e->dptr(s, to_g[k], var);
+      const double *src = e->dptr(s, from_g[k], var);
+      if (!dst || !src) return fail(FCX_E_MISSING, "regridding %s: source or destination unbound", kVarNames[var0(var)]);
+      if (!c.set) {
+        int r = launch_zero(dst, e->n[to_g[k] - 1], e->stream);
+        if (r) return fail(FCX_E_HIP, "zero: %s", hipGetErrorString((hipError_t)r));
+        continue;
+      }
+      int r = launch_regrid_csr(c.d_row, c.d_col, c.d_w, src, dst, c.n_dst, e->stream);
+      if (r) return fail(FCX_E_HIP, "regrid: %s", hipGetErrorString((hipError_t)r));
+    }
+  }
+  return FCX_OK;
+}
+
+extern "C" int fcx_do_regridding(fcx_engine *e, int var, int surface_type) {
+  if (int r = check(e)) return r;
+  if (var < 1 || var > kNumVars || surface_type < 0 || surface_type > kMaxTypes)
+    return fail(FCX_E_ARG, "bad regridding arguments");
+  static const int from_g[4] = {2, 3, 1, 1}, to_g[4] = {1, 1, 2, 3}, bit[4] = {1, 1, 2, 4};
+  std::vector<int> src, dst;
+  for (int s = 1; s <= kMaxTypes; ++s) {
+    if (!(s == surface_type || surface_type == 0)) continue;
+    for (int k = 0; k < 4; ++k)
+      if (e->put_to[s][from_g[k] - 1][var0(var)] & bit[k]) {
+        src.push_back(e->buf(s, from_g[k], var));
+        dst.push_back(e->buf(s, to_g[k], var));
+      }
+  }
+  if (src.empty()) return FCX_OK;
+  for (int b : src)
+    if (b < 0) return fail(FCX_E_MISSING, "regridding %s: source unbound", kVarNames[var0(var)]);
+  for (int b : dst)
+    if (b < 0) return fail(FCX_E_MISSING, "regridding %s: destination unbound", kVarNames[var0(var)]);
+  if (int r = copy_bufs(e, src, true)) return r;
+  if (int r = regrid_var(e, var, surface_type)) return r;
+  if (int r = copy_bufs(e, dst, false)) return r;
+  return fcx_synchronize(e);
+}
+
+// ------------------------------------------------------------------ queries
+
+extern "C" int fcx_device_ptr(fcx_engine *e, int s, int g, int var, double **dptr) {
+  if (int r = check(e)) return r;
+  if (!dptr || s < 0 || s > kMaxTypes || g < 1 || g > 3 || var < 1 || var > kNumVars)
+    return fail(FCX_E_ARG, "bad arguments");
+  *dptr = e->dptr(s, g, var);
+  return FCX_OK;
+}
+
+extern "C" int fcx_last_kernel_ms(fcx_engine *e, float *ms) {
+  if (!e || !ms) return fail(FCX_E_ARG, "NULL argument");
+  if (!e->timed) return fail(FCX_E_STATE, "no run recorded");
+  HIP_TRY(hipEventSynchronize(e->ev1));
+  HIP_TRY(hipEventElapsedTime(ms, e->ev0, e->ev1));
+  return FCX_OK;
+}
+
+extern "C" int fcx_algorithmic_bytes(fcx_engine *e, int phase, int64_t *bytes) {
+  if (int r = check(e)) return r;
+  if (!bytes || phase < 1 || phase > 3) return fail(FCX_E_ARG, "bad arguments");
+  Plan *pl;
+  if (int r = get_plan(e, phase_stages(phase), phase, &pl)) return r;
+  int64_t b = 0;
+  for (int id : pl->reads) b += e->bufs[id].n;
+  for (int id : pl->writes) b += e->bufs[id].n;
+  if (e->lcorr && (phase & FCX_PHASE_NORMAL)) b += e->n[0];
+  *bytes = b * (int64_t)sizeof(double);
+  return FCX_OK;
+}

@@ -1,0 +1,76 @@
+// fcx_internal.h -- engine <-> kernel contract (device parameter block) of libfcx.
+#pragma once
+#include <cstdint>
+#include "../../include/fcx.h"
+
+namespace fcx {
+
+constexpr int kMaxTypes = FCX_MAX_SURFACE_TYPES;
+constexpr int kNumVars = FCX_NUM_VARS;
+constexpr int kMaxAvg = 24;
+
+// Stage bits of one launch, in the reference call order (flux_calculator.F90:902-991).
+enum Stage : uint32_t {
+  S_RBBR = 1u << 0,    // calc_flux_radiation_blackbody          (early phase)
+  S_QSUR_T = 1u << 1,  // calc_spec_vapor_surface(t)
+  S_QSUR_U = 1u << 2,  // calc_spec_vapor_surface(u)
+  S_QSUR_V = 1u << 3,  // calc_spec_vapor_surface(v)
+  S_MEVA = 1u << 4,    // calc_flux_mass_evap (+ bias)
+  S_HLAT = 1u << 5,    // calc_flux_heat_latent
+  S_HSEN = 1u << 6,    // calc_flux_heat_sensible
+  S_UMOM = 1u << 7,    // calc_flux_momentum_east  (u grid)
+  S_VMOM = 1u << 8,    // calc_flux_momentum_north (v grid)
+  S_RSDR = 1u << 9,    // distribute_shortwave_radiation_flux
+  S_AVG = 1u << 10,    // average_across_surface_types of the registered type-0 outputs
+};
+
+// Per surface type, per launch.  A nullptr input means "not needed by this launch"; a
+// nullptr output means "not stored" (method none/copy, or stage not in this launch).
+struct TGridPtrs {
+  const double *tsur, *fice, *psur, *patm, *qatm, *tatm, *uatm, *vatm;
+  const double *amoi, *cmoi, *chea;
+  const double *qsur_in;  // QSUR(s,t) when not produced in-register (none/copy/not run)
+  const double *meva_in;  // MEVA(s,t) when MEVA is not produced in this launch
+  double *qsur, *meva, *hlat, *hsen, *rbbr, *rsdr;
+};
+struct UVGridPtrs {
+  const double *tsur, *fice, *psur, *uatm, *vatm, *amom, *cmom;
+  const double *qsur_in;
+  double *qsur, *mom;  // mom = UMOM on the u grid, VMOM on the v grid
+};
+struct TypeParams {
+  TGridPtrs t;
+  UVGridPtrs uv[2];
+  int8_t m_qsur[3], m_meva, m_hlat, m_hsen, m_mom, m_rbbr;
+  int8_t bias_adds;  // how many times corr(month) is added to MEVA (1 + #'copy' aliases)
+  int8_t pad[7];
+};
+// type-0 average: X0 = sum_{s=1..T} X_s * FARE_s, in order (calc:376-383)
+struct AvgEntry {
+  double *x0;
+  int32_t grid;  // 0,1,2
+  int32_t pad;
+  const double *x[kMaxTypes];
+  const double *fare[kMaxTypes];
+};
+struct Params {
+  int64_t n[3];          // cells per grid
+  int64_t n_max;         // max of the grids in this launch
+  int32_t num_types;
+  uint32_t stages;
+  const double *rsdd0;   // RSDD of type 0 (t grid), for S_RSDR
+  int32_t merged_uv;     // u/v grids are the t grid (same buffers, same sizes)
+  int32_t num_avg;
+  TypeParams type[kMaxTypes];
+  AvgEntry avg[kMaxAvg];
+};
+
+// launchers (fcx_kernels.hip); return hipError_t as int
+// corr_m: month slice [n_t] of the bias corrections (device), or nullptr
+int launch_cells(const Params *host_params, const Params *dev_params, const double *corr_m,
+                 int cells_per_thread, void *stream);
+int launch_regrid_csr(const int32_t *row_ptr, const int32_t *col, const double *w,
+                      const double *src, double *dst, int64_t n_dst, void *stream);
+int launch_zero(double *x, int64_t n, void *stream);
+
+}  // namespace fcx

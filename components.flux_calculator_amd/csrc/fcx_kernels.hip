@@ -1,0 +1,352 @@
+// fcx_kernels.hip -- CDNA4 (gfx950) kernels of the exchange-grid flux engine.
+//
+// cells_kernel: ONE fused pass over the exchange-grid cells for every flux of a coupling
+// step (flux_calculator.F90:902-991): RBBR, QSUR(t,u,v), MEVA(+bias), HLAT, HSEN, UMOM,
+// VMOM, RSDR and the type-0 averages.  The reference makes one pass over memory per flux
+// and per surface type (7+ passes, one scalar call per cell); here every input array is
+// read once and every output written once, so the kernel is HBM-bandwidth bound
+// (arithmetic intensity ~1.5-2 flop/B, well below the fp64-vector/HBM ridge).
+//
+// Layout: struct-of-arrays, one contiguous fp64 array per (surface type, grid, var) --
+// exactly the reference data model (flux_calculator_basic.F90:86-103), so a wave reads
+// 64 x 16 B = 1 KiB per array per load instruction (two cells per lane, dwordx4).
+// Method dispatch (namelist which_* strings, calc:37-48 etc.) is a per-type int8 read
+// from the parameter block: wave-uniform, so it is a scalar branch and costs no
+// divergence.  Surface types are processed type-major per cell; every cross-type effect
+// the reference's flux-major order has (the 'copy' aliases, the bias added once more per
+// aliased copy, calc:112-116) is resolved by the planner in fcx_engine.hip.
+#include <hip/hip_runtime.h>
+#include "fcx_internal.h"
+#include "fcx_physics.h"
+
+#pragma clang fp contract(off)
+
+namespace fcx {
+
+template <int C>
+struct Vec {
+  double v[C];
+};
+
+template <int C>
+__device__ __forceinline__ Vec<C> ld(const double *__restrict__ p, int64_t j0, int64_t n) {
+  Vec<C> r;
+  if constexpr (C == 2) {
+    if (j0 + 2 <= n) {
+      const double2 t = *reinterpret_cast<const double2 *>(p + j0);
+      r.v[0] = t.x;
+      r.v[1] = t.y;
+      return r;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < C; ++i) r.v[i] = (j0 + i < n) ? p[j0 + i] : 1.0;
+  return r;
+}
+
+template <int C>
+__device__ __forceinline__ void st(double *__restrict__ p, int64_t j0, int64_t n, const Vec<C> &x) {
+  if constexpr (C == 2) {
+    if (j0 + 2 <= n) {
+      *reinterpret_cast<double2 *>(p + j0) = make_double2(x.v[0], x.v[1]);
+      return;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < C; ++i)
+    if (j0 + i < n) p[j0 + i] = x.v[i];
+}
+
+template <int C>
+__device__ __forceinline__ Vec<C> splat(double a) {
+  Vec<C> r;
+#pragma unroll
+  for (int i = 0; i < C; ++i) r.v[i] = a;
+  return r;
+}
+
+#define FOR_C _Pragma("unroll") for (int i = 0; i < C; ++i)
+
+// Momentum of one (type, u- or v-grid) cell group; `north` selects VMOM.
+template <int C>
+__device__ __forceinline__ void momentum(int8_t m, bool north, const UVGridPtrs &g,
+                                         const Vec<C> &ts, const Vec<C> &ps, const Vec<C> &u,
+                                         const Vec<C> &v, const Vec<C> &vel, const Vec<C> &qs,
+                                         const Vec<C> &a, int64_t j0, int64_t n) {
+  if (!g.mom) return;
+  Vec<C> out;
+  if (m == FCX_ZERO) {
+    out = splat<C>(0.0);
+  } else if (m == FCX_CCLM || m == FCX_MOM5) {
+    FOR_C {
+      const double rate = mom_cclm_rate(a.v[i], ps.v[i], qs.v[i], ts.v[i], vel.v[i]);
+      out.v[i] = -(rate * (north ? v.v[i] : u.v[i]));
+    }
+  } else if (m == FCX_RCO) {
+    FOR_C {
+      const double rate = mom_rco_rate(vel.v[i]);
+      out.v[i] = -(rate * (north ? v.v[i] : u.v[i]));
+    }
+  } else {
+    return;
+  }
+  st<C>(g.mom, j0, n, out);
+}
+
+// QSUR + momentum on one separate u or v grid (non-merged layout).
+template <int C>
+__device__ __forceinline__ void uv_grid(const TypeParams &tp, int k, uint32_t stages, int64_t j0,
+                                        int64_t n) {
+  const UVGridPtrs &g = tp.uv[k];
+  const uint32_t s_qsur = k == 0 ? S_QSUR_U : S_QSUR_V;
+  const uint32_t s_mom = k == 0 ? S_UMOM : S_VMOM;
+  const bool do_q = (stages & s_qsur) && tp.m_qsur[1 + k] == FCX_CCLM && g.qsur;
+  const bool do_m = (stages & s_mom) && g.mom;
+  if (!do_q && !do_m) return;
+  Vec<C> ts = {}, fi = {}, ps = {}, u = {}, v = {}, a = {}, qs = {};
+  if (g.tsur) ts = ld<C>(g.tsur, j0, n);
+  if (g.psur) ps = ld<C>(g.psur, j0, n);
+  if (do_q) fi = ld<C>(g.fice, j0, n);
+  if (do_m) {
+    u = ld<C>(g.uatm, j0, n);
+    v = ld<C>(g.vatm, j0, n);
+    if (tp.m_mom == FCX_CCLM) a = ld<C>(g.amom, j0, n);
+    if (tp.m_mom == FCX_MOM5) a = ld<C>(g.cmom, j0, n);
+    if (g.qsur_in && !do_q) qs = ld<C>(g.qsur_in, j0, n);
+  }
+  if (do_q) {
+    FOR_C qs.v[i] = qsur_cclm(fi.v[i], ps.v[i], ts.v[i]);
+    st<C>(g.qsur, j0, n, qs);
+  }
+  if (do_m) {
+    Vec<C> vel;
+    FOR_C vel.v[i] = wind(u.v[i], v.v[i]);
+    momentum<C>(tp.m_mom, k == 1, g, ts, ps, u, v, vel, qs, a, j0, n);
+  }
+}
+
+template <int C, bool MERGED>
+__device__ __forceinline__ void process(const Params *__restrict__ P, const double *__restrict__ corr_m,
+                                        int64_t j0) {
+  const uint32_t stages = P->stages;
+  const int T = P->num_types;
+  const int64_t nt = P->n[0];
+  const bool do_t = j0 < nt;
+  Vec<C> corr = {};
+  if (do_t && corr_m && (stages & S_MEVA)) corr = ld<C>(corr_m, j0, nt);
+  Vec<C> rsdd = {};
+  if (do_t && P->rsdd0 && (stages & S_RSDR)) rsdd = ld<C>(P->rsdd0, j0, nt);
+
+  for (int s = 0; s < T; ++s) {
+    const TypeParams &tp = P->type[s];
+    const TGridPtrs &g = tp.t;
+    if (do_t) {
+      // ---- load every t-grid input this type needs (before any store of this type)
+      Vec<C> ts = {}, fi = {}, ps = {}, pa = {}, qa = {}, ta = {}, u = {}, v = {}, amoi = {},
+             cmoi = {}, chea = {}, qs = {}, me = {};
+      if (g.tsur) ts = ld<C>(g.tsur, j0, nt);
+      if (g.fice) fi = ld<C>(g.fice, j0, nt);
+      if (g.psur) ps = ld<C>(g.psur, j0, nt);
+      if (g.patm) pa = ld<C>(g.patm, j0, nt);
+      if (g.qatm) qa = ld<C>(g.qatm, j0, nt);
+      if (g.tatm) ta = ld<C>(g.tatm, j0, nt);
+      if (g.uatm) u = ld<C>(g.uatm, j0, nt);
+      if (g.vatm) v = ld<C>(g.vatm, j0, nt);
+      if (g.amoi) amoi = ld<C>(g.amoi, j0, nt);
+      if (g.cmoi) cmoi = ld<C>(g.cmoi, j0, nt);
+      if (g.chea) chea = ld<C>(g.chea, j0, nt);
+      if (g.qsur_in) qs = ld<C>(g.qsur_in, j0, nt);
+      if (g.meva_in) me = ld<C>(g.meva_in, j0, nt);
+      Vec<C> amom = {}, cmom = {};
+      if constexpr (MERGED) {
+        const UVGridPtrs &gu = tp.uv[0];
+        if (gu.amom) amom = ld<C>(gu.amom, j0, nt);
+        if (gu.cmom) cmom = ld<C>(gu.cmom, j0, nt);
+      }
+      Vec<C> vel;
+      FOR_C vel.v[i] = wind(u.v[i], v.v[i]);
+
+      // ---- calc_flux_radiation_blackbody (calc:331-343)
+      if ((stages & S_RBBR) && g.rbbr) {
+        Vec<C> r;
+        if (tp.m_rbbr == FCX_STBO) {
+          FOR_C r.v[i] = rbbr_stbo(ts.v[i]);
+          st<C>(g.rbbr, j0, nt, r);
+        } else if (tp.m_rbbr == FCX_ZERO) {
+          st<C>(g.rbbr, j0, nt, splat<C>(0.0));
+        }
+      }
+      // ---- calc_spec_vapor_surface(t) (calc:37-49)
+      if ((stages & S_QSUR_T) && tp.m_qsur[0] == FCX_CCLM) {
+        FOR_C qs.v[i] = qsur_cclm(fi.v[i], ps.v[i], ts.v[i]);
+        if (g.qsur) st<C>(g.qsur, j0, nt, qs);
+      }
+      // ---- calc_flux_mass_evap (calc:75-118), P2: TATM in the T_s slot
+      if (stages & S_MEVA) {
+        const int8_t m = tp.m_meva;
+        bool have = true;
+        if (m == FCX_ZERO) {
+          me = splat<C>(0.0);
+        } else if (m == FCX_CCLM || m == FCX_MOM5) {
+          const Vec<C> &a = (m == FCX_CCLM) ? amoi : cmoi;
+          FOR_C me.v[i] = meva_cclm(a.v[i], ps.v[i], qa.v[i], qs.v[i], ta.v[i], vel.v[i]);
+        } else if (m == FCX_RCO) {
+          FOR_C me.v[i] = meva_rco(qa.v[i], ts.v[i], vel.v[i]);
+        } else {
+          have = false;  // none / copy
+        }
+        if (have) {
+          for (int b = 0; b < tp.bias_adds; ++b) {
+            FOR_C me.v[i] = me.v[i] + corr.v[i];
+          }
+          if (g.meva) st<C>(g.meva, j0, nt, me);
+        }
+      }
+      // ---- calc_flux_heat_latent (calc:135-152)
+      if ((stages & S_HLAT) && g.hlat) {
+        Vec<C> h;
+        if (tp.m_hlat == FCX_WATER) {
+          FOR_C h.v[i] = me.v[i] * kLv;
+          st<C>(g.hlat, j0, nt, h);
+        } else if (tp.m_hlat == FCX_ICE) {
+          FOR_C h.v[i] = me.v[i] * kLs;
+          st<C>(g.hlat, j0, nt, h);
+        } else if (tp.m_hlat == FCX_ZERO) {
+          st<C>(g.hlat, j0, nt, splat<C>(0.0));
+        }
+      }
+      // ---- calc_flux_heat_sensible (calc:167-206), P3: QATM in the q_s slot
+      if ((stages & S_HSEN) && g.hsen) {
+        const int8_t m = tp.m_hsen;
+        Vec<C> h;
+        if (m == FCX_CCLM || m == FCX_MOM5) {
+          const Vec<C> &a = (m == FCX_CCLM) ? amoi : chea;
+          FOR_C h.v[i] = hsen_cclm(a.v[i], pa.v[i], ps.v[i], qa.v[i], ta.v[i], ts.v[i], vel.v[i]);
+          st<C>(g.hsen, j0, nt, h);
+        } else if (m == FCX_RCO) {
+          FOR_C h.v[i] = hsen_rco(ta.v[i], ts.v[i], vel.v[i]);
+          st<C>(g.hsen, j0, nt, h);
+        } else if (m == FCX_ZERO) {
+          st<C>(g.hsen, j0, nt, splat<C>(0.0));
+        }
+      }
+      if constexpr (MERGED) {
+        // u and v grids ARE the t grid: QSUR(u/v) = QSUR(t) (same inputs, same method),
+        // one wind speed and one exchange rate serve UMOM and VMOM.
+        for (int k = 0; k < 2; ++k) {
+          const UVGridPtrs &gk = tp.uv[k];
+          const uint32_t s_qsur = k == 0 ? S_QSUR_U : S_QSUR_V;
+          if ((stages & s_qsur) && tp.m_qsur[1 + k] == FCX_CCLM && gk.qsur) {
+            if (!((stages & S_QSUR_T) && tp.m_qsur[0] == FCX_CCLM)) {
+              FOR_C qs.v[i] = qsur_cclm(fi.v[i], ps.v[i], ts.v[i]);
+            }
+            st<C>(gk.qsur, j0, nt, qs);
+          }
+        }
+        const bool do_u = (stages & S_UMOM) && tp.uv[0].mom;
+        const bool do_v = (stages & S_VMOM) && tp.uv[1].mom;
+        if (do_u || do_v) {
+          const Vec<C> &a = (tp.m_mom == FCX_MOM5) ? cmom : amom;
+          if (do_u) momentum<C>(tp.m_mom, false, tp.uv[0], ts, ps, u, v, vel, qs, a, j0, nt);
+          if (do_v) momentum<C>(tp.m_mom, true, tp.uv[1], ts, ps, u, v, vel, qs, a, j0, nt);
+        }
+      }
+      // ---- distribute_shortwave_radiation_flux (calc:355-362): RSDR_s = RSDD_0
+      if ((stages & S_RSDR) && g.rsdr) st<C>(g.rsdr, j0, nt, rsdd);
+    }
+    if constexpr (!MERGED) {
+      if (j0 < P->n[1]) uv_grid<C>(tp, 0, stages, j0, P->n[1]);
+      if (j0 < P->n[2]) uv_grid<C>(tp, 1, stages, j0, P->n[2]);
+    }
+  }
+
+  // ---- average_across_surface_types (calc:376-383), summed in type order
+  if (stages & S_AVG) {
+    for (int e = 0; e < P->num_avg; ++e) {
+      const AvgEntry &ae = P->avg[e];
+      const int64_t n = P->n[ae.grid];
+      if (j0 >= n) continue;
+      Vec<C> acc = splat<C>(0.0);
+      for (int s = 0; s < T; ++s) {
+        const Vec<C> x = ld<C>(ae.x[s], j0, n);
+        const Vec<C> f = ld<C>(ae.fare[s], j0, n);
+        FOR_C acc.v[i] = acc.v[i] + x.v[i] * f.v[i];
+      }
+      st<C>(ae.x0, j0, n, acc);
+    }
+  }
+}
+
+template <int C, bool MERGED>
+__global__ __launch_bounds__(256) void cells_kernel(const Params *__restrict__ P,
+                                                    const double *__restrict__ corr_m) {
+  const int64_t units = (P->n_max + C - 1) / C;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u < units; u += stride)
+    process<C, MERGED>(P, corr_m, u * C);
+}
+
+// do_regridding (basic:463-522) as CSR-by-destination: row d holds the links with
+// dst_index == d in their original link order, so the sequential sum from 0.0 reproduces
+// the reference's scatter-add order exactly (bit-identical) without atomics.
+__global__ __launch_bounds__(256) void regrid_csr_kernel(const int32_t *__restrict__ row_ptr,
+                                                         const int32_t *__restrict__ col,
+                                                         const double *__restrict__ w,
+                                                         const double *__restrict__ src,
+                                                         double *__restrict__ dst, int64_t n_dst) {
+  const int64_t d = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (d >= n_dst) return;
+  double acc = 0.0;
+  for (int32_t k = row_ptr[d]; k < row_ptr[d + 1]; ++k) acc = acc + src[col[k]] * w[k];
+  dst[d] = acc;
+}
+
+__global__ void zero_kernel(double *x, int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += stride) x[j] = 0.0;
+}
+
+static int grid_for(int64_t units) {
+  // memory-bound grid-stride: enough waves to fill 256 CUs x 8 blocks, capped
+  int64_t blocks = (units + 255) / 256;
+  if (blocks > 256 * 8) blocks = 256 * 8;
+  if (blocks < 1) blocks = 1;
+  return (int)blocks;
+}
+
+int launch_cells(const Params *hp, const Params *dp, const double *corr_m, int cells_per_thread,
+                 void *stream) {
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int64_t units = (hp->n_max + cells_per_thread - 1) / cells_per_thread;
+  const int blocks = grid_for(units);
+  if (cells_per_thread == 2) {
+    if (hp->merged_uv)
+      hipLaunchKernelGGL((cells_kernel<2, true>), dim3(blocks), dim3(256), 0, s, dp, corr_m);
+    else
+      hipLaunchKernelGGL((cells_kernel<2, false>), dim3(blocks), dim3(256), 0, s, dp, corr_m);
+  } else {
+    if (hp->merged_uv)
+      hipLaunchKernelGGL((cells_kernel<1, true>), dim3(blocks), dim3(256), 0, s, dp, corr_m);
+    else
+      hipLaunchKernelGGL((cells_kernel<1, false>), dim3(blocks), dim3(256), 0, s, dp, corr_m);
+  }
+  return (int)hipGetLastError();
+}
+
+int launch_regrid_csr(const int32_t *row_ptr, const int32_t *col, const double *w,
+                      const double *src, double *dst, int64_t n_dst, void *stream) {
+  if (n_dst <= 0) return 0;
+  const int blocks = (int)((n_dst + 255) / 256);
+  hipLaunchKernelGGL(regrid_csr_kernel, dim3(blocks), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), row_ptr, col, w, src, dst, n_dst);
+  return (int)hipGetLastError();
+}
+
+int launch_zero(double *x, int64_t n, void *stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(zero_kernel, dim3(grid_for(n)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), x, n);
+  return (int)hipGetLastError();
+}
+
+}  // namespace fcx

@@ -1,0 +1,90 @@
+"""ctypes binding of libfcx.so (include/fcx.h).
+
+The product path is the HIP library: loading fails loudly (FcxError) when it has not been
+built; there is no CPU fallback anywhere in this package.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.normpath(os.path.join(_HERE, "..", "..", "lib", "libfcx.so"))
+
+FCX_OK = 0
+FCX_MEM_HOST = 0x0
+FCX_MEM_DEVICE = 0x1
+FCX_ALLOCATED = 0x2
+FCX_CORR_CELL_MAJOR = 0
+FCX_CORR_MONTH_MAJOR = 1
+
+# every symbol declared in include/fcx.h: (name, restype, argtypes)
+_c = ctypes
+_P = _c.c_void_p
+_I = _c.c_int
+_I32 = _c.c_int32
+_I64 = _c.c_int64
+_DP = _c.POINTER(_c.c_double)
+SIGNATURES = [
+    ("fcx_last_error", _c.c_char_p, []),
+    ("fcx_version", _I, []),
+    ("fcx_method_from_string", _I, [_c.c_char_p, _c.c_size_t]),
+    ("fcx_current_month", _I, [_I32, _I64, _c.POINTER(_I32)]),
+    ("fcx_create", _I, [_I, _I, _c.POINTER(_I32), _c.POINTER(_P)]),
+    ("fcx_destroy", _I, [_P]),
+    ("fcx_set_stream", _I, [_P, _P]),
+    ("fcx_set_method", _I, [_P, _I, _I, _I]),
+    ("fcx_bind_field", _I, [_P, _I, _I, _I, _P, _I64, _I]),
+    ("fcx_set_corrections", _I, [_P, _I, _I32, _P, _I64, _I]),
+    ("fcx_set_regrid_matrix", _I, [_P, _I, _I64, _P, _P, _P]),
+    ("fcx_set_put_to", _I, [_P, _I, _I, _I, _I]),
+    ("fcx_add_average", _I, [_P, _I, _I, _I]),
+    ("fcx_commit", _I, [_P]),
+    ("fcx_upload", _I, [_P, _I]),
+    ("fcx_run", _I, [_P, _I, _I32]),
+    ("fcx_download", _I, [_P, _I]),
+    ("fcx_step", _I, [_P, _I, _I32]),
+    ("fcx_synchronize", _I, [_P]),
+    ("fcx_calc_spec_vapor_surface", _I, [_P, _I]),
+    ("fcx_calc_flux_mass_evap", _I, [_P, _I32]),
+    ("fcx_calc_flux_heat_latent", _I, [_P]),
+    ("fcx_calc_flux_heat_sensible", _I, [_P]),
+    ("fcx_calc_flux_momentum_east", _I, [_P, _I]),
+    ("fcx_calc_flux_momentum_north", _I, [_P, _I]),
+    ("fcx_calc_flux_radiation_blackbody", _I, [_P]),
+    ("fcx_distribute_shortwave_radiation_flux", _I, [_P]),
+    ("fcx_average_across_surface_types", _I, [_P, _I, _I]),
+    ("fcx_do_regridding", _I, [_P, _I, _I]),
+    ("fcx_device_ptr", _I, [_P, _I, _I, _I, _c.POINTER(_DP)]),
+    ("fcx_last_kernel_ms", _I, [_P, _c.POINTER(_c.c_float)]),
+    ("fcx_algorithmic_bytes", _I, [_P, _I, _c.POINTER(_I64)]),
+]
+
+
+class FcxError(RuntimeError):
+    """Non-zero status of a libfcx entry point (message from fcx_last_error)."""
+
+    def __init__(self, status, message):
+        super().__init__(f"fcx status {status}: {message}")
+        self.status = status
+
+
+_lib = None
+
+
+def load():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise FcxError(-1, f"{LIB_PATH} is not built (run __graft_entry__.build())")
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, res, args in SIGNATURES:
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+    return _lib
+
+
+def check(status):
+    if status != FCX_OK:
+        raise FcxError(status, load().fcx_last_error().decode(errors="replace"))
+    return status

@@ -1,0 +1,121 @@
+"""Engine: one libfcx engine bound to a LocalFields (one rank, one GPU)."""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from .basic import FLUX_ID, IDX, METHOD_ID, PHASE_ALL, PHASE_EARLY, PHASE_NORMAL
+from .local_field import LocalFields, data_ptr, is_device
+
+
+class Engine:
+    """Binds every slot of a LocalFields to a new libfcx engine and commits it.
+
+    methods: {which_table_name: [method string per surface type 1..T]}
+    corrections: None or (init_date, array) with array shaped like the Fortran
+        corrections(1, 12, grid_size(1)) -> numpy [n][12] (cell-major) or [12][n].
+    averages: iterable of (phase, grid, name) type-0 outputs averaged before their put.
+    """
+
+    def __init__(self, lf: LocalFields, num_surface_types, methods, corrections=None,
+                 averages=(), regrid=None, device=0, stream=None):
+        self.lib = _lib.load()
+        self.lf = lf
+        self.T = int(num_surface_types)
+        self.methods = {k: list(v) for k, v in methods.items()}
+        self._keep = []
+        h = ctypes.c_void_p()
+        gs = (ctypes.c_int32 * 3)(*lf.grid_size)
+        _lib.check(self.lib.fcx_create(device, self.T, gs, ctypes.byref(h)))
+        self.h = h
+        try:
+            if stream is not None:
+                _lib.check(self.lib.fcx_set_stream(h, ctypes.c_void_p(stream)))
+            for table, per_type in self.methods.items():
+                for s, m in enumerate(per_type[: self.T], start=1):
+                    mid = METHOD_ID[m.rstrip()] if isinstance(m, str) else int(m)
+                    _lib.check(self.lib.fcx_set_method(h, FLUX_ID[table], s, mid))
+            for s, g, var, a, alloc in lf.slots():
+                flags = (_lib.FCX_MEM_DEVICE if is_device(a) else _lib.FCX_MEM_HOST)
+                if alloc:
+                    flags |= _lib.FCX_ALLOCATED
+                n = a.shape[0]
+                _lib.check(self.lib.fcx_bind_field(h, s, g, var, ctypes.c_void_p(data_ptr(a)), n, flags))
+            if corrections is not None:
+                init_date, corr = corrections
+                corr = np.ascontiguousarray(corr, dtype=np.float64)
+                layout = _lib.FCX_CORR_CELL_MAJOR if corr.shape[-1] == 12 else _lib.FCX_CORR_MONTH_MAJOR
+                self._keep.append(corr)
+                _lib.check(self.lib.fcx_set_corrections(h, 1, int(init_date), ctypes.c_void_p(corr.ctypes.data),
+                                                        lf.grid_size[0], layout))
+            if regrid:
+                for which, (src, dst, w) in regrid.get("matrices", {}).items():
+                    src = np.ascontiguousarray(src, dtype=np.int32)
+                    dst = np.ascontiguousarray(dst, dtype=np.int32)
+                    w = np.ascontiguousarray(w, dtype=np.float64)
+                    self._keep += [src, dst, w]
+                    _lib.check(self.lib.fcx_set_regrid_matrix(
+                        h, which, src.shape[0], ctypes.c_void_p(src.ctypes.data),
+                        ctypes.c_void_p(dst.ctypes.data), ctypes.c_void_p(w.ctypes.data)))
+            for (s, g, name), mask in lf.put_to.items():
+                _lib.check(self.lib.fcx_set_put_to(h, s, g, IDX[name], mask))
+            for phase, g, name in averages:
+                _lib.check(self.lib.fcx_add_average(h, phase, g, IDX[name]))
+            _lib.check(self.lib.fcx_commit(h))
+        except Exception:
+            self.lib.fcx_destroy(h)
+            self.h = None
+            raise
+
+    # ---- fused path
+    def upload(self, phase=PHASE_ALL):
+        _lib.check(self.lib.fcx_upload(self.h, phase))
+
+    def run(self, phase=PHASE_ALL, current_step_time=0):
+        _lib.check(self.lib.fcx_run(self.h, phase, int(current_step_time)))
+
+    def download(self, phase=PHASE_ALL):
+        _lib.check(self.lib.fcx_download(self.h, phase))
+
+    def step(self, phase=PHASE_ALL, current_step_time=0):
+        _lib.check(self.lib.fcx_step(self.h, phase, int(current_step_time)))
+
+    def synchronize(self):
+        _lib.check(self.lib.fcx_synchronize(self.h))
+
+    def last_kernel_ms(self):
+        ms = ctypes.c_float()
+        _lib.check(self.lib.fcx_last_kernel_ms(self.h, ctypes.byref(ms)))
+        return ms.value
+
+    def algorithmic_bytes(self, phase=PHASE_ALL):
+        b = ctypes.c_int64()
+        _lib.check(self.lib.fcx_algorithmic_bytes(self.h, phase, ctypes.byref(b)))
+        return b.value
+
+    def device_ptr(self, s, g, name):
+        p = ctypes.POINTER(ctypes.c_double)()
+        _lib.check(self.lib.fcx_device_ptr(self.h, s, g, IDX[name], ctypes.byref(p)))
+        return ctypes.cast(p, ctypes.c_void_p).value
+
+    def close(self):
+        if self.h is not None:
+            self.lib.fcx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def current_month(init_date, seconds):
+    """datetime_helpers.get_current_date(...)['current_month'] via libfcx."""
+    lib = _lib.load()
+    m = ctypes.c_int32()
+    _lib.check(lib.fcx_current_month(int(init_date), int(seconds), ctypes.byref(m)))
+    return m.value
+
+
+__all__ = ["Engine", "current_month", "PHASE_EARLY", "PHASE_NORMAL", "PHASE_ALL"]

@@ -1,0 +1,147 @@
+/*
+ * fcx.h -- C ABI of the MI355X exchange-grid flux engine (libfcx.so).
+ *
+ * This is the drop-in boundary for the per-coupling-step flux path of the IOW-ESM
+ * flux_calculator.  It replaces the compute of module flux_calculator_calculate
+ * (/root/reference/src/flux_calculator_calculate.F90) and do_regridding
+ * (flux_calculator_basic.F90:463-522); the Fortran host keeps its data model, OASIS
+ * put/get and namcouple surface.  The iso_c_binding shim that binds these entry points
+ * under the reference subroutine names is
+ * components.flux_calculator_amd/fortran/flux_calculator_calculate.F90.
+ *
+ * Plain C: integers, doubles and opaque handles only.  Every entry point returns an int
+ * status (FCX_OK == 0); on failure fcx_last_error() returns a message (thread-local).
+ * The reference calc_* never fail at run time (validation happens in
+ * flux_calculator_prepare.F90); here validation happens in fcx_commit and later calls
+ * only fail on HIP errors or misuse.  Not re-entrant per engine (one engine per rank and
+ * GPU, calls serialised by the host loop, as in the reference).
+ */
+#ifndef FCX_H
+#define FCX_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FCX_VERSION 1
+#define FCX_MAX_SURFACE_TYPES 10 /* flux_calculator_basic.F90:28 */
+#define FCX_NUM_VARS 35          /* flux_calculator_basic.F90:42 */
+
+/* Variable ids: identical to the reference idx_* values (flux_calculator_basic.F90:526-568). */
+enum fcx_var {
+  FCX_ALBE = 1, FCX_ALBA, FCX_AMOI, FCX_AMOM, FCX_FARE, FCX_FICE, FCX_PATM, FCX_PSUR,
+  FCX_QATM, FCX_TATM, FCX_TSUR, FCX_UATM, FCX_VATM, FCX_U10M, FCX_V10M,
+  FCX_CMOM, FCX_CMOI, FCX_CHEA, FCX_QSUR, FCX_HLAT, FCX_HSEN,
+  FCX_MEVA, FCX_MPRE, FCX_MRAI, FCX_MSNO,
+  FCX_RBBR, FCX_RLWD, FCX_RLWU, FCX_RSID, FCX_RSIU, FCX_RSIN, FCX_RSDD, FCX_RSDR,
+  FCX_UMOM, FCX_VMOM
+};
+
+/* which_grid: 1 = t_grid, 2 = u_grid, 3 = v_grid (flux_calculator_basic.F90:64) */
+enum fcx_grid { FCX_T_GRID = 1, FCX_U_GRID = 2, FCX_V_GRID = 3 };
+
+/* Method strings of the namelist which_* tables (flux_calculator.F90:99-107). */
+enum fcx_method {
+  FCX_NONE = 0, FCX_ZERO, FCX_COPY, FCX_CCLM, FCX_MOM5, FCX_RCO, FCX_WATER, FCX_ICE, FCX_STBO
+};
+
+/* The which_* tables, in the order of the namelist (flux_calculator.F90:99-107). */
+enum fcx_flux {
+  FCX_SPEC_VAPOR_SURFACE_T = 0, FCX_SPEC_VAPOR_SURFACE_U, FCX_SPEC_VAPOR_SURFACE_V,
+  FCX_FLUX_MASS_EVAP, FCX_FLUX_HEAT_LATENT, FCX_FLUX_HEAT_SENSIBLE, FCX_FLUX_MOMENTUM,
+  FCX_FLUX_RADIATION_BLACKBODY, FCX_NUM_FLUXES
+};
+
+/* Coupling-step phases (flux_calculator.F90:872-936 early, :942-1026 normal). */
+enum fcx_phase { FCX_PHASE_EARLY = 1, FCX_PHASE_NORMAL = 2, FCX_PHASE_ALL = 3 };
+
+/* Regridding matrices (flux_calculator.F90:330-337). */
+enum fcx_regrid { FCX_U_TO_T = 0, FCX_V_TO_T, FCX_T_TO_U, FCX_T_TO_V };
+
+enum fcx_status {
+  FCX_OK = 0, FCX_E_ARG = 1, FCX_E_STATE = 2, FCX_E_UNSUPPORTED = 3, FCX_E_HIP = 4,
+  FCX_E_MISSING = 5, FCX_E_NOMEM = 6
+};
+
+/* fcx_bind_field flags */
+#define FCX_MEM_HOST   0x0 /* ptr is a host array owned by the caller (Fortran)       */
+#define FCX_MEM_DEVICE 0x1 /* ptr is device memory owned by the caller (zero copy)     */
+#define FCX_ALLOCATED  0x2 /* realarray%allocated (basic:88): an own array, not alias */
+
+/* fcx_set_corrections layouts */
+#define FCX_CORR_CELL_MAJOR  0 /* Fortran corrections(1,12,grid_size(1)) (bias:29-30,191) */
+#define FCX_CORR_MONTH_MAJOR 1 /* [12][grid_size(1)] (the device layout)                 */
+
+typedef struct fcx_engine fcx_engine;
+
+const char *fcx_last_error(void);
+int fcx_version(void);
+
+/* trim(method)=='CCLM' etc. on a blank-padded Fortran CHARACTER(len=20); -1 if unknown */
+int fcx_method_from_string(const char *s, size_t len);
+
+/* datetime_helpers.get_current_date (pyfort/datetime_helpers.py:4-13): calendar month of
+ * init_date (YYYYMMDD) + seconds.  Replaces the Fortran->C->CPython round trip of
+ * calc:66-73. */
+int fcx_current_month(int32_t init_date, int64_t seconds, int32_t *month);
+
+/* ---- engine set-up (after flux_calculator.F90:761, when allocations are final) ---- */
+int fcx_create(int device, int num_surface_types, const int32_t grid_size[3], fcx_engine **out);
+int fcx_destroy(fcx_engine *e);
+/* hipStream_t to run on (default: a stream owned by the engine) */
+int fcx_set_stream(fcx_engine *e, void *hip_stream);
+/* methods(my_bottom_model, surface_type) of one which_* table */
+int fcx_set_method(fcx_engine *e, int flux, int surface_type, int method);
+/* local_field(surface_type, grid)%var(var)%field => ptr(1:n).  Identical pointers in
+ * several slots are aliases (basic:334-358, prepare:36-38) and share one device buffer. */
+int fcx_bind_field(fcx_engine *e, int surface_type, int grid, int var, double *ptr, int64_t n,
+                   int flags);
+/* bias_corrections: lcorrections(E_MASS_EVAP_CORRECTION), init_date, corrections(1,:,:) */
+int fcx_set_corrections(fcx_engine *e, int enabled, int32_t init_date, const double *corr,
+                        int64_t n, int layout);
+/* sparse_regridding_matrix (basic:117-122): 1-based, rank-local, offset-corrected links */
+int fcx_set_regrid_matrix(fcx_engine *e, int which, int64_t num_elements, const int32_t *src_index,
+                          const int32_t *dst_index, const double *weight);
+/* realarray%put_to_{t,u,v}_grid of (surface_type, grid, var): bit0 t, bit1 u, bit2 v */
+int fcx_set_put_to(fcx_engine *e, int surface_type, int grid, int var, int mask);
+/* register a type-0 output that is averaged before its oasis_put (flux_calculator.F90:
+ * 911-918 early, 1001-1008 normal).  Follows the P7 trigger: only applied when the type-0
+ * array is FCX_ALLOCATED and surface type 2 exists. */
+int fcx_add_average(fcx_engine *e, int phase, int grid, int var);
+/* validate (flux_calculator_prepare.F90 rules), allocate device mirrors, build plans */
+int fcx_commit(fcx_engine *e);
+
+/* ---- per coupling step: fused path ---- */
+int fcx_upload(fcx_engine *e, int phase);   /* H2D of host-bound inputs of the phase  */
+int fcx_run(fcx_engine *e, int phase, int32_t current_step_time); /* device compute  */
+int fcx_download(fcx_engine *e, int phase); /* D2H of host-bound outputs of the phase */
+int fcx_step(fcx_engine *e, int phase, int32_t current_step_time); /* the three above */
+int fcx_synchronize(fcx_engine *e);
+
+/* ---- per call: the reference subroutines one by one (exact drop-in semantics; each
+ * call uploads what it reads, computes, downloads what it writes, and synchronises) ---- */
+int fcx_calc_spec_vapor_surface(fcx_engine *e, int which_grid);            /* calc:25  */
+int fcx_calc_flux_mass_evap(fcx_engine *e, int32_t current_step_time);     /* calc:54  */
+int fcx_calc_flux_heat_latent(fcx_engine *e);                              /* calc:124 */
+int fcx_calc_flux_heat_sensible(fcx_engine *e);                            /* calc:156 */
+int fcx_calc_flux_momentum_east(fcx_engine *e, int which_grid);            /* calc:212 */
+int fcx_calc_flux_momentum_north(fcx_engine *e, int which_grid);           /* calc:265 */
+int fcx_calc_flux_radiation_blackbody(fcx_engine *e);                      /* calc:320 */
+int fcx_distribute_shortwave_radiation_flux(fcx_engine *e);                /* calc:347 */
+int fcx_average_across_surface_types(fcx_engine *e, int which_grid, int var); /* calc:368 */
+int fcx_do_regridding(fcx_engine *e, int var, int surface_type);           /* basic:463 */
+
+/* ---- device-resident use and measurement ---- */
+/* device buffer behind a slot (NULL if unbound) */
+int fcx_device_ptr(fcx_engine *e, int surface_type, int grid, int var, double **dptr);
+/* device time (hipEvents on the engine stream) of the kernels of the last fcx_run */
+int fcx_last_kernel_ms(fcx_engine *e, float *ms);
+/* algorithmic HBM bytes of one fcx_run(phase) (each distinct array read once, written once) */
+int fcx_algorithmic_bytes(fcx_engine *e, int phase, int64_t *bytes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FCX_H */

@@ -1,0 +1,168 @@
+"""ctypes access to the CPU oracles (TEST INFRASTRUCTURE ONLY).
+
+  libfco.so      oracle/fco.c, the plain-C restatement (always built by build())
+  libfco_ref.so  the reference flux_lib compiled from /root/reference + ref_harness.F90
+                 (built only where /root/reference exists; travels to the GPU box)
+
+run_case() executes one coupling step of a synthetic Case in the reference order
+(flux_calculator.F90:902-1008) on a private deep copy of the case's arrays (aliasing kept)
+and returns {(s, g, name): ndarray} for every output.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_SO = os.path.join(ROOT, "oracle", "_build", "libfco.so")
+REF_SO = os.path.join(ROOT, "oracle", "_ref", "libfco_ref.so")
+
+NV, MT = 35, 10
+c_int32, c_void_p, c_uint8 = ctypes.c_int32, ctypes.c_void_p, ctypes.c_uint8
+
+
+class FcoMatrix(ctypes.Structure):
+    _fields_ = [("num_elements", c_int32), ("pad", c_int32), ("src_index", c_void_p),
+                ("dst_index", c_void_p), ("weight", c_void_p)]
+
+
+class FcoState(ctypes.Structure):
+    _fields_ = [
+        ("num_surface_types", c_int32),
+        ("grid_size", c_int32 * 3),
+        ("method", (c_int32 * MT) * 8),
+        ("lcorrections", c_int32),
+        ("current_month", c_int32),
+        ("corrections", c_void_p),
+        ("field", ((c_void_p * NV) * 3) * (MT + 1)),
+        ("allocated", ((c_uint8 * NV) * 3) * (MT + 1)),
+        ("put_to", ((c_uint8 * NV) * 3) * (MT + 1)),
+        ("regrid", FcoMatrix * 4),
+    ]
+
+
+_libs = {}
+
+
+def load(kind="c"):
+    if kind not in _libs:
+        path = ORACLE_SO if kind == "c" else REF_SO
+        if not os.path.exists(path):
+            return None
+        lib = ctypes.CDLL(path)
+        p = "fco_" if kind == "c" else "ref_"
+        for name in ("calc_flux_mass_evap", "calc_flux_heat_latent", "calc_flux_heat_sensible",
+                     "calc_flux_radiation_blackbody", "distribute_shortwave_radiation_flux"):
+            getattr(lib, p + name).argtypes = [ctypes.POINTER(FcoState)]
+        for name in ("calc_spec_vapor_surface", "calc_flux_momentum_east", "calc_flux_momentum_north"):
+            getattr(lib, p + name).argtypes = [ctypes.POINTER(FcoState), ctypes.c_int]
+        getattr(lib, p + "average_across_surface_types").argtypes = [
+            ctypes.POINTER(FcoState), ctypes.c_int, ctypes.c_int]
+        if kind == "c":
+            lib.fco_do_regridding.argtypes = [ctypes.POINTER(FcoState), ctypes.c_int, ctypes.c_int]
+            lib.fco_current_month.argtypes = [ctypes.c_int32, ctypes.c_int64]
+            lib.fco_current_month.restype = ctypes.c_int
+            lib.fco_step_threads.argtypes = [ctypes.POINTER(FcoState), ctypes.c_int]
+            lib.fco_step.argtypes = [ctypes.POINTER(FcoState)]
+        _libs[kind] = (lib, p)
+    return _libs[kind]
+
+
+def current_month(init_date, seconds):
+    lib, _ = load("c")
+    return lib.fco_current_month(int(init_date), int(seconds))
+
+
+FLUX_ORDER = ("which_spec_vapor_surface_t", "which_spec_vapor_surface_u",
+              "which_spec_vapor_surface_v", "which_flux_mass_evap", "which_flux_heat_latent",
+              "which_flux_heat_sensible", "which_flux_momentum", "which_flux_radiation_blackbody")
+METHODS = ("none", "zero", "copy", "CCLM", "MOM5", "RCO", "water", "ice", "StBo")
+VARNAMES = (
+    "ALBE", "ALBA", "AMOI", "AMOM", "FARE", "FICE", "PATM", "PSUR", "QATM", "TATM", "TSUR", "UATM",
+    "VATM", "U10M", "V10M", "CMOM", "CMOI", "CHEA", "QSUR", "HLAT", "HSEN", "MEVA", "MPRE", "MRAI",
+    "MSNO", "RBBR", "RLWD", "RLWU", "RSID", "RSIU", "RSIN", "RSDD", "RSDR", "UMOM", "VMOM")
+IDX0 = {n: i for i, n in enumerate(VARNAMES)}
+
+
+class OracleState:
+    """A private copy of a case's LocalFields (aliasing preserved) wired into FcoState."""
+
+    def __init__(self, case, current_step_time=0):
+        self.case = case
+        self.arrays = {}
+        copies = {}
+        for key, a in case.lf.field.items():
+            a = np.asarray(a) if isinstance(a, np.ndarray) else a.detach().cpu().numpy()
+            if id(a) not in copies:
+                copies[id(a)] = np.array(a, dtype=np.float64, copy=True)
+            self.arrays[key] = copies[id(a)]
+        st = FcoState()
+        st.num_surface_types = case.num_surface_types
+        for g in range(3):
+            st.grid_size[g] = case.lf.grid_size[g]
+        for f, table in enumerate(FLUX_ORDER):
+            for s, m in enumerate(case.methods[table], start=1):
+                st.method[f][s - 1] = METHODS.index(m.rstrip())
+        for (s, g, name), a in self.arrays.items():
+            st.field[s][g - 1][IDX0[name]] = a.ctypes.data
+            st.allocated[s][g - 1][IDX0[name]] = 1 if (s, g, name) in case.lf.allocated else 0
+        for (s, g, name), mask in case.lf.put_to.items():
+            st.put_to[s][g - 1][IDX0[name]] = mask
+        self._keep = []
+        if case.regrid:
+            for which, (src, dst, w) in case.regrid.get("matrices", {}).items():
+                src = np.ascontiguousarray(src, dtype=np.int32)
+                dst = np.ascontiguousarray(dst, dtype=np.int32)
+                w = np.ascontiguousarray(w, dtype=np.float64)
+                self._keep += [src, dst, w]
+                st.regrid[which].num_elements = src.shape[0]
+                st.regrid[which].src_index = src.ctypes.data
+                st.regrid[which].dst_index = dst.ctypes.data
+                st.regrid[which].weight = w.ctypes.data
+        if case.corrections is not None:
+            init_date, corr = case.corrections
+            corr = np.ascontiguousarray(corr, dtype=np.float64)
+            self._keep.append(corr)
+            st.lcorrections = 1
+            st.corrections = corr.ctypes.data
+            st.current_month = current_month(init_date, current_step_time)
+        self.st = st
+
+    def outputs(self):
+        return {k: self.arrays[k].copy() for k in self.case.outputs}
+
+
+def run_case(case, kind="c", current_step_time=0, phases=(1, 2), regrid=False):
+    """One coupling step in the order of flux_calculator.F90:902-1008 on an oracle."""
+    lib, p = load(kind)
+    o = OracleState(case, current_step_time)
+    sp = ctypes.byref(o.st)
+    fn = lambda name: getattr(lib, p + name)  # noqa: E731
+    rg = (lambda v: lib.fco_do_regridding(sp, IDX0[v], 0)) if regrid else (lambda v: None)
+
+    def averages(phase):
+        for ph, g, name in case.averages:
+            if ph == phase:
+                fn("average_across_surface_types")(sp, g, IDX0[name])
+
+    if 1 in phases:
+        fn("calc_flux_radiation_blackbody")(sp)
+        rg("RBBR")
+        averages(1)
+    if 2 in phases:
+        for g in (1, 2, 3):
+            fn("calc_spec_vapor_surface")(sp, g)
+        rg("QSUR")
+        fn("calc_flux_mass_evap")(sp)
+        rg("MEVA")
+        fn("calc_flux_heat_latent")(sp)
+        rg("HLAT")
+        fn("calc_flux_heat_sensible")(sp)
+        rg("HSEN")
+        fn("calc_flux_momentum_east")(sp, 2)
+        rg("UMOM")
+        fn("calc_flux_momentum_north")(sp, 3)
+        rg("VMOM")
+        fn("distribute_shortwave_radiation_flux")(sp)
+        averages(2)
+    return o.outputs()
