@@ -548,10 +548,10 @@ static int build_plan(fcx_engine *e, uint32_t stages, int avg_phases, Plan &pl) 
         }
         if (mm[k] && tp.m_mom != FCX_ZERO) {
           uv = true;
-          if (cclm) {
+          if (cclm) {  // merged: the kernel reads the (shared) coefficient through uv[0]
             ps = ts = q_needed = true;
-            if (tp.m_mom == FCX_CCLM) gp.amom = in(s, g, FCX_AMOM);
-            else gp.cmom = in(s, g, FCX_CMOM);
+            if (tp.m_mom == FCX_CCLM) tp.uv[0].amom = in(s, g, FCX_AMOM);
+            else tp.uv[0].cmom = in(s, g, FCX_CMOM);
           }
         }
       } else {

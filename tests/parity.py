@@ -1,0 +1,35 @@
+"""Parity metric of SURVEY.md 8d (fp64): per field
+    max_j |x - x_ref| / max(|x_ref[j]|, 1e-6 * ||x_ref||_inf)  <=  1e-10
+(mixed abs/rel, normalised per field: pure elementwise relative error is ill-posed where
+q_s - q_a or T_s - T_a*EF cancel).  Integer/index results are compared bit-exactly.
+"""
+import numpy as np
+
+FP64_TOL = 1e-10
+
+
+def mixed_error(x, ref):
+    x = np.asarray(x, dtype=np.float64)
+    ref = np.asarray(ref, dtype=np.float64)
+    if x.shape != ref.shape:
+        raise AssertionError(f"shape {x.shape} != {ref.shape}")
+    if ref.size == 0:
+        return 0.0
+    if not np.all(np.isfinite(x) == np.isfinite(ref)):
+        return np.inf
+    fin = np.isfinite(ref)
+    if not fin.any():
+        return 0.0
+    scale = np.maximum(np.abs(ref[fin]), 1e-6 * np.max(np.abs(ref[fin])))
+    scale = np.where(scale == 0.0, 1.0, scale)
+    return float(np.max(np.abs(x[fin] - ref[fin]) / scale))
+
+
+def assert_parity(got: dict, ref: dict, tol=FP64_TOL, label=""):
+    worst = {}
+    for key, r in ref.items():
+        e = mixed_error(got[key], r)
+        worst[key] = e
+    bad = {k: v for k, v in worst.items() if not v <= tol}
+    assert not bad, f"{label}: fields over tolerance {tol}: {bad}"
+    return worst

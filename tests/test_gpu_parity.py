@@ -1,0 +1,208 @@
+"""GPU parity: libfcx (HIP, gfx950) against the CPU oracle on the same seeded inputs.
+
+All calls go through the C ABI (include/fcx.h) via ctypes.  Tolerance: SURVEY.md 8d,
+written in tests/parity.py (1e-10 mixed abs/rel per field, fp64).  The oracle is the C
+restatement (oracle/fco.c), itself pinned bit-exactly to the reference flux_lib by
+tests/test_oracle_golden.py.
+"""
+import numpy as np
+import pytest
+
+import oracle_lib
+from parity import assert_parity
+
+pytestmark = pytest.mark.gpu
+
+fcx = pytest.importorskip("fcx")
+from fcx.basic import PHASE_ALL, PHASE_EARLY, PHASE_NORMAL  # noqa: E402
+from fcx.engine import Engine  # noqa: E402
+from fcx.synthetic import build_case  # noqa: E402
+from fcx import flux_calculator_calculate as fcc  # noqa: E402
+
+STEP_T = 3600 * 24 * 31  # inside February of 1961: month 2 bias slice
+
+
+def engine_for(case, **kw):
+    return Engine(case.lf, case.num_surface_types, case.methods, corrections=case.corrections,
+                  averages=case.averages, regrid=case.regrid, **kw)
+
+
+def outputs(case):
+    return {k: np.array(case.lf.field[k], copy=True) for k in case.outputs}
+
+
+def fused(case, t=STEP_T, phases=(PHASE_ALL,)):
+    eng = engine_for(case)
+    for ph in phases:
+        eng.step(ph, t)
+    got = outputs(case)
+    eng.close()
+    return got
+
+
+@pytest.mark.parametrize("variant", ["CCLM", "MOM5", "RCO"])
+@pytest.mark.parametrize("bias", [False, True])
+@pytest.mark.parametrize("n", [1, 2, 3, 4097])
+def test_fused_t1(variant, bias, n):
+    case = build_case(variant, n=n, T=1, bias=bias)
+    ref = oracle_lib.run_case(case, "c", current_step_time=STEP_T)
+    assert_parity(fused(case), ref, label=case.name)
+
+
+@pytest.mark.parametrize("variant", ["CCLM", "MOM5", "RCO"])
+def test_fused_t3_averages(variant):
+    case = build_case(variant, n=3001, T=3, bias=True)
+    ref = oracle_lib.run_case(case, "c", current_step_time=STEP_T)
+    assert_parity(fused(case), ref, label=case.name)
+
+
+def test_fused_ten_surface_types():
+    case = build_case("MOM5", n=777, T=10, bias=True)
+    ref = oracle_lib.run_case(case, "c", current_step_time=STEP_T)
+    assert_parity(fused(case), ref, label=case.name)
+
+
+@pytest.mark.parametrize("variant", ["CCLM", "MOM5", "RCO"])
+def test_separate_uv_grids(variant):
+    case = build_case(variant, n=2049, T=2, bias=False, sep_grids=(2101, 1999))
+    ref = oracle_lib.run_case(case, "c", current_step_time=STEP_T)
+    assert_parity(fused(case), ref, label=case.name)
+
+
+def test_early_then_normal_phase():
+    case = build_case("CCLM", n=1500, T=3, bias=True)
+    ref = oracle_lib.run_case(case, "c", current_step_time=STEP_T)
+    assert_parity(fused(case, phases=(PHASE_EARLY, PHASE_NORMAL)), ref, label=case.name)
+
+
+@pytest.mark.parametrize("per_type", [
+    {2: dict(which_flux_mass_evap="copy", which_flux_heat_latent="water")},
+    {2: dict(which_flux_mass_evap="zero", which_flux_heat_sensible="zero",
+             which_flux_momentum="zero", which_flux_radiation_blackbody="zero")},
+    {3: dict(which_flux_mass_evap="copy", which_flux_heat_latent="copy",
+             which_flux_heat_sensible="copy", which_flux_momentum="copy",
+             which_flux_radiation_blackbody="copy", which_spec_vapor_surface_t="copy",
+             which_spec_vapor_surface_u="copy", which_spec_vapor_surface_v="copy")},
+    {1: dict(which_flux_mass_evap="RCO"), 2: dict(which_flux_heat_sensible="RCO")},
+])
+def test_method_edges(per_type):
+    """zero / copy (bias added once more per aliased copy, calc:112-116) / mixed methods."""
+    case = build_case("CCLM", n=1025, T=3, bias=True, per_type=per_type)
+    ref = oracle_lib.run_case(case, "c", current_step_time=STEP_T)
+    assert_parity(fused(case), ref, label=str(per_type))
+
+
+def test_per_call_dropin_sequence():
+    """The reference subroutines one by one (calc:25-385) through the C ABI."""
+    case = build_case("MOM5", n=2500, T=3, bias=True)
+    ref = oracle_lib.run_case(case, "c", current_step_time=STEP_T)
+    fcc.prepare(case.lf, 1, case.num_surface_types, case.methods, corrections=case.corrections)
+    m = fcc.methods_2d(case.methods)
+    T, gs, lf = case.num_surface_types, case.grid_size, case.lf
+    fcc.calc_flux_radiation_blackbody(1, T, m["which_flux_radiation_blackbody"], gs, lf)
+    for name, g in (("RBBR", 1), ("TSUR", 1)):
+        fcc.average_across_surface_types(g, name, T, gs, lf)
+    for g, tab in ((1, "which_spec_vapor_surface_t"), (2, "which_spec_vapor_surface_u"),
+                   (3, "which_spec_vapor_surface_v")):
+        fcc.calc_spec_vapor_surface(1, T, g, m[tab], gs, lf)
+    fcc.calc_flux_mass_evap(1, T, m["which_flux_mass_evap"], gs, lf, current_step_time=STEP_T)
+    fcc.calc_flux_heat_latent(1, T, m["which_flux_heat_latent"], gs, lf)
+    fcc.calc_flux_heat_sensible(1, T, m["which_flux_heat_sensible"], gs, lf)
+    fcc.calc_flux_momentum_east(1, T, 2, m["which_flux_momentum"], gs, lf)
+    fcc.calc_flux_momentum_north(1, T, 3, m["which_flux_momentum"], gs, lf)
+    fcc.distribute_shortwave_radiation_flux(1, T, gs, lf)
+    for name, g in (("MEVA", 1), ("HLAT", 1), ("HSEN", 1), ("UMOM", 2), ("VMOM", 3)):
+        fcc.average_across_surface_types(g, name, T, gs, lf)
+    got = outputs(case)
+    fcc.release(lf)
+    assert_parity(got, ref, label="per-call")
+
+
+def test_bias_month_boundary():
+    """Steps that cross a month boundary pick the right corrections slice."""
+    for t in (0, 2678399, 2678400, 3600 * 24 * 59):
+        case = build_case("CCLM", n=999, T=1, bias=True)
+        ref = oracle_lib.run_case(case, "c", current_step_time=t)
+        assert_parity(fused(case, t=t), ref, label=f"t={t}")
+
+
+def test_regridding_staged():
+    """do_regridding (basic:463-522) after each calc: QSUR t->u and MEVA t->v."""
+    rng = np.random.default_rng(7)
+    case = build_case("CCLM", n=600, T=2, bias=False, sep_grids=(550, 520))
+    nt, nu, nv = case.grid_size
+    mats = {}
+    for which, (ns, nd) in {2: (nt, nu), 3: (nt, nv)}.items():
+        nnz = 3 * nd
+        mats[which] = (rng.integers(1, ns + 1, nnz), np.repeat(np.arange(1, nd + 1), 3)[rng.permutation(nnz)],
+                       rng.uniform(0.0, 1.0, nnz))
+    case.regrid = {"matrices": mats}
+    for s in (1, 2):
+        # QSUR on u is regridded from t instead of computed; MEVA lands on v too
+        case.methods["which_spec_vapor_surface_u"][s - 1] = "none"
+        case.lf.put_to[(s, 1, "QSUR")] = 2
+        case.lf.put_to[(s, 1, "MEVA")] = 4
+        case.lf.allocate_localvar("MEVA", s, 3, value=np.nan)
+        case.outputs.append((s, 3, "MEVA"))
+    ref = oracle_lib.run_case(case, "c", current_step_time=STEP_T, regrid=True)
+    got = fused(case, phases=(PHASE_EARLY, PHASE_NORMAL))
+    assert_parity(got, ref, label="regrid")
+
+
+def test_device_resident_zero_copy():
+    """Fields bound as device memory (torch, FCX_MEM_DEVICE): no host staging."""
+    torch = pytest.importorskip("torch")
+    case_h = build_case("MOM5", n=4099, T=1, bias=True)
+    ref = oracle_lib.run_case(case_h, "c", current_step_time=STEP_T)
+    case = build_case("MOM5", n=4099, T=1, bias=True, device="cuda:0")
+    eng = engine_for(case)
+    eng.run(PHASE_ALL, STEP_T)
+    eng.synchronize()
+    got = {k: case.lf.to_numpy(*k) for k in case.outputs}
+    eng.close()
+    assert_parity(got, ref, label="device")
+    del torch
+
+
+def test_unaligned_device_pointers_use_scalar_path():
+    torch = pytest.importorskip("torch")
+    case_h = build_case("CCLM", n=1001, T=1, bias=False)
+    ref = oracle_lib.run_case(case_h, "c", current_step_time=STEP_T)
+    case = build_case("CCLM", n=1001, T=1, bias=False, device="cuda:0")
+    # shift every array by one element (8-B aligned, not 16-B)
+    shifted = {}
+    for key, a in list(case.lf.field.items()):
+        if id(a) not in shifted:
+            b = torch.empty(a.shape[0] + 1, dtype=torch.float64, device="cuda:0")[1:]
+            b.copy_(a)
+            shifted[id(a)] = b
+        case.lf.field[key] = shifted[id(a)]
+    eng = engine_for(case)
+    eng.run(PHASE_ALL, STEP_T)
+    eng.synchronize()
+    got = {k: case.lf.to_numpy(*k) for k in case.outputs}
+    eng.close()
+    assert_parity(got, ref, label="unaligned")
+
+
+def test_large_grid_sampled():
+    """10M cells (config 3 size): parity on a 20k-cell sample, all outputs finite."""
+    n = 10_000_000
+    case = build_case("CCLM", n=n, T=1, bias=True)
+    got = fused(case)
+    rng = np.random.default_rng(3)
+    idx = np.unique(np.concatenate([rng.integers(0, n, 20000), [0, 1, n - 2, n - 1]]))
+    small = build_case("CCLM", n=idx.size, T=1, bias=True)
+    # rebuild the small case from the sampled cells of the big one (aliasing kept)
+    remap = {}
+    for key, a in case.lf.field.items():
+        if id(a) not in remap:
+            remap[id(a)] = np.ascontiguousarray(a[idx])
+        small.lf.field[key] = remap[id(a)]
+    init_date, corr = case.corrections
+    small.corrections = (init_date, np.ascontiguousarray(corr[idx]))
+    ref = oracle_lib.run_case(small, "c", current_step_time=STEP_T)
+    sampled = {k: v[idx] for k, v in got.items()}
+    assert_parity(sampled, ref, label="10M sampled")
+    for k, v in got.items():
+        assert np.isfinite(v).all(), k
