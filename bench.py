@@ -1,0 +1,224 @@
+#!/usr/bin/env python3
+"""Benchmark of the exchange-grid flux path on MI355X (BASELINE.json configs[2]).
+
+Workload (per GPU): the synthetic 10M-cell exchange grid of SURVEY.md 8d, one coupling
+step = the fused flux kernel of each of the CCLM, MOM5 and RCO variants back-to-back (T=1,
+u/v grids = t grid, outputs QSUR MEVA HLAT HSEN RBBR UMOM VMOM; RCO has no QSUR).  Inputs
+are resident in HBM before the timed region.  value = exchange-grid cells processed per
+second over the whole job, one variant over N cells counting N cells.
+
+Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): one rank
+per GPU, each owns a contiguous APPLE cell range of its own 10M cells (decomp_def.F90:23-31,
+weak scaling); the flux path has no cross-rank exchange.
+
+Also reported:
+  roofline      algorithmic bytes of the dominant kernel / its mean HIP-event duration
+  cpu_baseline  the CPU oracle on a bounded sample of the same workload (rank 0, N=1 only):
+                "reference" = the reference flux_lib compiled from source (oracle/_ref),
+                "port" = the C restatement (oracle/fco.c)
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "components.flux_calculator_amd", "python"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+METRIC = "exchange-grid Mcells/s per coupling step; achieved HBM GB/s vs MI355X peak"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md chip-level parameters)
+VARIANTS = ("CCLM", "MOM5", "RCO")
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--cells", type=int, default=10_000_000, help="exchange-grid cells per GPU")
+    p.add_argument("--variants", default=",".join(VARIANTS))
+    p.add_argument("--types", type=int, default=1, help="surface types")
+    p.add_argument("--bias", action="store_true", help="monthly evaporation bias corrections")
+    p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget")
+    p.add_argument("--cpu-cells", type=int, default=1_000_000)
+    p.add_argument("--no-cpu", action="store_true")
+    return p.parse_args()
+
+
+def cpu_baseline(args, variants):
+    """Oracle timing on the host cores, single thread, bounded sample of the same workload."""
+    import oracle_lib
+    from fcx.synthetic import build_case, inputs_for_bench
+
+    kind = "reference" if oracle_lib.load("ref") is not None else "port"
+    n = args.cpu_cells
+    data = inputs_for_bench(n)
+    cases = [build_case(v, n=n, T=args.types, bias=args.bias, data=data if args.types == 1 else None)
+             for v in variants]
+    states = [oracle_lib.OracleState(c, 0) for c in cases]
+    lib_kind = "ref" if kind == "reference" else "c"
+    cells, t0, reps = 0, time.perf_counter(), 0
+    while True:
+        for st in states:
+            oracle_lib.run_state(st, lib_kind)
+            cells += n
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= args.cpu_seconds and reps >= 2:
+            break
+    return {
+        "value": cells / el / 1e6,
+        "unit": "Mcells/s",
+        "cores": 1,
+        "kind": kind,
+        "sample": f"{reps} coupling steps x {len(variants)} variants ({'+'.join(variants)}) over "
+                  f"{n} cells, T={args.types}, reference call order, {el:.1f} s on 1 thread",
+    }
+
+
+def main():
+    args = parse()
+    variants = tuple(v for v in args.variants.split(",") if v)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import torch
+    import torch.distributed as dist
+
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from fcx.basic import PHASE_ALL
+    from fcx.engine import Engine
+    from fcx.synthetic import BASE_SEED, build_case, inputs_for_bench
+
+    # this rank's APPLE range of the global grid (decomp_def.F90:23-31): weak scaling,
+    # every rank owns args.cells cells; the seed follows the global offset
+    n = args.cells
+    offset = rank * n
+    host = inputs_for_bench(n, seed=BASE_SEED + offset)
+    data = {k: torch.as_tensor(v).to(dev) for k, v in host.items()}
+    del host
+    stream = torch.cuda.current_stream(dev)
+    cases, engines = [], []
+    for v in variants:
+        c = build_case(v, n=n, T=args.types, bias=args.bias, device=dev,
+                       data=data if args.types == 1 else None)
+        e = Engine(c.lf, c.num_surface_types, c.methods, corrections=c.corrections,
+                   averages=c.averages, device=local_rank, stream=stream.cuda_stream)
+        cases.append(c)
+        engines.append(e)
+    alg_bytes = [e.algorithmic_bytes(PHASE_ALL) for e in engines]
+
+    def step(t, events=None):
+        for i, e in enumerate(engines):
+            if events is not None:
+                events[i][0].record(stream)
+            e.run(PHASE_ALL, t)
+            if events is not None:
+                events[i][1].record(stream)
+
+    for w in range(args.warmup):
+        step(w * 3600)
+    torch.cuda.synchronize()
+
+    ev = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in engines] for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(k * 3600, ev[k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = np.array([[a.elapsed_time(b) for (a, b) in row] for row in ev])  # [steps][variant]
+
+    t_max = elapsed
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t_max = float(tt.item())
+    ms_per_step = t_max / args.steps * 1e3
+    cells_per_step = n * len(variants) * world
+    value = cells_per_step * args.steps / t_max / 1e6
+
+    mean_ms = kern_ms.mean(axis=0)
+    dom = int(np.argmax(mean_ms))
+    achieved = alg_bytes[dom] / (mean_ms[dom] * 1e-3) / 1e9
+    per_variant = {
+        v: {"kernel_ms": round(float(mean_ms[i]), 4),
+            "alg_bytes": int(alg_bytes[i]),
+            "bytes_per_cell": round(alg_bytes[i] / n, 3),
+            "GBps": round(alg_bytes[i] / (mean_ms[i] * 1e-3) / 1e9, 1)}
+        for i, v in enumerate(variants)}
+    traffic = None
+    tfile = os.path.join(ROOT, "profiles", "traffic.json")
+    if os.path.exists(tfile):
+        try:
+            t = json.load(open(tfile))
+            key = f"{variants[dom]}:{n}:T{args.types}:bias{int(args.bias)}"
+            traffic = t.get(key)
+        except Exception:
+            traffic = None
+
+    out = {
+        "metric": METRIC,
+        "value": round(value, 1),
+        "unit": "Mcells/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (SURVEY.md 8d distributions, seeded PCG64)",
+        "config": {
+            "workload": "config3: synthetic exchange grid, CCLM+MOM5+RCO fused flux kernels "
+                        "back-to-back per coupling step, inputs HBM-resident",
+            "cells_per_gpu": n,
+            "cells_per_step": cells_per_step,
+            "variants": list(variants),
+            "surface_types": args.types,
+            "bias_corrections": bool(args.bias),
+            "grids": "u/v grids = t grid",
+            "parallelism": f"dp{world} (APPLE contiguous cell ranges)",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": f"cells_kernel[{variants[dom]}]",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": traffic,
+            "alg_bytes_per_launch": int(alg_bytes[dom]),
+            "mean_kernel_ms": round(float(mean_ms[dom]), 4),
+        },
+        "kernels": per_variant,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cb = cpu_baseline(args, variants)
+        out["cpu_baseline"] = cb
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    for e in engines:
+        e.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -99,6 +99,8 @@ struct fcx_engine {
   void *pool = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool timed = false;
+  bool gpu_ready = false;
+  bool user_stream = false;
 
   fcx_engine() {
     for (auto &a : slot)
@@ -166,27 +168,22 @@ extern "C" int fcx_create(int device, int num_surface_types, const int32_t grid_
     return fail(FCX_E_ARG, "num_surface_types=%d outside 1..%d", num_surface_types, kMaxTypes);
   for (int g = 0; g < 3; ++g)
     if (grid_size[g] < 0) return fail(FCX_E_ARG, "grid_size(%d)=%d < 0", g + 1, grid_size[g]);
-  HIP_TRY(hipSetDevice(device));
+  // no HIP call here: the device is touched first in fcx_commit, so that the bindings and
+  // their validation can be exercised on a host without a GPU
   auto *e = new fcx_engine();
   e->device = device;
   e->T = num_surface_types;
   for (int g = 0; g < 3; ++g) e->n[g] = grid_size[g];
-  hipError_t err = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
-  if (err != hipSuccess) {
-    delete e;
-    return fail(FCX_E_HIP, "hipStreamCreate: %s", hipGetErrorString(err));
-  }
-  e->own_stream = true;
-  if (hipEventCreate(&e->ev0) != hipSuccess || hipEventCreate(&e->ev1) != hipSuccess) {
-    delete e;
-    return fail(FCX_E_HIP, "hipEventCreate failed");
-  }
   *out = e;
   return FCX_OK;
 }
 
 extern "C" int fcx_destroy(fcx_engine *e) {
   if (!e) return FCX_OK;
+  if (!e->gpu_ready) {
+    delete e;
+    return FCX_OK;
+  }
   (void)hipSetDevice(e->device);
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   for (auto &kv : e->plans) (void)hipFree(kv.second.dev);
@@ -212,6 +209,21 @@ extern "C" int fcx_set_stream(fcx_engine *e, void *stream) {
   }
   e->stream = reinterpret_cast<hipStream_t>(stream);
   e->own_stream = false;
+  e->user_stream = true;
+  return FCX_OK;
+}
+
+// first device contact of an engine: device, stream, timing events
+static int gpu_init(fcx_engine *e) {
+  if (e->gpu_ready) return FCX_OK;
+  HIP_TRY(hipSetDevice(e->device));
+  if (!e->user_stream) {
+    HIP_TRY(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+    e->own_stream = true;
+  }
+  HIP_TRY(hipEventCreate(&e->ev0));
+  HIP_TRY(hipEventCreate(&e->ev1));
+  e->gpu_ready = true;
   return FCX_OK;
 }
 
@@ -659,8 +671,8 @@ static int get_plan(fcx_engine *e, uint32_t stages, int avg_phases, Plan **pl) {
 extern "C" int fcx_commit(fcx_engine *e) {
   if (!e) return fail(FCX_E_ARG, "NULL engine");
   if (e->committed) return FCX_OK;
-  HIP_TRY(hipSetDevice(e->device));
   if (int r = validate(e)) return r;
+  if (int r = gpu_init(e)) return r;
   // one pooled allocation for all host-bound mirrors, 256-B aligned sub-buffers
   size_t total = 0;
   std::vector<size_t> off(e->bufs.size(), 0);
@@ -953,5 +965,30 @@ extern "C" int fcx_algorithmic_bytes(fcx_engine *e, int phase, int64_t *bytes) {
   for (int id : pl->writes) b += e->bufs[id].n;
   if (e->lcorr && (phase & FCX_PHASE_NORMAL)) b += e->n[0];
   *bytes = b * (int64_t)sizeof(double);
+  return FCX_OK;
+}
+
+// ------------------------------------------------------------------ device memory
+
+extern "C" int fcx_device_malloc(int device, size_t bytes, void **ptr) {
+  if (!ptr) return fail(FCX_E_ARG, "ptr is NULL");
+  HIP_TRY(hipSetDevice(device));
+  hipError_t err = hipMalloc(ptr, bytes ? bytes : 1);
+  if (err != hipSuccess) return fail(FCX_E_NOMEM, "hipMalloc(%zu): %s", bytes, hipGetErrorString(err));
+  return FCX_OK;
+}
+
+extern "C" int fcx_device_free(void *ptr) {
+  HIP_TRY(hipFree(ptr));
+  return FCX_OK;
+}
+
+extern "C" int fcx_memcpy(void *dst, const void *src, size_t bytes, int kind) {
+  const hipMemcpyKind k = kind == 1   ? hipMemcpyHostToDevice
+                          : kind == 2 ? hipMemcpyDeviceToHost
+                          : kind == 3 ? hipMemcpyDeviceToDevice
+                                      : hipMemcpyDefault;
+  if (kind < 1 || kind > 3) return fail(FCX_E_ARG, "memcpy kind %d", kind);
+  HIP_TRY(hipMemcpy(dst, src, bytes, k));
   return FCX_OK;
 }

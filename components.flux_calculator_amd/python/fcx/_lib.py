@@ -56,6 +56,9 @@ SIGNATURES = [
     ("fcx_device_ptr", _I, [_P, _I, _I, _I, _c.POINTER(_DP)]),
     ("fcx_last_kernel_ms", _I, [_P, _c.POINTER(_c.c_float)]),
     ("fcx_algorithmic_bytes", _I, [_P, _I, _c.POINTER(_I64)]),
+    ("fcx_device_malloc", _I, [_I, _c.c_size_t, _c.POINTER(_P)]),
+    ("fcx_device_free", _I, [_P]),
+    ("fcx_memcpy", _I, [_P, _P, _c.c_size_t, _I]),
 ]
 
 
@@ -71,8 +74,17 @@ _lib = None
 
 
 def load():
+    """Load libfcx.  libfcx's DT_NEEDED is the unversioned libamdhip64.so, so it binds to the
+    HIP runtime already in the process.  PyTorch-ROCm carries its own runtime
+    (torch/lib/libamdhip64.so); when torch is installed it is imported first so that the
+    process has exactly one HIP runtime (torch's) and torch tensors, streams and events
+    can be handed to libfcx directly.  The GPU itself is not touched here."""
     global _lib
     if _lib is None:
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         if not os.path.exists(LIB_PATH):
             raise FcxError(-1, f"{LIB_PATH} is not built (run __graft_entry__.build())")
         lib = ctypes.CDLL(LIB_PATH)

@@ -141,6 +141,12 @@ int fcx_last_kernel_ms(fcx_engine *e, float *ms);
 /* algorithmic HBM bytes of one fcx_run(phase) (each distinct array read once, written once) */
 int fcx_algorithmic_bytes(fcx_engine *e, int phase, int64_t *bytes);
 
+/* device memory for hosts that keep fields resident in HBM (bind with FCX_MEM_DEVICE) */
+int fcx_device_malloc(int device, size_t bytes, void **ptr);
+int fcx_device_free(void *ptr);
+/* synchronous copy; kind: 1 host->device, 2 device->host, 3 device->device */
+int fcx_memcpy(void *dst, const void *src, size_t bytes, int kind);
+
 #ifdef __cplusplus
 }
 #endif

@@ -134,8 +134,15 @@ class OracleState:
 
 def run_case(case, kind="c", current_step_time=0, phases=(1, 2), regrid=False):
     """One coupling step in the order of flux_calculator.F90:902-1008 on an oracle."""
-    lib, p = load(kind)
     o = OracleState(case, current_step_time)
+    run_state(o, kind, phases, regrid)
+    return o.outputs()
+
+
+def run_state(o, kind="c", phases=(1, 2), regrid=False):
+    """The coupling step on an existing OracleState (its arrays are updated in place)."""
+    case = o.case
+    lib, p = load(kind)
     sp = ctypes.byref(o.st)
     fn = lambda name: getattr(lib, p + name)  # noqa: E731
     rg = (lambda v: lib.fco_do_regridding(sp, IDX0[v], 0)) if regrid else (lambda v: None)
@@ -165,4 +172,3 @@ def run_case(case, kind="c", current_step_time=0, phases=(1, 2), regrid=False):
         rg("VMOM")
         fn("distribute_shortwave_radiation_flux")(sp)
         averages(2)
-    return o.outputs()

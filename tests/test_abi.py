@@ -1,0 +1,109 @@
+"""The C ABI library: loads without a GPU, exports every symbol include/fcx.h declares,
+and its host-side logic (method strings, binding validation, regrid links) behaves like
+the reference's prepare step.  No compute call is made here."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from fcx import _lib
+from fcx.engine import Engine
+from fcx.synthetic import build_case
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "fcx.h")
+
+
+def declared_symbols():
+    text = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:const\s+char\s*\*|int)\s*(fcx_\w+)\s*\(", text, re.M)))
+
+
+def test_header_declares_entry_points():
+    syms = declared_symbols()
+    assert len(syms) >= 35
+    for must in ("fcx_create", "fcx_commit", "fcx_run", "fcx_calc_flux_mass_evap",
+                 "fcx_average_across_surface_types", "fcx_do_regridding", "fcx_last_error"):
+        assert must in syms
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _lib.load()
+    missing = [s for s in declared_symbols() if not hasattr(lib, s)]
+    assert not missing, missing
+    bound = {name for name, _, _ in _lib.SIGNATURES}
+    assert set(declared_symbols()) == bound, set(declared_symbols()) ^ bound
+
+
+def test_library_is_gfx950_only_and_unversioned_hip():
+    data = open(_lib.LIB_PATH, "rb").read()
+    assert b"gfx950" in data
+    assert b"libamdhip64.so.7\0" not in data  # DT_NEEDED rewritten (tools/unversion_needed.py)
+
+
+@pytest.mark.parametrize("s,expect", [("CCLM", 3), ("CCLM" + " " * 16, 3), ("MOM5", 4), ("RCO ", 5),
+                                      ("water", 6), ("ice", 7), ("StBo", 8), ("none", 0), ("zero", 1),
+                                      ("copy", 2), ("cclm", -1), ("", -1), ("StBo2", -1)])
+def test_method_from_string_trims_like_fortran(s, expect):
+    lib = _lib.load()
+    b = s.encode()
+    assert lib.fcx_method_from_string(b, len(b)) == expect
+
+
+def test_create_and_validate_without_gpu_missing_input():
+    """prepare_flux_mass_evap: CCLM lacking QATM -> error naming the field, before any HIP call."""
+    case = build_case("CCLM", n=64, T=1)
+    for g in (1, 2, 3):
+        case.lf.field.pop((1, g, "QATM"), None)
+        case.lf.field.pop((0, g, "QATM"), None)
+    with pytest.raises(_lib.FcxError) as ei:
+        Engine(case.lf, 1, case.methods)
+    assert ei.value.status == 5 and "QATM" in str(ei.value) and "MEVA" in str(ei.value)
+
+
+def test_unknown_method_rejected():
+    case = build_case("CCLM", n=64, T=1)
+    bad = dict(case.methods)
+    bad["which_flux_heat_latent"] = ["CCLM"]  # not a latent-heat method (prepare:139-142)
+    with pytest.raises(_lib.FcxError) as ei:
+        Engine(case.lf, 1, bad)
+    assert "HLAT" in str(ei.value)
+
+
+def test_short_array_rejected():
+    lib = _lib.load()
+    h = ctypes.c_void_p()
+    gs = (ctypes.c_int32 * 3)(100, 100, 100)
+    _lib.check(lib.fcx_create(0, 1, gs, ctypes.byref(h)))
+    a = np.zeros(50)
+    st = lib.fcx_bind_field(h, 1, 1, 11, ctypes.c_void_p(a.ctypes.data), 50, 0)
+    assert st == 1 and b"shorter than grid_size" in lib.fcx_last_error()
+    lib.fcx_destroy(h)
+
+
+def test_regrid_links_outside_local_grid_rejected():
+    """read_regridding_matrix aborts when links leave the task's range (io:183-191)."""
+    lib = _lib.load()
+    h = ctypes.c_void_p()
+    gs = (ctypes.c_int32 * 3)(10, 8, 8)
+    _lib.check(lib.fcx_create(0, 1, gs, ctypes.byref(h)))
+    src = np.array([1, 11], dtype=np.int32)  # 11 > grid_size(t)
+    dst = np.array([1, 2], dtype=np.int32)
+    w = np.ones(2)
+    st = lib.fcx_set_regrid_matrix(h, 2, 2, ctypes.c_void_p(src.ctypes.data),
+                                   ctypes.c_void_p(dst.ctypes.data), ctypes.c_void_p(w.ctypes.data))
+    assert st == 1 and b"outside the local grids" in lib.fcx_last_error()
+    lib.fcx_destroy(h)
+
+
+def test_engine_calls_before_commit_fail_cleanly():
+    lib = _lib.load()
+    h = ctypes.c_void_p()
+    gs = (ctypes.c_int32 * 3)(10, 10, 10)
+    _lib.check(lib.fcx_create(0, 1, gs, ctypes.byref(h)))
+    assert lib.fcx_run(h, 3, 0) == 2  # FCX_E_STATE
+    assert b"fcx_commit" in lib.fcx_last_error()
+    assert lib.fcx_create(0, 11, gs, ctypes.byref(h)) == 1  # > MAX_SURFACE_TYPES
+    lib.fcx_destroy(h)

@@ -206,3 +206,21 @@ def test_large_grid_sampled():
     assert_parity(sampled, ref, label="10M sampled")
     for k, v in got.items():
         assert np.isfinite(v).all(), k
+
+
+def _golden_cases():
+    import test_oracle_golden as tg
+
+    return tg.CASES
+
+
+@pytest.mark.parametrize("stem", _golden_cases())
+def test_golden_reference_outputs(stem):
+    """libfcx against the REFERENCE flux_lib's own outputs (tests/golden, 1e-10 mixed)."""
+    import test_oracle_golden as tg
+
+    case, data, spec = tg.load_case(stem)
+    ref = {(int(k.split(":")[0]), int(k.split(":")[1]), k.split(":")[2]): data[f"out:{k}"]
+           for k in spec["outputs"]}
+    got = fused(case, t=tg.MANIFEST["step_time"], phases=(PHASE_EARLY, PHASE_NORMAL))
+    assert_parity(got, ref, label=stem)
