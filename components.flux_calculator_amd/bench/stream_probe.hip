@@ -1,0 +1,116 @@
+// stream_probe.hip -- what HBM bandwidth does an R-in / W-out fp64 SoA stream reach on
+// MI355X?  Trivial arithmetic, same access pattern as the fused flux kernel (CCLM: 10 input
+// arrays, 7 output arrays).  Used to set the achievable ceiling the flux kernel is judged
+// against; not part of the product.
+//   hipcc --offload-arch=gfx950 -O3 stream_probe.hip -o stream_probe && ./stream_probe
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <vector>
+
+#define CHECK(x)                                                                           \
+  do {                                                                                     \
+    hipError_t e = (x);                                                                    \
+    if (e != hipSuccess) {                                                                 \
+      printf("%s: %s\n", #x, hipGetErrorString(e));                                        \
+      return 1;                                                                            \
+    }                                                                                      \
+  } while (0)
+
+typedef double d2 __attribute__((ext_vector_type(2)));
+
+struct Ptrs {
+  const double *in[16];
+  double *out[16];
+};
+
+template <int R, int W, int C, bool NT>
+__global__ __launch_bounds__(256) void probe(Ptrs p, long n) {
+  const long units = n / C;
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long u = (long)blockIdx.x * blockDim.x + threadIdx.x; u < units; u += stride) {
+    double acc[C];
+#pragma unroll
+    for (int i = 0; i < C; ++i) acc[i] = 0.0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if constexpr (C == 2) {
+        d2 t = NT ? __builtin_nontemporal_load(reinterpret_cast<const d2 *>(p.in[r]) + u)
+                       : reinterpret_cast<const d2 *>(p.in[r])[u];
+        acc[0] += t[0];
+        acc[1] += t[1];
+      } else if constexpr (C == 4) {
+        const d2 *q = reinterpret_cast<const d2 *>(p.in[r]) + 2 * u;
+        d2 a = NT ? __builtin_nontemporal_load(q) : q[0];
+        d2 b = NT ? __builtin_nontemporal_load(q + 1) : q[1];
+        acc[0] += a[0]; acc[1] += a[1]; acc[2] += b[0]; acc[3] += b[1];
+      } else {
+        acc[0] += NT ? __builtin_nontemporal_load(p.in[r] + u) : p.in[r][u];
+      }
+    }
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      if constexpr (C == 2) {
+        d2 t = d2{acc[0] * (w + 1), acc[1] * (w + 1)};
+        if (NT) __builtin_nontemporal_store(t, reinterpret_cast<d2 *>(p.out[w]) + u);
+        else reinterpret_cast<d2 *>(p.out[w])[u] = t;
+      } else if constexpr (C == 4) {
+        d2 *q = reinterpret_cast<d2 *>(p.out[w]) + 2 * u;
+        d2 a = d2{acc[0] * (w + 1), acc[1] * (w + 1)};
+        d2 b = d2{acc[2] * (w + 1), acc[3] * (w + 1)};
+        if (NT) { __builtin_nontemporal_store(a, q); __builtin_nontemporal_store(b, q + 1); }
+        else { q[0] = a; q[1] = b; }
+      } else {
+        if (NT) __builtin_nontemporal_store(acc[0] * (w + 1), p.out[w] + u);
+        else p.out[w][u] = acc[0] * (w + 1);
+      }
+    }
+  }
+}
+
+template <int R, int W, int C, bool NT>
+int run(const char *name, Ptrs &p, long n, int blocks) {
+  hipEvent_t a, b;
+  CHECK(hipEventCreate(&a));
+  CHECK(hipEventCreate(&b));
+  for (int i = 0; i < 3; ++i) hipLaunchKernelGGL((probe<R, W, C, NT>), dim3(blocks), dim3(256), 0, 0, p, n);
+  CHECK(hipDeviceSynchronize());
+  const int reps = 20;
+  CHECK(hipEventRecord(a));
+  for (int i = 0; i < reps; ++i) hipLaunchKernelGGL((probe<R, W, C, NT>), dim3(blocks), dim3(256), 0, 0, p, n);
+  CHECK(hipEventRecord(b));
+  CHECK(hipEventSynchronize(b));
+  float ms;
+  CHECK(hipEventElapsedTime(&ms, a, b));
+  ms /= reps;
+  const double bytes = (double)(R + W) * n * 8.0;
+  printf("%-28s R=%2d W=%2d C=%d nt=%d blocks=%6d  %8.3f ms  %7.1f GB/s\n", name, R, W, C, (int)NT,
+         blocks, ms, bytes / (ms * 1e-3) / 1e9);
+  return 0;
+}
+
+int main() {
+  const long n = 10'000'000;
+  Ptrs p;
+  for (int i = 0; i < 16; ++i) {
+    double *x;
+    CHECK(hipMalloc(&x, n * sizeof(double)));
+    CHECK(hipMemset(x, 0, n * sizeof(double)));
+    p.in[i] = x;
+    CHECK(hipMalloc(&p.out[i], n * sizeof(double)));
+  }
+  for (int blocks : {1024, 2048, 4096, 8192, 19532}) {
+    run<1, 1, 2, false>("copy", p, n, blocks);
+    run<10, 7, 2, false>("cclm-shape", p, n, blocks);
+  }
+  run<1, 1, 4, false>("copy", p, n, 2048);
+  run<10, 7, 1, false>("cclm-shape", p, n, 2048);
+  run<10, 7, 4, false>("cclm-shape", p, n, 2048);
+  run<10, 7, 2, true>("cclm-shape", p, n, 2048);
+  run<10, 7, 4, true>("cclm-shape", p, n, 2048);
+  run<11, 7, 2, false>("mom5-shape", p, n, 2048);
+  run<5, 6, 2, false>("rco-shape", p, n, 2048);
+  run<17, 0, 2, false>("read-only 17", p, n, 2048);
+  run<1, 16, 2, false>("write-heavy 1/16", p, n, 2048);
+  return 0;
+}

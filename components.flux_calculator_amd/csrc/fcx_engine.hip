@@ -67,6 +67,7 @@ struct Plan {
   Params host{};
   Params *dev = nullptr;
   std::vector<int> reads, writes;  // buffer ids
+  int variant = 0;                 // T=1 specialisation (LaunchConfig::variant)
 };
 
 int var0(int var) { return var - 1; }
@@ -101,6 +102,8 @@ struct fcx_engine {
   bool timed = false;
   bool gpu_ready = false;
   bool user_stream = false;
+  LaunchConfig launch;      // fcx_set_option
+  bool specialize = true;
 
   fcx_engine() {
     for (auto &a : slot)
@@ -651,6 +654,19 @@ static int build_plan(fcx_engine *e, uint32_t stages, int avg_phases, Plan &pl) 
   for (int b : pl.reads)
     if (!writes.count(b)) pure.push_back(b);
   pl.reads.swap(pure);
+  // T=1 hot path of a standard variant: every method of the type matches one of the
+  // compile-time method sets of cells_kernel<.., VAR>
+  pl.variant = 0;
+  if (e->T == 1 && P.merged_uv) {
+    const TypeParams &tp = P.type[0];
+    for (int v = 1; v <= 3; ++v) {
+      const int m = v == 1 ? FCX_CCLM : v == 2 ? FCX_MOM5 : FCX_RCO;
+      const int q = v == 3 ? FCX_NONE : FCX_CCLM;
+      if (tp.m_meva == m && tp.m_hsen == m && tp.m_mom == m && tp.m_qsur[0] == q &&
+          tp.m_qsur[1] == q && tp.m_qsur[2] == q)
+        pl.variant = v;
+    }
+  }
   HIP_TRY(hipMalloc(&pl.dev, sizeof(Params)));
   HIP_TRY(hipMemcpy(pl.dev, &P, sizeof(Params), hipMemcpyHostToDevice));
   return FCX_OK;
@@ -742,8 +758,11 @@ static int copy_bufs(fcx_engine *e, const std::vector<int> &ids, bool h2d) {
 
 static int launch_plan(fcx_engine *e, Plan *pl, const double *corr_m) {
   if (pl->host.n_max <= 0) return FCX_OK;
-  const int cpt = e->aligned16 ? 2 : 1;
-  const int r = launch_cells(&pl->host, pl->dev, corr_m, cpt, e->stream);
+  LaunchConfig lc = e->launch;
+  if (!e->aligned16) lc.cells_per_thread = 1;
+  lc.merged = pl->host.merged_uv != 0;
+  lc.variant = (e->specialize && lc.merged) ? pl->variant : 0;
+  const int r = launch_cells(&pl->host, pl->dev, corr_m, lc, e->stream);
   if (r) return fail(FCX_E_HIP, "cells_kernel launch: %s", hipGetErrorString((hipError_t)r));
   return FCX_OK;
 }
@@ -991,4 +1010,28 @@ extern "C" int fcx_memcpy(void *dst, const void *src, size_t bytes, int kind) {
   if (kind < 1 || kind > 3) return fail(FCX_E_ARG, "memcpy kind %d", kind);
   HIP_TRY(hipMemcpy(dst, src, bytes, k));
   return FCX_OK;
+}
+
+// ------------------------------------------------------------------ tuning
+
+extern "C" int fcx_set_option(fcx_engine *e, int option, int64_t value) {
+  if (!e) return fail(FCX_E_ARG, "NULL engine");
+  switch (option) {
+    case FCX_OPT_CELLS_PER_THREAD:
+      if (value != 1 && value != 2) return fail(FCX_E_ARG, "cells per thread must be 1 or 2");
+      e->launch.cells_per_thread = (int)value;
+      return FCX_OK;
+    case FCX_OPT_MAX_BLOCKS:
+      if (value < 0 || value > (1 << 30)) return fail(FCX_E_ARG, "max blocks %lld", (long long)value);
+      e->launch.max_blocks = (int)value;
+      return FCX_OK;
+    case FCX_OPT_NONTEMPORAL:
+      e->launch.nontemporal = value != 0;
+      return FCX_OK;
+    case FCX_OPT_SPECIALIZE:
+      e->specialize = value != 0;
+      return FCX_OK;
+    default:
+      return fail(FCX_E_ARG, "option %d unknown", option);
+  }
 }

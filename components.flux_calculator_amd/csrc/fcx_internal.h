@@ -66,9 +66,18 @@ struct Params {
 };
 
 // launchers (fcx_kernels.hip); return hipError_t as int
+// how one cells_kernel launch is instantiated
+struct LaunchConfig {
+  int cells_per_thread = 2;  // 1 or 2 (2 needs 16-B aligned arrays)
+  int max_blocks = 8192;     // grid-stride cap; 0 = one unit per thread (8192: tuned)
+  bool nontemporal = true;   // non-temporal hint on the streamed loads/stores
+  bool merged = false;       // u/v grids are the t grid
+  int variant = 0;           // 0 generic, 1 CCLM, 2 MOM5, 3 RCO (T=1 specialisations)
+};
+
 // corr_m: month slice [n_t] of the bias corrections (device), or nullptr
 int launch_cells(const Params *host_params, const Params *dev_params, const double *corr_m,
-                 int cells_per_thread, void *stream);
+                 const LaunchConfig &lc, void *stream);
 int launch_regrid_csr(const int32_t *row_ptr, const int32_t *col, const double *w,
                       const double *src, double *dst, int64_t n_dst, void *stream);
 int launch_zero(double *x, int64_t n, void *stream);

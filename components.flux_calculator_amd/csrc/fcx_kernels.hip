@@ -28,14 +28,19 @@ struct Vec {
   double v[C];
 };
 
-template <int C>
+typedef double d2 __attribute__((ext_vector_type(2)));
+
+// NT: streamed once -> non-temporal hint (the arrays are read once and written once per
+// step; the 256 MB Infinity Cache cannot hold a 10M-cell step anyway)
+template <int C, bool NT>
 __device__ __forceinline__ Vec<C> ld(const double *__restrict__ p, int64_t j0, int64_t n) {
   Vec<C> r;
   if constexpr (C == 2) {
     if (j0 + 2 <= n) {
-      const double2 t = *reinterpret_cast<const double2 *>(p + j0);
-      r.v[0] = t.x;
-      r.v[1] = t.y;
+      const d2 *q = reinterpret_cast<const d2 *>(p + j0);
+      const d2 t = NT ? __builtin_nontemporal_load(q) : *q;
+      r.v[0] = t[0];
+      r.v[1] = t[1];
       return r;
     }
   }
@@ -44,11 +49,16 @@ __device__ __forceinline__ Vec<C> ld(const double *__restrict__ p, int64_t j0, i
   return r;
 }
 
-template <int C>
+template <int C, bool NT>
 __device__ __forceinline__ void st(double *__restrict__ p, int64_t j0, int64_t n, const Vec<C> &x) {
   if constexpr (C == 2) {
     if (j0 + 2 <= n) {
-      *reinterpret_cast<double2 *>(p + j0) = make_double2(x.v[0], x.v[1]);
+      d2 *q = reinterpret_cast<d2 *>(p + j0);
+      const d2 t = {x.v[0], x.v[1]};
+      if (NT)
+        __builtin_nontemporal_store(t, q);
+      else
+        *q = t;
       return;
     }
   }
@@ -66,9 +76,11 @@ __device__ __forceinline__ Vec<C> splat(double a) {
 }
 
 #define FOR_C _Pragma("unroll") for (int i = 0; i < C; ++i)
+#define LD(p, j, n) ld<C, NT>(p, j, n)
+#define ST(p, j, n, x) st<C, NT>(p, j, n, x)
 
 // Momentum of one (type, u- or v-grid) cell group; `north` selects VMOM.
-template <int C>
+template <int C, bool NT>
 __device__ __forceinline__ void momentum(int8_t m, bool north, const UVGridPtrs &g,
                                          const Vec<C> &ts, const Vec<C> &ps, const Vec<C> &u,
                                          const Vec<C> &v, const Vec<C> &vel, const Vec<C> &qs,
@@ -90,11 +102,11 @@ __device__ __forceinline__ void momentum(int8_t m, bool north, const UVGridPtrs 
   } else {
     return;
   }
-  st<C>(g.mom, j0, n, out);
+  ST(g.mom, j0, n, out);
 }
 
 // QSUR + momentum on one separate u or v grid (non-merged layout).
-template <int C>
+template <int C, bool NT>
 __device__ __forceinline__ void uv_grid(const TypeParams &tp, int k, uint32_t stages, int64_t j0,
                                         int64_t n) {
   const UVGridPtrs &g = tp.uv[k];
@@ -104,64 +116,74 @@ __device__ __forceinline__ void uv_grid(const TypeParams &tp, int k, uint32_t st
   const bool do_m = (stages & s_mom) && g.mom;
   if (!do_q && !do_m) return;
   Vec<C> ts = {}, fi = {}, ps = {}, u = {}, v = {}, a = {}, qs = {};
-  if (g.tsur) ts = ld<C>(g.tsur, j0, n);
-  if (g.psur) ps = ld<C>(g.psur, j0, n);
-  if (do_q) fi = ld<C>(g.fice, j0, n);
+  if (g.tsur) ts = LD(g.tsur, j0, n);
+  if (g.psur) ps = LD(g.psur, j0, n);
+  if (do_q) fi = LD(g.fice, j0, n);
   if (do_m) {
-    u = ld<C>(g.uatm, j0, n);
-    v = ld<C>(g.vatm, j0, n);
-    if (tp.m_mom == FCX_CCLM) a = ld<C>(g.amom, j0, n);
-    if (tp.m_mom == FCX_MOM5) a = ld<C>(g.cmom, j0, n);
-    if (g.qsur_in && !do_q) qs = ld<C>(g.qsur_in, j0, n);
+    u = LD(g.uatm, j0, n);
+    v = LD(g.vatm, j0, n);
+    if (tp.m_mom == FCX_CCLM) a = LD(g.amom, j0, n);
+    if (tp.m_mom == FCX_MOM5) a = LD(g.cmom, j0, n);
+    if (g.qsur_in && !do_q) qs = LD(g.qsur_in, j0, n);
   }
   if (do_q) {
     FOR_C qs.v[i] = qsur_cclm(fi.v[i], ps.v[i], ts.v[i]);
-    st<C>(g.qsur, j0, n, qs);
+    ST(g.qsur, j0, n, qs);
   }
   if (do_m) {
     Vec<C> vel;
     FOR_C vel.v[i] = wind(u.v[i], v.v[i]);
-    momentum<C>(tp.m_mom, k == 1, g, ts, ps, u, v, vel, qs, a, j0, n);
+    momentum<C, NT>(tp.m_mom, k == 1, g, ts, ps, u, v, vel, qs, a, j0, n);
   }
 }
 
-template <int C, bool MERGED>
+// VAR: 0 = generic (any T, methods read from the parameter block); 1/2/3 = the T=1 hot
+// path of the CCLM / MOM5 / RCO variant with QSUR/MEVA/HSEN/momentum methods fixed at
+// compile time, so the other method paths vanish from the code and its register budget.
+template <int C, bool MERGED, int VAR, bool NT>
 __device__ __forceinline__ void process(const Params *__restrict__ P, const double *__restrict__ corr_m,
                                         int64_t j0) {
   const uint32_t stages = P->stages;
-  const int T = P->num_types;
+  const int T = VAR ? 1 : P->num_types;
   const int64_t nt = P->n[0];
   const bool do_t = j0 < nt;
   Vec<C> corr = {};
-  if (do_t && corr_m && (stages & S_MEVA)) corr = ld<C>(corr_m, j0, nt);
+  if (do_t && corr_m && (stages & S_MEVA)) corr = LD(corr_m, j0, nt);
   Vec<C> rsdd = {};
-  if (do_t && P->rsdd0 && (stages & S_RSDR)) rsdd = ld<C>(P->rsdd0, j0, nt);
+  if (do_t && P->rsdd0 && (stages & S_RSDR)) rsdd = LD(P->rsdd0, j0, nt);
 
   for (int s = 0; s < T; ++s) {
     const TypeParams &tp = P->type[s];
     const TGridPtrs &g = tp.t;
+    constexpr int8_t kVarMethod = VAR == 1 ? FCX_CCLM : VAR == 2 ? FCX_MOM5 : FCX_RCO;
+    const int8_t m_q = VAR ? (VAR == 3 ? FCX_NONE : FCX_CCLM) : tp.m_qsur[0];
+    const int8_t m_qu = VAR ? m_q : tp.m_qsur[1];
+    const int8_t m_qv = VAR ? m_q : tp.m_qsur[2];
+    const int8_t m_me = VAR ? kVarMethod : tp.m_meva;
+    const int8_t m_hs = VAR ? kVarMethod : tp.m_hsen;
+    const int8_t m_mo = VAR ? kVarMethod : tp.m_mom;
     if (do_t) {
       // ---- load every t-grid input this type needs (before any store of this type)
       Vec<C> ts = {}, fi = {}, ps = {}, pa = {}, qa = {}, ta = {}, u = {}, v = {}, amoi = {},
              cmoi = {}, chea = {}, qs = {}, me = {};
-      if (g.tsur) ts = ld<C>(g.tsur, j0, nt);
-      if (g.fice) fi = ld<C>(g.fice, j0, nt);
-      if (g.psur) ps = ld<C>(g.psur, j0, nt);
-      if (g.patm) pa = ld<C>(g.patm, j0, nt);
-      if (g.qatm) qa = ld<C>(g.qatm, j0, nt);
-      if (g.tatm) ta = ld<C>(g.tatm, j0, nt);
-      if (g.uatm) u = ld<C>(g.uatm, j0, nt);
-      if (g.vatm) v = ld<C>(g.vatm, j0, nt);
-      if (g.amoi) amoi = ld<C>(g.amoi, j0, nt);
-      if (g.cmoi) cmoi = ld<C>(g.cmoi, j0, nt);
-      if (g.chea) chea = ld<C>(g.chea, j0, nt);
-      if (g.qsur_in) qs = ld<C>(g.qsur_in, j0, nt);
-      if (g.meva_in) me = ld<C>(g.meva_in, j0, nt);
+      if (g.tsur) ts = LD(g.tsur, j0, nt);
+      if (g.fice) fi = LD(g.fice, j0, nt);
+      if (g.psur) ps = LD(g.psur, j0, nt);
+      if (g.patm) pa = LD(g.patm, j0, nt);
+      if (g.qatm) qa = LD(g.qatm, j0, nt);
+      if (g.tatm) ta = LD(g.tatm, j0, nt);
+      if (g.uatm) u = LD(g.uatm, j0, nt);
+      if (g.vatm) v = LD(g.vatm, j0, nt);
+      if (g.amoi) amoi = LD(g.amoi, j0, nt);
+      if (g.cmoi) cmoi = LD(g.cmoi, j0, nt);
+      if (g.chea) chea = LD(g.chea, j0, nt);
+      if (g.qsur_in) qs = LD(g.qsur_in, j0, nt);
+      if (g.meva_in) me = LD(g.meva_in, j0, nt);
       Vec<C> amom = {}, cmom = {};
       if constexpr (MERGED) {
         const UVGridPtrs &gu = tp.uv[0];
-        if (gu.amom) amom = ld<C>(gu.amom, j0, nt);
-        if (gu.cmom) cmom = ld<C>(gu.cmom, j0, nt);
+        if (gu.amom) amom = LD(gu.amom, j0, nt);
+        if (gu.cmom) cmom = LD(gu.cmom, j0, nt);
       }
       Vec<C> vel;
       FOR_C vel.v[i] = wind(u.v[i], v.v[i]);
@@ -171,19 +193,19 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
         Vec<C> r;
         if (tp.m_rbbr == FCX_STBO) {
           FOR_C r.v[i] = rbbr_stbo(ts.v[i]);
-          st<C>(g.rbbr, j0, nt, r);
+          ST(g.rbbr, j0, nt, r);
         } else if (tp.m_rbbr == FCX_ZERO) {
-          st<C>(g.rbbr, j0, nt, splat<C>(0.0));
+          ST(g.rbbr, j0, nt, splat<C>(0.0));
         }
       }
       // ---- calc_spec_vapor_surface(t) (calc:37-49)
-      if ((stages & S_QSUR_T) && tp.m_qsur[0] == FCX_CCLM) {
+      if ((stages & S_QSUR_T) && m_q == FCX_CCLM) {
         FOR_C qs.v[i] = qsur_cclm(fi.v[i], ps.v[i], ts.v[i]);
-        if (g.qsur) st<C>(g.qsur, j0, nt, qs);
+        if (g.qsur) ST(g.qsur, j0, nt, qs);
       }
       // ---- calc_flux_mass_evap (calc:75-118), P2: TATM in the T_s slot
       if (stages & S_MEVA) {
-        const int8_t m = tp.m_meva;
+        const int8_t m = m_me;
         bool have = true;
         if (m == FCX_ZERO) {
           me = splat<C>(0.0);
@@ -199,7 +221,7 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
           for (int b = 0; b < tp.bias_adds; ++b) {
             FOR_C me.v[i] = me.v[i] + corr.v[i];
           }
-          if (g.meva) st<C>(g.meva, j0, nt, me);
+          if (g.meva) ST(g.meva, j0, nt, me);
         }
       }
       // ---- calc_flux_heat_latent (calc:135-152)
@@ -207,27 +229,27 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
         Vec<C> h;
         if (tp.m_hlat == FCX_WATER) {
           FOR_C h.v[i] = me.v[i] * kLv;
-          st<C>(g.hlat, j0, nt, h);
+          ST(g.hlat, j0, nt, h);
         } else if (tp.m_hlat == FCX_ICE) {
           FOR_C h.v[i] = me.v[i] * kLs;
-          st<C>(g.hlat, j0, nt, h);
+          ST(g.hlat, j0, nt, h);
         } else if (tp.m_hlat == FCX_ZERO) {
-          st<C>(g.hlat, j0, nt, splat<C>(0.0));
+          ST(g.hlat, j0, nt, splat<C>(0.0));
         }
       }
       // ---- calc_flux_heat_sensible (calc:167-206), P3: QATM in the q_s slot
       if ((stages & S_HSEN) && g.hsen) {
-        const int8_t m = tp.m_hsen;
+        const int8_t m = m_hs;
         Vec<C> h;
         if (m == FCX_CCLM || m == FCX_MOM5) {
           const Vec<C> &a = (m == FCX_CCLM) ? amoi : chea;
           FOR_C h.v[i] = hsen_cclm(a.v[i], pa.v[i], ps.v[i], qa.v[i], ta.v[i], ts.v[i], vel.v[i]);
-          st<C>(g.hsen, j0, nt, h);
+          ST(g.hsen, j0, nt, h);
         } else if (m == FCX_RCO) {
           FOR_C h.v[i] = hsen_rco(ta.v[i], ts.v[i], vel.v[i]);
-          st<C>(g.hsen, j0, nt, h);
+          ST(g.hsen, j0, nt, h);
         } else if (m == FCX_ZERO) {
-          st<C>(g.hsen, j0, nt, splat<C>(0.0));
+          ST(g.hsen, j0, nt, splat<C>(0.0));
         }
       }
       if constexpr (MERGED) {
@@ -236,27 +258,27 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
         for (int k = 0; k < 2; ++k) {
           const UVGridPtrs &gk = tp.uv[k];
           const uint32_t s_qsur = k == 0 ? S_QSUR_U : S_QSUR_V;
-          if ((stages & s_qsur) && tp.m_qsur[1 + k] == FCX_CCLM && gk.qsur) {
-            if (!((stages & S_QSUR_T) && tp.m_qsur[0] == FCX_CCLM)) {
+          if ((stages & s_qsur) && (k == 0 ? m_qu : m_qv) == FCX_CCLM && gk.qsur) {
+            if (!((stages & S_QSUR_T) && m_q == FCX_CCLM)) {
               FOR_C qs.v[i] = qsur_cclm(fi.v[i], ps.v[i], ts.v[i]);
             }
-            st<C>(gk.qsur, j0, nt, qs);
+            ST(gk.qsur, j0, nt, qs);
           }
         }
         const bool do_u = (stages & S_UMOM) && tp.uv[0].mom;
         const bool do_v = (stages & S_VMOM) && tp.uv[1].mom;
         if (do_u || do_v) {
-          const Vec<C> &a = (tp.m_mom == FCX_MOM5) ? cmom : amom;
-          if (do_u) momentum<C>(tp.m_mom, false, tp.uv[0], ts, ps, u, v, vel, qs, a, j0, nt);
-          if (do_v) momentum<C>(tp.m_mom, true, tp.uv[1], ts, ps, u, v, vel, qs, a, j0, nt);
+          const Vec<C> &a = (m_mo == FCX_MOM5) ? cmom : amom;
+          if (do_u) momentum<C, NT>(m_mo, false, tp.uv[0], ts, ps, u, v, vel, qs, a, j0, nt);
+          if (do_v) momentum<C, NT>(m_mo, true, tp.uv[1], ts, ps, u, v, vel, qs, a, j0, nt);
         }
       }
       // ---- distribute_shortwave_radiation_flux (calc:355-362): RSDR_s = RSDD_0
-      if ((stages & S_RSDR) && g.rsdr) st<C>(g.rsdr, j0, nt, rsdd);
+      if ((stages & S_RSDR) && g.rsdr) ST(g.rsdr, j0, nt, rsdd);
     }
     if constexpr (!MERGED) {
-      if (j0 < P->n[1]) uv_grid<C>(tp, 0, stages, j0, P->n[1]);
-      if (j0 < P->n[2]) uv_grid<C>(tp, 1, stages, j0, P->n[2]);
+      if (j0 < P->n[1]) uv_grid<C, NT>(tp, 0, stages, j0, P->n[1]);
+      if (j0 < P->n[2]) uv_grid<C, NT>(tp, 1, stages, j0, P->n[2]);
     }
   }
 
@@ -268,22 +290,22 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
       if (j0 >= n) continue;
       Vec<C> acc = splat<C>(0.0);
       for (int s = 0; s < T; ++s) {
-        const Vec<C> x = ld<C>(ae.x[s], j0, n);
-        const Vec<C> f = ld<C>(ae.fare[s], j0, n);
+        const Vec<C> x = LD(ae.x[s], j0, n);
+        const Vec<C> f = LD(ae.fare[s], j0, n);
         FOR_C acc.v[i] = acc.v[i] + x.v[i] * f.v[i];
       }
-      st<C>(ae.x0, j0, n, acc);
+      ST(ae.x0, j0, n, acc);
     }
   }
 }
 
-template <int C, bool MERGED>
+template <int C, bool MERGED, int VAR, bool NT>
 __global__ __launch_bounds__(256) void cells_kernel(const Params *__restrict__ P,
                                                     const double *__restrict__ corr_m) {
   const int64_t units = (P->n_max + C - 1) / C;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u < units; u += stride)
-    process<C, MERGED>(P, corr_m, u * C);
+    process<C, MERGED, VAR, NT>(P, corr_m, u * C);
 }
 
 // do_regridding (basic:463-522) as CSR-by-destination: row d holds the links with
@@ -306,30 +328,52 @@ __global__ void zero_kernel(double *x, int64_t n) {
   for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += stride) x[j] = 0.0;
 }
 
-static int grid_for(int64_t units) {
-  // memory-bound grid-stride: enough waves to fill 256 CUs x 8 blocks, capped
+static int grid_for(int64_t units, int max_blocks = 256 * 8) {
+  // memory-bound grid-stride: enough waves to fill 256 CUs, capped (0 = one unit per thread)
   int64_t blocks = (units + 255) / 256;
-  if (blocks > 256 * 8) blocks = 256 * 8;
+  if (max_blocks > 0 && blocks > max_blocks) blocks = max_blocks;
   if (blocks < 1) blocks = 1;
   return (int)blocks;
 }
 
-int launch_cells(const Params *hp, const Params *dp, const double *corr_m, int cells_per_thread,
+template <int C, bool MERGED, int VAR, bool NT>
+static void launch_one(int blocks, hipStream_t s, const Params *dp, const double *corr_m) {
+  hipLaunchKernelGGL((cells_kernel<C, MERGED, VAR, NT>), dim3(blocks), dim3(256), 0, s, dp, corr_m);
+}
+
+template <int C, bool MERGED, int VAR>
+static void launch_nt(bool nt, int blocks, hipStream_t s, const Params *dp, const double *corr_m) {
+  if (nt)
+    launch_one<C, MERGED, VAR, true>(blocks, s, dp, corr_m);
+  else
+    launch_one<C, MERGED, VAR, false>(blocks, s, dp, corr_m);
+}
+
+template <int C>
+static void launch_c(const LaunchConfig &lc, int blocks, hipStream_t s, const Params *dp,
+                     const double *corr_m) {
+  if (!lc.merged) {
+    launch_nt<C, false, 0>(lc.nontemporal, blocks, s, dp, corr_m);
+    return;
+  }
+  switch (lc.variant) {
+    case 1: launch_nt<C, true, 1>(lc.nontemporal, blocks, s, dp, corr_m); break;
+    case 2: launch_nt<C, true, 2>(lc.nontemporal, blocks, s, dp, corr_m); break;
+    case 3: launch_nt<C, true, 3>(lc.nontemporal, blocks, s, dp, corr_m); break;
+    default: launch_nt<C, true, 0>(lc.nontemporal, blocks, s, dp, corr_m); break;
+  }
+}
+
+int launch_cells(const Params *hp, const Params *dp, const double *corr_m, const LaunchConfig &lc,
                  void *stream) {
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const int64_t units = (hp->n_max + cells_per_thread - 1) / cells_per_thread;
-  const int blocks = grid_for(units);
-  if (cells_per_thread == 2) {
-    if (hp->merged_uv)
-      hipLaunchKernelGGL((cells_kernel<2, true>), dim3(blocks), dim3(256), 0, s, dp, corr_m);
-    else
-      hipLaunchKernelGGL((cells_kernel<2, false>), dim3(blocks), dim3(256), 0, s, dp, corr_m);
-  } else {
-    if (hp->merged_uv)
-      hipLaunchKernelGGL((cells_kernel<1, true>), dim3(blocks), dim3(256), 0, s, dp, corr_m);
-    else
-      hipLaunchKernelGGL((cells_kernel<1, false>), dim3(blocks), dim3(256), 0, s, dp, corr_m);
-  }
+  const int c = lc.cells_per_thread == 1 ? 1 : 2;
+  const int64_t units = (hp->n_max + c - 1) / c;
+  const int blocks = grid_for(units, lc.max_blocks);
+  if (c == 2)
+    launch_c<2>(lc, blocks, s, dp, corr_m);
+  else
+    launch_c<1>(lc, blocks, s, dp, corr_m);
   return (int)hipGetLastError();
 }
 

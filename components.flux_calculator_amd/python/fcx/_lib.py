@@ -56,6 +56,7 @@ SIGNATURES = [
     ("fcx_device_ptr", _I, [_P, _I, _I, _I, _c.POINTER(_DP)]),
     ("fcx_last_kernel_ms", _I, [_P, _c.POINTER(_c.c_float)]),
     ("fcx_algorithmic_bytes", _I, [_P, _I, _c.POINTER(_I64)]),
+    ("fcx_set_option", _I, [_P, _I, _I64]),
     ("fcx_device_malloc", _I, [_I, _c.c_size_t, _c.POINTER(_P)]),
     ("fcx_device_free", _I, [_P]),
     ("fcx_memcpy", _I, [_P, _P, _c.c_size_t, _I]),

@@ -93,6 +93,11 @@ class Engine:
         _lib.check(self.lib.fcx_algorithmic_bytes(self.h, phase, ctypes.byref(b)))
         return b.value
 
+    OPTIONS = {"cells_per_thread": 1, "max_blocks": 2, "nontemporal": 3, "specialize": 4}
+
+    def set_option(self, name, value):
+        _lib.check(self.lib.fcx_set_option(self.h, self.OPTIONS[name], int(value)))
+
     def device_ptr(self, s, g, name):
         p = ctypes.POINTER(ctypes.c_double)()
         _lib.check(self.lib.fcx_device_ptr(self.h, s, g, IDX[name], ctypes.byref(p)))

@@ -141,6 +141,15 @@ int fcx_last_kernel_ms(fcx_engine *e, float *ms);
 /* algorithmic HBM bytes of one fcx_run(phase) (each distinct array read once, written once) */
 int fcx_algorithmic_bytes(fcx_engine *e, int phase, int64_t *bytes);
 
+/* launch tuning of the fused cells kernel (defaults are the measured best on MI355X) */
+enum fcx_option {
+  FCX_OPT_CELLS_PER_THREAD = 1, /* 1 or 2 cells per lane (2: 16-B loads; default 2)       */
+  FCX_OPT_MAX_BLOCKS = 2,       /* grid-stride cap in 256-thread blocks; 0 = no cap       */
+  FCX_OPT_NONTEMPORAL = 3,      /* non-temporal hint on streamed loads/stores (default 1) */
+  FCX_OPT_SPECIALIZE = 4        /* T=1 CCLM/MOM5/RCO specialised kernels (default 1)      */
+};
+int fcx_set_option(fcx_engine *e, int option, int64_t value);
+
 /* device memory for hosts that keep fields resident in HBM (bind with FCX_MEM_DEVICE) */
 int fcx_device_malloc(int device, size_t bytes, void **ptr);
 int fcx_device_free(void *ptr);
