@@ -1,0 +1,217 @@
+! fcx_c_api.F90 -- iso_c_binding interfaces of include/fcx.h for Fortran hosts.
+!
+! One interface per C entry point, plain C types only (integers, doubles, c_ptr).  Every
+! function returns the C status (FCX_OK == 0); fcx_error_message() turns fcx_last_error()
+! into a Fortran string.
+MODULE fcx_c_api
+  USE, INTRINSIC :: iso_c_binding
+  IMPLICIT NONE
+
+  INTEGER(c_int), PARAMETER :: FCX_OK = 0
+  INTEGER(c_int), PARAMETER :: FCX_PHASE_EARLY = 1, FCX_PHASE_NORMAL = 2, FCX_PHASE_ALL = 3
+  INTEGER(c_int), PARAMETER :: FCX_MEM_HOST = 0, FCX_MEM_DEVICE = 1, FCX_ALLOCATED = 2
+  INTEGER(c_int), PARAMETER :: FCX_CORR_CELL_MAJOR = 0, FCX_CORR_MONTH_MAJOR = 1
+  ! which_* tables (enum fcx_flux)
+  INTEGER(c_int), PARAMETER :: FCX_SPEC_VAPOR_SURFACE_T = 0, FCX_SPEC_VAPOR_SURFACE_U = 1, &
+                               FCX_SPEC_VAPOR_SURFACE_V = 2, FCX_FLUX_MASS_EVAP = 3, &
+                               FCX_FLUX_HEAT_LATENT = 4, FCX_FLUX_HEAT_SENSIBLE = 5, &
+                               FCX_FLUX_MOMENTUM = 6, FCX_FLUX_RADIATION_BLACKBODY = 7
+  ! regridding matrices (enum fcx_regrid)
+  INTEGER(c_int), PARAMETER :: FCX_U_TO_T = 0, FCX_V_TO_T = 1, FCX_T_TO_U = 2, FCX_T_TO_V = 3
+
+  INTERFACE
+    FUNCTION fcx_last_error() BIND(C, name='fcx_last_error')
+      IMPORT :: c_ptr
+      TYPE(c_ptr) :: fcx_last_error
+    END FUNCTION
+    FUNCTION fcx_version() BIND(C, name='fcx_version')
+      IMPORT :: c_int
+      INTEGER(c_int) :: fcx_version
+    END FUNCTION
+    FUNCTION fcx_method_from_string(s, len) BIND(C, name='fcx_method_from_string')
+      IMPORT :: c_int, c_char, c_size_t
+      CHARACTER(kind=c_char), DIMENSION(*), INTENT(IN) :: s
+      INTEGER(c_size_t), VALUE :: len
+      INTEGER(c_int) :: fcx_method_from_string
+    END FUNCTION
+    FUNCTION fcx_current_month(init_date, seconds, month) BIND(C, name='fcx_current_month')
+      IMPORT :: c_int, c_int32_t, c_int64_t
+      INTEGER(c_int32_t), VALUE :: init_date
+      INTEGER(c_int64_t), VALUE :: seconds
+      INTEGER(c_int32_t), INTENT(OUT) :: month
+      INTEGER(c_int) :: fcx_current_month
+    END FUNCTION
+    FUNCTION fcx_create(device, num_surface_types, grid_size, engine) BIND(C, name='fcx_create')
+      IMPORT :: c_int, c_int32_t, c_ptr
+      INTEGER(c_int), VALUE :: device, num_surface_types
+      INTEGER(c_int32_t), DIMENSION(3), INTENT(IN) :: grid_size
+      TYPE(c_ptr), INTENT(OUT) :: engine
+      INTEGER(c_int) :: fcx_create
+    END FUNCTION
+    FUNCTION fcx_destroy(engine) BIND(C, name='fcx_destroy')
+      IMPORT :: c_int, c_ptr
+      TYPE(c_ptr), VALUE :: engine
+      INTEGER(c_int) :: fcx_destroy
+    END FUNCTION
+    FUNCTION fcx_set_method(engine, flux, surface_type, method) BIND(C, name='fcx_set_method')
+      IMPORT :: c_int, c_ptr
+      TYPE(c_ptr), VALUE :: engine
+      INTEGER(c_int), VALUE :: flux, surface_type, method
+      INTEGER(c_int) :: fcx_set_method
+    END FUNCTION
+    FUNCTION fcx_bind_field(engine, surface_type, grid, var, ptr, n, flags) BIND(C, name='fcx_bind_field')
+      IMPORT :: c_int, c_ptr, c_int64_t
+      TYPE(c_ptr), VALUE :: engine, ptr
+      INTEGER(c_int), VALUE :: surface_type, grid, var, flags
+      INTEGER(c_int64_t), VALUE :: n
+      INTEGER(c_int) :: fcx_bind_field
+    END FUNCTION
+    FUNCTION fcx_set_corrections(engine, enabled, init_date, corr, n, layout) BIND(C, name='fcx_set_corrections')
+      IMPORT :: c_int, c_int32_t, c_int64_t, c_ptr
+      TYPE(c_ptr), VALUE :: engine, corr
+      INTEGER(c_int), VALUE :: enabled, layout
+      INTEGER(c_int32_t), VALUE :: init_date
+      INTEGER(c_int64_t), VALUE :: n
+      INTEGER(c_int) :: fcx_set_corrections
+    END FUNCTION
+    FUNCTION fcx_set_regrid_matrix(engine, which, nnz, src, dst, w) BIND(C, name='fcx_set_regrid_matrix')
+      IMPORT :: c_int, c_int64_t, c_ptr
+      TYPE(c_ptr), VALUE :: engine, src, dst, w
+      INTEGER(c_int), VALUE :: which
+      INTEGER(c_int64_t), VALUE :: nnz
+      INTEGER(c_int) :: fcx_set_regrid_matrix
+    END FUNCTION
+    FUNCTION fcx_set_put_to(engine, surface_type, grid, var, mask) BIND(C, name='fcx_set_put_to')
+      IMPORT :: c_int, c_ptr
+      TYPE(c_ptr), VALUE :: engine
+      INTEGER(c_int), VALUE :: surface_type, grid, var, mask
+      INTEGER(c_int) :: fcx_set_put_to
+    END FUNCTION
+    FUNCTION fcx_add_average(engine, phase, grid, var) BIND(C, name='fcx_add_average')
+      IMPORT :: c_int, c_ptr
+      TYPE(c_ptr), VALUE :: engine
+      INTEGER(c_int), VALUE :: phase, grid, var
+      INTEGER(c_int) :: fcx_add_average
+    END FUNCTION
+    FUNCTION fcx_commit(engine) BIND(C, name='fcx_commit')
+      IMPORT :: c_int, c_ptr
+      TYPE(c_ptr), VALUE :: engine
+      INTEGER(c_int) :: fcx_commit
+    END FUNCTION
+    FUNCTION fcx_step(engine, phase, t) BIND(C, name='fcx_step')
+      IMPORT :: c_int, c_int32_t, c_ptr
+      TYPE(c_ptr), VALUE :: engine
+      INTEGER(c_int), VALUE :: phase
+      INTEGER(c_int32_t), VALUE :: t
+      INTEGER(c_int) :: fcx_step
+    END FUNCTION
+    FUNCTION fcx_run(engine, phase, t) BIND(C, name='fcx_run')
+      IMPORT :: c_int, c_int32_t, c_ptr
+      TYPE(c_ptr), VALUE :: engine
+      INTEGER(c_int), VALUE :: phase
+      INTEGER(c_int32_t), VALUE :: t
+      INTEGER(c_int) :: fcx_run
+    END FUNCTION
+    FUNCTION fcx_upload(engine, phase) BIND(C, name='fcx_upload')
+      IMPORT :: c_int, c_ptr
+      TYPE(c_ptr), VALUE :: engine
+      INTEGER(c_int), VALUE :: phase
+      INTEGER(c_int) :: fcx_upload
+    END FUNCTION
+    FUNCTION fcx_download(engine, phase) BIND(C, name='fcx_download')
+      IMPORT :: c_int, c_ptr
+      TYPE(c_ptr), VALUE :: engine
+      INTEGER(c_int), VALUE :: phase
+      INTEGER(c_int) :: fcx_download
+    END FUNCTION
+    FUNCTION fcx_synchronize(engine) BIND(C, name='fcx_synchronize')
+      IMPORT :: c_int, c_ptr
+      TYPE(c_ptr), VALUE :: engine
+      INTEGER(c_int) :: fcx_synchronize
+    END FUNCTION
+    FUNCTION fcx_calc_spec_vapor_surface(engine, which_grid) BIND(C, name='fcx_calc_spec_vapor_surface')
+      IMPORT :: c_int, c_ptr
+      TYPE(c_ptr), VALUE :: engine
+      INTEGER(c_int), VALUE :: which_grid
+      INTEGER(c_int) :: fcx_calc_spec_vapor_surface
+    END FUNCTION
+    FUNCTION fcx_calc_flux_mass_evap(engine, t) BIND(C, name='fcx_calc_flux_mass_evap')
+      IMPORT :: c_int, c_int32_t, c_ptr
+      TYPE(c_ptr), VALUE :: engine
+      INTEGER(c_int32_t), VALUE :: t
+      INTEGER(c_int) :: fcx_calc_flux_mass_evap
+    END FUNCTION
+    FUNCTION fcx_calc_flux_heat_latent(engine) BIND(C, name='fcx_calc_flux_heat_latent')
+      IMPORT :: c_int, c_ptr
+      TYPE(c_ptr), VALUE :: engine
+      INTEGER(c_int) :: fcx_calc_flux_heat_latent
+    END FUNCTION
+    FUNCTION fcx_calc_flux_heat_sensible(engine) BIND(C, name='fcx_calc_flux_heat_sensible')
+      IMPORT :: c_int, c_ptr
+      TYPE(c_ptr), VALUE :: engine
+      INTEGER(c_int) :: fcx_calc_flux_heat_sensible
+    END FUNCTION
+    FUNCTION fcx_calc_flux_momentum_east(engine, which_grid) BIND(C, name='fcx_calc_flux_momentum_east')
+      IMPORT :: c_int, c_ptr
+      TYPE(c_ptr), VALUE :: engine
+      INTEGER(c_int), VALUE :: which_grid
+      INTEGER(c_int) :: fcx_calc_flux_momentum_east
+    END FUNCTION
+    FUNCTION fcx_calc_flux_momentum_north(engine, which_grid) BIND(C, name='fcx_calc_flux_momentum_north')
+      IMPORT :: c_int, c_ptr
+      TYPE(c_ptr), VALUE :: engine
+      INTEGER(c_int), VALUE :: which_grid
+      INTEGER(c_int) :: fcx_calc_flux_momentum_north
+    END FUNCTION
+    FUNCTION fcx_calc_flux_radiation_blackbody(engine) BIND(C, name='fcx_calc_flux_radiation_blackbody')
+      IMPORT :: c_int, c_ptr
+      TYPE(c_ptr), VALUE :: engine
+      INTEGER(c_int) :: fcx_calc_flux_radiation_blackbody
+    END FUNCTION
+    FUNCTION fcx_distribute_shortwave_radiation_flux(engine) &
+        BIND(C, name='fcx_distribute_shortwave_radiation_flux')
+      IMPORT :: c_int, c_ptr
+      TYPE(c_ptr), VALUE :: engine
+      INTEGER(c_int) :: fcx_distribute_shortwave_radiation_flux
+    END FUNCTION
+    FUNCTION fcx_average_across_surface_types(engine, which_grid, var) &
+        BIND(C, name='fcx_average_across_surface_types')
+      IMPORT :: c_int, c_ptr
+      TYPE(c_ptr), VALUE :: engine
+      INTEGER(c_int), VALUE :: which_grid, var
+      INTEGER(c_int) :: fcx_average_across_surface_types
+    END FUNCTION
+    FUNCTION fcx_do_regridding(engine, var, surface_type) BIND(C, name='fcx_do_regridding')
+      IMPORT :: c_int, c_ptr
+      TYPE(c_ptr), VALUE :: engine
+      INTEGER(c_int), VALUE :: var, surface_type
+      INTEGER(c_int) :: fcx_do_regridding
+    END FUNCTION
+  END INTERFACE
+
+CONTAINS
+
+  ! fcx_last_error() as a Fortran string
+  FUNCTION fcx_error_message() RESULT(msg)
+    CHARACTER(len=512) :: msg
+    TYPE(c_ptr) :: p
+    CHARACTER(kind=c_char), DIMENSION(:), POINTER :: chars
+    INTEGER :: i
+    msg = ''
+    p = fcx_last_error()
+    IF (.NOT. c_associated(p)) RETURN
+    CALL c_f_pointer(p, chars, [512])
+    DO i = 1, 512
+      IF (chars(i) == c_null_char) EXIT
+      msg(i:i) = chars(i)
+    END DO
+  END FUNCTION
+
+  ! trim(method) of a CHARACTER(len=20) namelist entry -> enum fcx_method (-1 unknown)
+  FUNCTION fcx_method_id(method) RESULT(id)
+    CHARACTER(len=*), INTENT(IN) :: method
+    INTEGER(c_int) :: id
+    id = fcx_method_from_string(method, INT(LEN(method), c_size_t))
+  END FUNCTION
+
+END MODULE fcx_c_api

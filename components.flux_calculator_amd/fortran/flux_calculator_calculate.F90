@@ -1,0 +1,274 @@
+! flux_calculator_calculate.F90 -- drop-in replacement of the reference module
+! flux_calculator_calculate (/root/reference/src/flux_calculator_calculate.F90) that runs
+! the flux path on an MI355X through libfcx (include/fcx.h).
+!
+! Same module name, same public subroutines, same arguments:
+!   calc_spec_vapor_surface, calc_flux_mass_evap, calc_flux_heat_latent,
+!   calc_flux_heat_sensible, calc_flux_momentum_east, calc_flux_momentum_north,
+!   calc_flux_radiation_blackbody, distribute_shortwave_radiation_flux,
+!   average_across_surface_types
+! plus the engine life cycle the host calls once (INTEGRATION.md):
+!   fcx_attach              after flux_calculator.F90:761 (all allocations/aliases final)
+!   fcx_register_average    for each type-0 output (optional: fused averaging)
+!   fcx_commit_engine       validate + device mirrors
+!   fcx_run_phase           fused coupling-step phase (replaces :902 and :972-991)
+!   fcx_detach              at finalisation
+! The per-call subroutines keep the reference's exact semantics (each uploads what it
+! reads, computes on the GPU, downloads what it writes).  Errors are written to w_unit
+! and stop the rank (the reference's prepare-time errors call mpi_finalize(1)).
+MODULE flux_calculator_calculate
+
+    USE flux_calculator_basic
+    USE fcx_c_api
+    USE, INTRINSIC :: iso_c_binding
+
+    IMPLICIT NONE
+    PRIVATE
+
+    PUBLIC calc_spec_vapor_surface
+    PUBLIC calc_flux_mass_evap
+    PUBLIC calc_flux_heat_latent
+    PUBLIC calc_flux_heat_sensible
+    PUBLIC calc_flux_momentum_east
+    PUBLIC calc_flux_momentum_north
+    PUBLIC calc_flux_radiation_blackbody
+    PUBLIC distribute_shortwave_radiation_flux
+    PUBLIC average_across_surface_types
+    PUBLIC fcx_attach, fcx_register_average, fcx_commit_engine, fcx_run_phase, fcx_detach
+
+    TYPE(c_ptr), SAVE :: engine = c_null_ptr
+
+CONTAINS
+
+    SUBROUTINE check(status, where)
+        INTEGER(c_int),   INTENT(IN) :: status
+        CHARACTER(len=*), INTENT(IN) :: where
+        IF (status /= FCX_OK) THEN
+            WRITE (w_unit,*) 'flux engine error in ', where, ': ', TRIM(fcx_error_message())
+            CALL FLUSH(w_unit)
+            ERROR STOP 1
+        ENDIF
+    END SUBROUTINE check
+
+    SUBROUTINE set_table(flux, methods, my_bottom_model, num_surface_types)
+        INTEGER(c_int),                          INTENT(IN) :: flux
+        CHARACTER(len=20), DIMENSION(:,:),       INTENT(IN) :: methods
+        INTEGER,                                 INTENT(IN) :: my_bottom_model, num_surface_types
+        INTEGER :: i
+        INTEGER(c_int) :: m
+        DO i = 1, num_surface_types
+            m = fcx_method_id(methods(my_bottom_model, i))
+            IF (m < 0) THEN
+                WRITE (w_unit,*) 'Method ', methods(my_bottom_model, i), ' is not known.'
+                ERROR STOP 1
+            ENDIF
+            CALL check(fcx_set_method(engine, flux, INT(i, c_int), m), 'fcx_set_method')
+        ENDDO
+    END SUBROUTINE set_table
+
+    ! Bind every ASSOCIATED local_field slot (aliases = identical addresses), the method
+    ! tables, the bias corrections and the rank-local regridding matrices.
+    SUBROUTINE fcx_attach(my_bottom_model, num_surface_types, grid_size, local_field,          &
+                          which_spec_vapor_surface_t, which_spec_vapor_surface_u,            &
+                          which_spec_vapor_surface_v, which_flux_mass_evap,                  &
+                          which_flux_heat_latent, which_flux_heat_sensible,                  &
+                          which_flux_momentum, which_flux_radiation_blackbody,               &
+                          lcorrection, correction_init_date, corrections_mass_evap,          &
+                          regrid_u_to_t_matrix, regrid_v_to_t_matrix,                        &
+                          regrid_t_to_u_matrix, regrid_t_to_v_matrix, device)
+        INTEGER,                                  INTENT(IN) :: my_bottom_model, num_surface_types
+        INTEGER,                 DIMENSION(:),    INTENT(IN) :: grid_size
+        TYPE(local_fields_type), DIMENSION(0:,:), INTENT(IN), TARGET :: local_field
+        CHARACTER(len=20),       DIMENSION(:,:),  INTENT(IN) :: which_spec_vapor_surface_t, &
+            which_spec_vapor_surface_u, which_spec_vapor_surface_v, which_flux_mass_evap,    &
+            which_flux_heat_latent, which_flux_heat_sensible, which_flux_momentum,           &
+            which_flux_radiation_blackbody
+        LOGICAL,                                  INTENT(IN) :: lcorrection
+        INTEGER,                                  INTENT(IN) :: correction_init_date
+        REAL(kind=wp), DIMENSION(:,:), TARGET,    INTENT(IN), OPTIONAL :: corrections_mass_evap ! (12, grid_size(1))
+        TYPE(sparse_regridding_matrix),           INTENT(IN), OPTIONAL, TARGET :: regrid_u_to_t_matrix, &
+            regrid_v_to_t_matrix, regrid_t_to_u_matrix, regrid_t_to_v_matrix
+        INTEGER,                                  INTENT(IN), OPTIONAL :: device
+        INTEGER(c_int32_t) :: gs(3)
+        INTEGER(c_int) :: dev, flags, mask
+        INTEGER :: s, g, v
+
+        IF (c_associated(engine)) CALL fcx_detach()
+        gs = INT(grid_size(1:3), c_int32_t)
+        dev = 0
+        IF (PRESENT(device)) dev = INT(device, c_int)
+        CALL check(fcx_create(dev, INT(num_surface_types, c_int), gs, engine), 'fcx_create')
+
+        CALL set_table(FCX_SPEC_VAPOR_SURFACE_T, which_spec_vapor_surface_t, my_bottom_model, num_surface_types)
+        CALL set_table(FCX_SPEC_VAPOR_SURFACE_U, which_spec_vapor_surface_u, my_bottom_model, num_surface_types)
+        CALL set_table(FCX_SPEC_VAPOR_SURFACE_V, which_spec_vapor_surface_v, my_bottom_model, num_surface_types)
+        CALL set_table(FCX_FLUX_MASS_EVAP, which_flux_mass_evap, my_bottom_model, num_surface_types)
+        CALL set_table(FCX_FLUX_HEAT_LATENT, which_flux_heat_latent, my_bottom_model, num_surface_types)
+        CALL set_table(FCX_FLUX_HEAT_SENSIBLE, which_flux_heat_sensible, my_bottom_model, num_surface_types)
+        CALL set_table(FCX_FLUX_MOMENTUM, which_flux_momentum, my_bottom_model, num_surface_types)
+        CALL set_table(FCX_FLUX_RADIATION_BLACKBODY, which_flux_radiation_blackbody, my_bottom_model, &
+                       num_surface_types)
+
+        ! local_field(0:MAX_SURFACE_TYPES, 3)%var(MAX_VARNAMES) (flux_calculator.F90:159)
+        DO s = 0, MAX_SURFACE_TYPES
+            DO g = 1, 3
+                DO v = 1, MAX_VARNAMES
+                    IF (.NOT. ASSOCIATED(local_field(s,g)%var(v)%field)) CYCLE
+                    IF (SIZE(local_field(s,g)%var(v)%field) == 0) CYCLE
+                    flags = FCX_MEM_HOST
+                    IF (local_field(s,g)%var(v)%allocated) flags = IOR(flags, FCX_ALLOCATED)
+                    CALL check(fcx_bind_field(engine, INT(s, c_int), INT(g, c_int), INT(v, c_int),  &
+                                              c_loc(local_field(s,g)%var(v)%field(1)),          &
+                                              INT(SIZE(local_field(s,g)%var(v)%field), c_int64_t), &
+                                              flags), 'fcx_bind_field')
+                    mask = 0
+                    IF (local_field(s,g)%var(v)%put_to_t_grid) mask = IOR(mask, 1)
+                    IF (local_field(s,g)%var(v)%put_to_u_grid) mask = IOR(mask, 2)
+                    IF (local_field(s,g)%var(v)%put_to_v_grid) mask = IOR(mask, 4)
+                    IF (mask /= 0) CALL check(fcx_set_put_to(engine, INT(s, c_int), INT(g, c_int), &
+                                                             INT(v, c_int), mask), 'fcx_set_put_to')
+                ENDDO
+            ENDDO
+        ENDDO
+
+        ! bias_corrections: corrections(E_MASS_EVAP_CORRECTION, :, :) is (12, grid_size(1))
+        IF (lcorrection .AND. PRESENT(corrections_mass_evap)) THEN
+            CALL check(fcx_set_corrections(engine, 1_c_int, INT(correction_init_date, c_int32_t),  &
+                                           c_loc(corrections_mass_evap(1,1)),                    &
+                                           INT(grid_size(1), c_int64_t), FCX_CORR_CELL_MAJOR),    &
+                       'fcx_set_corrections')
+        ENDIF
+
+        IF (PRESENT(regrid_u_to_t_matrix)) CALL set_matrix(FCX_U_TO_T, regrid_u_to_t_matrix)
+        IF (PRESENT(regrid_v_to_t_matrix)) CALL set_matrix(FCX_V_TO_T, regrid_v_to_t_matrix)
+        IF (PRESENT(regrid_t_to_u_matrix)) CALL set_matrix(FCX_T_TO_U, regrid_t_to_u_matrix)
+        IF (PRESENT(regrid_t_to_v_matrix)) CALL set_matrix(FCX_T_TO_V, regrid_t_to_v_matrix)
+    END SUBROUTINE fcx_attach
+
+    SUBROUTINE set_matrix(which, m)
+        INTEGER(c_int),                         INTENT(IN) :: which
+        TYPE(sparse_regridding_matrix), TARGET, INTENT(IN) :: m
+        IF (m%num_elements <= 0) RETURN
+        CALL check(fcx_set_regrid_matrix(engine, which, INT(m%num_elements, c_int64_t),          &
+                                         c_loc(m%src_index%field(1)), c_loc(m%dst_index%field(1)), &
+                                         c_loc(m%weight%field(1))), 'fcx_set_regrid_matrix')
+    END SUBROUTINE set_matrix
+
+    ! output_field(j) with surface_type 0 (flux_calculator.F90:909-918, 999-1008)
+    SUBROUTINE fcx_register_average(early, which_grid, my_idx)
+        LOGICAL, INTENT(IN) :: early
+        INTEGER, INTENT(IN) :: which_grid, my_idx
+        INTEGER(c_int) :: phase
+        phase = FCX_PHASE_NORMAL
+        IF (early) phase = FCX_PHASE_EARLY
+        CALL check(fcx_add_average(engine, phase, INT(which_grid, c_int), INT(my_idx, c_int)), &
+                   'fcx_add_average')
+    END SUBROUTINE fcx_register_average
+
+    SUBROUTINE fcx_commit_engine()
+        CALL check(fcx_commit(engine), 'fcx_commit')
+    END SUBROUTINE fcx_commit_engine
+
+    ! One fused phase: upload the phase's inputs, all its fluxes + regrids + type-0
+    ! averages in one pass, download its outputs.  phase: FCX_PHASE_EARLY (replaces
+    ! flux_calculator.F90:902-918) or FCX_PHASE_NORMAL (replaces :972-1008).
+    SUBROUTINE fcx_run_phase(phase)
+        INTEGER(c_int), INTENT(IN) :: phase
+        CALL check(fcx_step(engine, phase, INT(current_step_time, c_int32_t)), 'fcx_step')
+    END SUBROUTINE fcx_run_phase
+
+    SUBROUTINE fcx_detach()
+        INTEGER(c_int) :: r
+        IF (.NOT. c_associated(engine)) RETURN
+        r = fcx_destroy(engine)
+        engine = c_null_ptr
+    END SUBROUTINE fcx_detach
+
+    !!!!!!!!!! the reference subroutines (flux_calculator_calculate.F90:25-385) !!!!!!!!!!
+
+    SUBROUTINE calc_spec_vapor_surface(my_bottom_model, num_surface_types, which_grid, methods, grid_size, local_field)
+        INTEGER,                                  INTENT(IN)    :: my_bottom_model
+        INTEGER,                                  INTENT(IN)    :: num_surface_types
+        INTEGER,                                  INTENT(IN)    :: which_grid
+        CHARACTER(len=20),       DIMENSION(:,:),  INTENT(IN)    :: methods
+        INTEGER,                 DIMENSION(:),    INTENT(IN)    :: grid_size
+        TYPE(local_fields_type), DIMENSION(0:,:), INTENT(INOUT) :: local_field
+        CALL check(fcx_calc_spec_vapor_surface(engine, INT(which_grid, c_int)), 'calc_spec_vapor_surface')
+    END SUBROUTINE calc_spec_vapor_surface
+
+    SUBROUTINE calc_flux_mass_evap(my_bottom_model, num_surface_types, methods, grid_size, local_field)
+        INTEGER,                                  INTENT(IN)    :: my_bottom_model
+        INTEGER,                                  INTENT(IN)    :: num_surface_types
+        CHARACTER(len=20),       DIMENSION(:,:),  INTENT(IN)    :: methods
+        INTEGER,                 DIMENSION(:),    INTENT(IN)    :: grid_size
+        TYPE(local_fields_type), DIMENSION(0:,:), INTENT(INOUT) :: local_field
+        ! the month of the bias correction comes from current_step_time (basic:125)
+        CALL check(fcx_calc_flux_mass_evap(engine, INT(current_step_time, c_int32_t)), 'calc_flux_mass_evap')
+    END SUBROUTINE calc_flux_mass_evap
+
+    SUBROUTINE calc_flux_heat_latent(my_bottom_model, num_surface_types, methods, grid_size, local_field)
+        INTEGER,                                  INTENT(IN)    :: my_bottom_model
+        INTEGER,                                  INTENT(IN)    :: num_surface_types
+        CHARACTER(len=20),       DIMENSION(:,:),  INTENT(IN)    :: methods
+        INTEGER,                 DIMENSION(:),    INTENT(IN)    :: grid_size
+        TYPE(local_fields_type), DIMENSION(0:,:), INTENT(INOUT) :: local_field
+        CALL check(fcx_calc_flux_heat_latent(engine), 'calc_flux_heat_latent')
+    END SUBROUTINE calc_flux_heat_latent
+
+    SUBROUTINE calc_flux_heat_sensible(my_bottom_model, num_surface_types, methods, grid_size, local_field)
+        INTEGER,                                  INTENT(IN)    :: my_bottom_model
+        INTEGER,                                  INTENT(IN)    :: num_surface_types
+        CHARACTER(len=20),       DIMENSION(:,:),  INTENT(IN)    :: methods
+        INTEGER,                 DIMENSION(:),    INTENT(IN)    :: grid_size
+        TYPE(local_fields_type), DIMENSION(0:,:), INTENT(INOUT) :: local_field
+        CALL check(fcx_calc_flux_heat_sensible(engine), 'calc_flux_heat_sensible')
+    END SUBROUTINE calc_flux_heat_sensible
+
+    SUBROUTINE calc_flux_momentum_east(my_bottom_model, num_surface_types, which_grid, methods, grid_size, local_field)
+        INTEGER,                                  INTENT(IN)    :: my_bottom_model
+        INTEGER,                                  INTENT(IN)    :: num_surface_types
+        INTEGER,                                  INTENT(IN)    :: which_grid
+        CHARACTER(len=20),       DIMENSION(:,:),  INTENT(IN)    :: methods
+        INTEGER,                 DIMENSION(:),    INTENT(IN)    :: grid_size
+        TYPE(local_fields_type), DIMENSION(0:,:), INTENT(INOUT) :: local_field
+        CALL check(fcx_calc_flux_momentum_east(engine, INT(which_grid, c_int)), 'calc_flux_momentum_east')
+    END SUBROUTINE calc_flux_momentum_east
+
+    SUBROUTINE calc_flux_momentum_north(my_bottom_model, num_surface_types, which_grid, methods, grid_size, local_field)
+        INTEGER,                                  INTENT(IN)    :: my_bottom_model
+        INTEGER,                                  INTENT(IN)    :: num_surface_types
+        INTEGER,                                  INTENT(IN)    :: which_grid
+        CHARACTER(len=20),       DIMENSION(:,:),  INTENT(IN)    :: methods
+        INTEGER,                 DIMENSION(:),    INTENT(IN)    :: grid_size
+        TYPE(local_fields_type), DIMENSION(0:,:), INTENT(INOUT) :: local_field
+        CALL check(fcx_calc_flux_momentum_north(engine, INT(which_grid, c_int)), 'calc_flux_momentum_north')
+    END SUBROUTINE calc_flux_momentum_north
+
+    SUBROUTINE calc_flux_radiation_blackbody(my_bottom_model, num_surface_types, methods, grid_size, local_field)
+        INTEGER,                                  INTENT(IN)    :: my_bottom_model
+        INTEGER,                                  INTENT(IN)    :: num_surface_types
+        CHARACTER(len=20),       DIMENSION(:,:),  INTENT(IN)    :: methods
+        INTEGER,                 DIMENSION(:),    INTENT(IN)    :: grid_size
+        TYPE(local_fields_type), DIMENSION(0:,:), INTENT(INOUT) :: local_field
+        CALL check(fcx_calc_flux_radiation_blackbody(engine), 'calc_flux_radiation_blackbody')
+    END SUBROUTINE calc_flux_radiation_blackbody
+
+    SUBROUTINE distribute_shortwave_radiation_flux(my_bottom_model, num_surface_types, grid_size, local_field)
+        INTEGER,                                  INTENT(IN)    :: my_bottom_model
+        INTEGER,                                  INTENT(IN)    :: num_surface_types
+        INTEGER,                 DIMENSION(:),    INTENT(IN)    :: grid_size
+        TYPE(local_fields_type), DIMENSION(0:,:), INTENT(INOUT) :: local_field
+        CALL check(fcx_distribute_shortwave_radiation_flux(engine), 'distribute_shortwave_radiation_flux')
+    END SUBROUTINE distribute_shortwave_radiation_flux
+
+    SUBROUTINE average_across_surface_types(which_grid, my_idx, num_surface_types, grid_size, local_field)
+        INTEGER,                                  INTENT(IN)    :: which_grid
+        INTEGER,                                  INTENT(IN)    :: my_idx
+        INTEGER,                                  INTENT(IN)    :: num_surface_types
+        INTEGER,                 DIMENSION(:),    INTENT(IN)    :: grid_size
+        TYPE(local_fields_type), DIMENSION(0:,:), INTENT(INOUT) :: local_field
+        CALL check(fcx_average_across_surface_types(engine, INT(which_grid, c_int), INT(my_idx, c_int)), &
+                   'average_across_surface_types')
+    END SUBROUTINE average_across_surface_types
+
+END MODULE flux_calculator_calculate
