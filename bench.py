@@ -47,6 +47,8 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget")
     p.add_argument("--cpu-cells", type=int, default=1_000_000)
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--atmos", type=int, default=1,
+                   help="exchange->atmosphere accumulation (+ one RCCL all-reduce when N>1)")
     return p.parse_args()
 
 
@@ -96,27 +98,49 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
-    from fcx.basic import PHASE_ALL
+    from fcx.basic import PHASE_ALL, PHASE_NORMAL
     from fcx.engine import Engine
+    from fcx.parallel import PeriodicAtmosMap, apple_range
     from fcx.synthetic import BASE_SEED, build_case, inputs_for_bench
 
     # this rank's APPLE range of the global grid (decomp_def.F90:23-31): weak scaling,
     # every rank owns args.cells cells; the seed follows the global offset
     n = args.cells
-    offset = rank * n
+    n_global = n * world
+    offset, size = apple_range(n_global, rank, world)
+    assert size == n
     host = inputs_for_bench(n, seed=BASE_SEED + offset)
     data = {k: torch.as_tensor(v).to(dev) for k, v in host.items()}
     del host
     stream = torch.cuda.current_stream(dev)
-    cases, engines = [], []
-    for v in variants:
+
+    # exchange -> atmosphere accumulation of the six fluxes sent to the atmosphere; the
+    # first/last local atmosphere cells shared with the neighbour ranks are completed by
+    # ONE all-reduce per step over all variants' boundary slots
+    atm_fields = (("MEVA", 1), ("HLAT", 1), ("HSEN", 1), ("RBBR", 1), ("UMOM", 2), ("VMOM", 3))
+    la = PeriodicAtmosMap().local(offset, n, rank, world, n_global) if args.atmos else None
+    nb, stride = max(world - 1, 0), len(atm_fields)
+    shared = torch.zeros(max(len(variants) * nb * stride, 1), dtype=torch.float64, device=dev)
+    cases, engines, atm_outs = [], [], []
+    for i, v in enumerate(variants):
         c = build_case(v, n=n, T=args.types, bias=args.bias, device=dev,
                        data=data if args.types == 1 else None)
+        atmos = None
+        if la is not None:
+            outs = {name: torch.empty(max(la.n_atmos, 1), dtype=torch.float64, device=dev)
+                    for name, _ in atm_fields}
+            atm_outs.append(outs)
+            atmos = {"local": la, "fields": [(PHASE_NORMAL, 1, g, name, outs[name]) for name, g in atm_fields],
+                     "shared": (shared[i * nb * stride:], stride) if nb else None}
         e = Engine(c.lf, c.num_surface_types, c.methods, corrections=c.corrections,
-                   averages=c.averages, device=local_rank, stream=stream.cuda_stream)
+                   averages=c.averages, device=local_rank, stream=stream.cuda_stream, atmos=atmos,
+                   options={"atmos_in_run": 0})
         cases.append(c)
         engines.append(e)
-    alg_bytes = [e.algorithmic_bytes(PHASE_ALL) for e in engines]
+    alg_bytes = [e.algorithmic_bytes(PHASE_ALL) for e in engines]  # the cells kernel alone
+    atm_bytes = 0
+    if la is not None:  # weights + re-read fields + atmosphere outputs, per variant
+        atm_bytes = n * 8 + (la.n_atmos + 1) * 4 + stride * (n + la.n_atmos) * 8
 
     def step(t, events=None):
         for i, e in enumerate(engines):
@@ -125,6 +149,12 @@ def main():
             e.run(PHASE_ALL, t)
             if events is not None:
                 events[i][1].record(stream)
+            if la is not None:
+                e.run_atmos(PHASE_ALL)
+        if la is not None and world > 1:
+            dist.all_reduce(shared)  # the one collective of the step (RCCL over xGMI)
+            for e in engines:
+                e.atmos_finish()
 
     for w in range(args.warmup):
         step(w * 3600)
@@ -186,8 +216,9 @@ def main():
         "dtype": "f64",
         "data": "synthetic (SURVEY.md 8d distributions, seeded PCG64)",
         "config": {
-            "workload": "config3: synthetic exchange grid, CCLM+MOM5+RCO fused flux kernels "
-                        "back-to-back per coupling step, inputs HBM-resident",
+            "workload": "config3/4: synthetic exchange grid, CCLM+MOM5+RCO fused flux kernels "
+                        "back-to-back per coupling step + exchange->atmosphere accumulation, "
+                        "inputs HBM-resident",
             "cells_per_gpu": n,
             "cells_per_step": cells_per_step,
             "variants": list(variants),
@@ -195,6 +226,10 @@ def main():
             "bias_corrections": bool(args.bias),
             "grids": "u/v grids = t grid",
             "parallelism": f"dp{world} (APPLE contiguous cell ranges)",
+            "atmos_accumulation": (f"6 fluxes -> {la.n_atmos} atmosphere cells per GPU (1 per ~4 "
+                                   "exchange cells), one all-reduce of the shared boundary cells per step"
+                                   if la is not None else "off"),
+            "atmos_alg_bytes_per_variant": int(atm_bytes),
         },
         "roofline": {
             "bound": "hbm",

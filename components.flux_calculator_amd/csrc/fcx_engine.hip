@@ -104,6 +104,23 @@ struct fcx_engine {
   bool user_stream = false;
   LaunchConfig launch;      // fcx_set_option
   bool specialize = true;
+  // exchange -> atmosphere accumulation
+  struct AtmosField {
+    int phase, s, g, var;
+    double *out_host = nullptr, *out_dev = nullptr;
+    bool external = false;
+  };
+  int64_t n_atmos = -1;
+  std::vector<int32_t> atm_row, atm_col;
+  std::vector<double> atm_w;
+  bool atm_contiguous = true;
+  int32_t *d_atm_row = nullptr, *d_atm_col = nullptr;
+  double *d_atm_w = nullptr;
+  std::vector<AtmosField> atm_fields;
+  double *atm_shared = nullptr;
+  int32_t atm_nb = 0, atm_stride = 0, atm_left = -1, atm_right = -1;
+  void *atm_pool = nullptr;
+  bool atmos_in_run = true;
 
   fcx_engine() {
     for (auto &a : slot)
@@ -196,6 +213,10 @@ extern "C" int fcx_destroy(fcx_engine *e) {
     (void)hipFree(r.d_w);
   }
   (void)hipFree(e->corr_dev);
+  (void)hipFree(e->d_atm_row);
+  (void)hipFree(e->d_atm_col);
+  (void)hipFree(e->d_atm_w);
+  (void)hipFree(e->atm_pool);
   (void)hipFree(e->pool);
   if (e->ev0) (void)hipEventDestroy(e->ev0);
   if (e->ev1) (void)hipEventDestroy(e->ev1);
@@ -720,6 +741,32 @@ extern "C" int fcx_commit(fcx_engine *e) {
       HIP_TRY(hipMemcpy(c.d_w, c.w.data(), c.w.size() * sizeof(double), hipMemcpyHostToDevice));
     }
   }
+  if (e->n_atmos >= 0) {
+    HIP_TRY(hipMalloc(&e->d_atm_row, e->atm_row.size() * sizeof(int32_t)));
+    HIP_TRY(hipMemcpy(e->d_atm_row, e->atm_row.data(), e->atm_row.size() * sizeof(int32_t),
+                      hipMemcpyHostToDevice));
+    HIP_TRY(hipMalloc(&e->d_atm_w, std::max<size_t>(e->atm_w.size(), 1) * sizeof(double)));
+    if (!e->atm_w.empty())
+      HIP_TRY(hipMemcpy(e->d_atm_w, e->atm_w.data(), e->atm_w.size() * sizeof(double), hipMemcpyHostToDevice));
+    if (!e->atm_contiguous) {
+      HIP_TRY(hipMalloc(&e->d_atm_col, std::max<size_t>(e->atm_col.size(), 1) * sizeof(int32_t)));
+      if (!e->atm_col.empty())
+        HIP_TRY(hipMemcpy(e->d_atm_col, e->atm_col.data(), e->atm_col.size() * sizeof(int32_t),
+                          hipMemcpyHostToDevice));
+    }
+    size_t need = 0;
+    for (auto &f : e->atm_fields)
+      if (!f.external) need += ((size_t)std::max<int64_t>(e->n_atmos, 1) * sizeof(double) + 255) / 256 * 256;
+    if (need) {
+      HIP_TRY(hipMalloc(&e->atm_pool, need));
+      size_t off = 0;
+      for (auto &f : e->atm_fields)
+        if (!f.external) {
+          f.out_dev = reinterpret_cast<double *>((char *)e->atm_pool + off);
+          off += ((size_t)std::max<int64_t>(e->n_atmos, 1) * sizeof(double) + 255) / 256 * 256;
+        }
+    }
+  }
   e->committed = true;
   return FCX_OK;
 }
@@ -805,6 +852,10 @@ extern "C" int fcx_download(fcx_engine *e, int phase) {
   Plan *pl;
   if (int r = get_plan(e, phase_stages(phase), phase, &pl)) return r;
   if (int r = copy_bufs(e, pl->writes, false)) return r;
+  for (auto &f : e->atm_fields)
+    if ((f.phase & phase) && !f.external && e->n_atmos > 0)
+      HIP_TRY(hipMemcpyAsync(f.out_host, f.out_dev, e->n_atmos * sizeof(double), hipMemcpyDeviceToHost,
+                             e->stream));
   if (e->any_regrid) {  // device-side regrid destinations of the fields this phase computes
     std::vector<int> extra;
     std::vector<int> vars;
@@ -822,6 +873,34 @@ extern "C" int fcx_download(fcx_engine *e, int phase) {
     extra.erase(std::unique(extra.begin(), extra.end()), extra.end());
     if (int r = copy_bufs(e, extra, false)) return r;
   }
+  return FCX_OK;
+}
+
+static AtmosArgs atmos_args(fcx_engine *e, int phase) {
+  AtmosArgs a{};
+  a.row_ptr = e->d_atm_row;
+  a.col = e->atm_contiguous ? nullptr : e->d_atm_col;
+  a.w = e->d_atm_w;
+  a.n_atmos = e->n_atmos;
+  a.stride = e->atm_stride;
+  a.left = e->atm_left;
+  a.right = e->atm_right;
+  a.shared = e->atm_shared;
+  for (auto &f : e->atm_fields) {
+    if (!(f.phase & phase) || a.nf >= kMaxAtmosFields) continue;
+    a.x[a.nf] = e->dptr(f.s, f.g, f.var);
+    a.out[a.nf] = f.out_dev;
+    ++a.nf;
+  }
+  return a;
+}
+
+static int run_atmos(fcx_engine *e, int phase) {
+  if (e->n_atmos < 0 || e->atm_fields.empty()) return FCX_OK;
+  const AtmosArgs a = atmos_args(e, phase);
+  if (a.nf == 0) return FCX_OK;
+  const int r = launch_atmos(a, e->stream);
+  if (r) return fail(FCX_E_HIP, "atmos_kernel launch: %s", hipGetErrorString((hipError_t)r));
   return FCX_OK;
 }
 
@@ -850,6 +929,8 @@ extern "C" int fcx_run(fcx_engine *e, int phase, int32_t t) {
     if (int r = get_plan(e, S_AVG, phase, &pl)) return r;
     if (int r = launch_plan(e, pl, nullptr)) return r;
   }
+  if (e->atmos_in_run)
+    if (int r = run_atmos(e, phase)) return r;
   HIP_TRY(hipEventRecord(e->ev1, e->stream));
   e->timed = true;
   return FCX_OK;
@@ -983,7 +1064,14 @@ extern "C" int fcx_algorithmic_bytes(fcx_engine *e, int phase, int64_t *bytes) {
   for (int id : pl->reads) b += e->bufs[id].n;
   for (int id : pl->writes) b += e->bufs[id].n;
   if (e->lcorr && (phase & FCX_PHASE_NORMAL)) b += e->n[0];
-  *bytes = b * (int64_t)sizeof(double);
+  int64_t extra = 0;  // atmosphere accumulation: weights (+cols), re-read fields, outputs
+  int nf = 0;
+  for (auto &f : e->atm_fields) nf += (f.phase & phase) ? 1 : 0;
+  if (nf && e->n_atmos >= 0 && e->atmos_in_run) {
+    extra += e->n[0] * 8 + (e->atm_contiguous ? 0 : e->n[0] * 4) + (e->n_atmos + 1) * 4;
+    extra += (int64_t)nf * (e->n[0] + e->n_atmos) * 8;
+  }
+  *bytes = b * (int64_t)sizeof(double) + extra;
   return FCX_OK;
 }
 
@@ -1031,7 +1119,102 @@ extern "C" int fcx_set_option(fcx_engine *e, int option, int64_t value) {
     case FCX_OPT_SPECIALIZE:
       e->specialize = value != 0;
       return FCX_OK;
+    case FCX_OPT_ATMOS_IN_RUN:
+      e->atmos_in_run = value != 0;
+      return FCX_OK;
     default:
       return fail(FCX_E_ARG, "option %d unknown", option);
   }
+}
+
+// ------------------------------------------------------------------ atmosphere accumulation
+
+extern "C" int fcx_set_atmos_map(fcx_engine *e, int64_t n_atmos, const int32_t *idx, const double *w) {
+  if (!e) return fail(FCX_E_ARG, "NULL engine");
+  if (e->committed) return fail(FCX_E_STATE, "engine already committed");
+  const int64_t n = e->n[0];
+  if (n_atmos < 0 || (n > 0 && (!idx || !w))) return fail(FCX_E_ARG, "bad atmosphere map");
+  std::vector<int32_t> count((size_t)n_atmos + 1, 0);
+  bool sorted = true;
+  for (int64_t x = 0; x < n; ++x) {
+    if (idx[x] < 0 || idx[x] >= n_atmos)
+      return fail(FCX_E_ARG, "atmosphere index %d of exchange cell %lld outside 0..%lld", idx[x],
+                  (long long)x, (long long)n_atmos - 1);
+    if (x > 0 && idx[x] < idx[x - 1]) sorted = false;
+    count[(size_t)idx[x] + 1]++;
+  }
+  e->n_atmos = n_atmos;
+  e->atm_row.assign((size_t)n_atmos + 1, 0);
+  for (int64_t a = 0; a < n_atmos; ++a) e->atm_row[(size_t)a + 1] = e->atm_row[(size_t)a] + count[(size_t)a + 1];
+  e->atm_contiguous = sorted;
+  e->atm_w.assign((size_t)n, 0.0);
+  e->atm_col.clear();
+  if (sorted) {
+    for (int64_t x = 0; x < n; ++x) e->atm_w[(size_t)x] = w[x];
+  } else {  // CSR by atmosphere cell, links kept in increasing exchange cell order
+    e->atm_col.assign((size_t)n, 0);
+    std::vector<int32_t> fill(e->atm_row.begin(), e->atm_row.end() - 1);
+    for (int64_t x = 0; x < n; ++x) {
+      const int32_t at = fill[(size_t)idx[x]]++;
+      e->atm_col[(size_t)at] = (int32_t)x;
+      e->atm_w[(size_t)at] = w[x];
+    }
+  }
+  return FCX_OK;
+}
+
+extern "C" int fcx_add_atmos_field(fcx_engine *e, int phase, int s, int g, int var, double *out, int flags) {
+  if (!e) return fail(FCX_E_ARG, "NULL engine");
+  if (e->committed) return fail(FCX_E_STATE, "engine already committed");
+  if (e->n_atmos < 0) return fail(FCX_E_STATE, "fcx_set_atmos_map first");
+  if (phase < 1 || phase > 3 || s < 0 || s > kMaxTypes || g < 1 || g > 3 || var < 1 || var > kNumVars || !out)
+    return fail(FCX_E_ARG, "bad atmosphere field arguments");
+  if (e->n[g - 1] != e->n[0]) return fail(FCX_E_UNSUPPORTED, "atmosphere fields must live on the t grid cells");
+  if ((int)e->atm_fields.size() >= kMaxAtmosFields)
+    return fail(FCX_E_UNSUPPORTED, "more than %d atmosphere fields", kMaxAtmosFields);
+  fcx_engine::AtmosField f;
+  f.phase = phase;
+  f.s = s;
+  f.g = g;
+  f.var = var;
+  if (flags & FCX_MEM_DEVICE) {
+    f.out_dev = out;
+    f.external = true;
+  } else {
+    f.out_host = out;
+  }
+  e->atm_fields.push_back(f);
+  return FCX_OK;
+}
+
+extern "C" int fcx_set_atmos_shared(fcx_engine *e, double *shared, int32_t nb, int32_t stride, int32_t left,
+                                    int32_t right) {
+  if (!e) return fail(FCX_E_ARG, "NULL engine");
+  if (nb < 0 || stride < 0 || left >= nb || right >= nb || (nb > 0 && !shared))
+    return fail(FCX_E_ARG, "bad shared boundary buffer");
+  if ((left >= 0 || right >= 0) && stride < (int32_t)e->atm_fields.size())
+    return fail(FCX_E_ARG, "stride %d < %zu atmosphere fields", stride, e->atm_fields.size());
+  if (left >= 0 && right >= 0 && e->n_atmos < 2)
+    return fail(FCX_E_UNSUPPORTED, "one atmosphere cell shared on both sides (shard too small)");
+  e->atm_shared = shared;
+  e->atm_nb = nb;
+  e->atm_stride = stride;
+  e->atm_left = left;
+  e->atm_right = right;
+  return FCX_OK;
+}
+
+extern "C" int fcx_atmos_finish(fcx_engine *e) {
+  if (int r = check(e)) return r;
+  if (!e->atm_shared || e->n_atmos <= 0) return FCX_OK;
+  const AtmosArgs a = atmos_args(e, FCX_PHASE_ALL);
+  const int r = launch_atmos_finish(a, e->atm_nb, e->stream);
+  if (r) return fail(FCX_E_HIP, "atmos_finish launch: %s", hipGetErrorString((hipError_t)r));
+  return FCX_OK;
+}
+
+extern "C" int fcx_run_atmos(fcx_engine *e, int phase) {
+  if (int r = check(e)) return r;
+  if (phase < 1 || phase > 3) return fail(FCX_E_ARG, "phase %d unknown", phase);
+  return run_atmos(e, phase);
 }

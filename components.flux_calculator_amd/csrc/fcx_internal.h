@@ -78,6 +78,22 @@ struct LaunchConfig {
 // corr_m: month slice [n_t] of the bias corrections (device), or nullptr
 int launch_cells(const Params *host_params, const Params *dev_params, const double *corr_m,
                  const LaunchConfig &lc, void *stream);
+constexpr int kMaxAtmosFields = 16;
+struct AtmosArgs {
+  const int32_t *row_ptr;  // [n_atmos + 1] into the exchange cells (CSR by atmosphere cell)
+  const int32_t *col;      // exchange cell of each link, or nullptr when col[k] == k
+  const double *w;         // [links]
+  int64_t n_atmos;
+  int32_t nf;
+  int32_t stride;
+  int32_t left, right;     // boundary slot of the first / last atmosphere cell, -1 = none
+  double *shared;
+  const double *x[kMaxAtmosFields];
+  double *out[kMaxAtmosFields];
+};
+int launch_atmos(const AtmosArgs &a, void *stream);
+int launch_atmos_finish(const AtmosArgs &a, int32_t n_boundaries, void *stream);
+
 int launch_regrid_csr(const int32_t *row_ptr, const int32_t *col, const double *w,
                       const double *src, double *dst, int64_t n_dst, void *stream);
 int launch_zero(double *x, int64_t n, void *stream);

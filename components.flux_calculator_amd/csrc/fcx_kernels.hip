@@ -323,6 +323,45 @@ __global__ __launch_bounds__(256) void regrid_csr_kernel(const int32_t *__restri
   dst[d] = acc;
 }
 
+// exchange -> atmosphere accumulation: one thread per local atmosphere cell sums its
+// exchange cells in increasing order from 0.0 (the sequential SCRIP weight application),
+// all registered fields at once so each weight is read once.  The first / last cell also
+// lands in its shared boundary slot when a neighbour rank contributes to it.
+__global__ __launch_bounds__(256) void atmos_kernel(const AtmosArgs a) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= a.n_atmos) return;
+  double acc[kMaxAtmosFields];
+#pragma unroll
+  for (int f = 0; f < kMaxAtmosFields; ++f) acc[f] = 0.0;
+  const int32_t k0 = a.row_ptr[c], k1 = a.row_ptr[c + 1];
+  for (int32_t k = k0; k < k1; ++k) {
+    const int32_t xi = a.col ? a.col[k] : k;
+    const double wk = a.w[k];
+#pragma unroll
+    for (int f = 0; f < kMaxAtmosFields; ++f)
+      if (f < a.nf) acc[f] = acc[f] + wk * a.x[f][xi];
+  }
+#pragma unroll
+  for (int f = 0; f < kMaxAtmosFields; ++f) {
+    if (f >= a.nf) break;
+    a.out[f][c] = acc[f];
+    if (c == 0 && a.left >= 0) a.shared[(int64_t)a.left * a.stride + f] = acc[f];
+    if (c == a.n_atmos - 1 && a.right >= 0) a.shared[(int64_t)a.right * a.stride + f] = acc[f];
+  }
+}
+
+// after the all-reduce: completed boundary sums back into the outputs, then every slot of
+// this engine's region is zeroed for the next step (one block)
+__global__ void atmos_finish_kernel(const AtmosArgs a, int32_t n_boundaries) {
+  const int t = threadIdx.x;
+  if (t < a.nf) {
+    if (a.left >= 0) a.out[t][0] = a.shared[(int64_t)a.left * a.stride + t];
+    if (a.right >= 0) a.out[t][a.n_atmos - 1] = a.shared[(int64_t)a.right * a.stride + t];
+  }
+  __syncthreads();
+  for (int64_t i = t; i < (int64_t)n_boundaries * a.stride; i += blockDim.x) a.shared[i] = 0.0;
+}
+
 __global__ void zero_kernel(double *x, int64_t n) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += stride) x[j] = 0.0;
@@ -383,6 +422,20 @@ int launch_regrid_csr(const int32_t *row_ptr, const int32_t *col, const double *
   const int blocks = (int)((n_dst + 255) / 256);
   hipLaunchKernelGGL(regrid_csr_kernel, dim3(blocks), dim3(256), 0,
                      reinterpret_cast<hipStream_t>(stream), row_ptr, col, w, src, dst, n_dst);
+  return (int)hipGetLastError();
+}
+
+int launch_atmos(const AtmosArgs &a, void *stream) {
+  if (a.n_atmos <= 0 || a.nf <= 0) return 0;
+  const int blocks = (int)((a.n_atmos + 255) / 256);
+  hipLaunchKernelGGL(atmos_kernel, dim3(blocks), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), a);
+  return (int)hipGetLastError();
+}
+
+int launch_atmos_finish(const AtmosArgs &a, int32_t n_boundaries, void *stream) {
+  if (!a.shared) return 0;
+  hipLaunchKernelGGL(atmos_finish_kernel, dim3(1), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     a, n_boundaries);
   return (int)hipGetLastError();
 }
 

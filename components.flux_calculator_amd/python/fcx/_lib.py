@@ -57,6 +57,11 @@ SIGNATURES = [
     ("fcx_last_kernel_ms", _I, [_P, _c.POINTER(_c.c_float)]),
     ("fcx_algorithmic_bytes", _I, [_P, _I, _c.POINTER(_I64)]),
     ("fcx_set_option", _I, [_P, _I, _I64]),
+    ("fcx_set_atmos_map", _I, [_P, _I64, _P, _P]),
+    ("fcx_add_atmos_field", _I, [_P, _I, _I, _I, _I, _P, _I]),
+    ("fcx_set_atmos_shared", _I, [_P, _P, _I32, _I32, _I32, _I32]),
+    ("fcx_atmos_finish", _I, [_P]),
+    ("fcx_run_atmos", _I, [_P, _I]),
     ("fcx_device_malloc", _I, [_I, _c.c_size_t, _c.POINTER(_P)]),
     ("fcx_device_free", _I, [_P]),
     ("fcx_memcpy", _I, [_P, _P, _c.c_size_t, _I]),

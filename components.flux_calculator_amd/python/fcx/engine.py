@@ -18,7 +18,12 @@ class Engine:
     """
 
     def __init__(self, lf: LocalFields, num_surface_types, methods, corrections=None,
-                 averages=(), regrid=None, device=0, stream=None):
+                 averages=(), regrid=None, device=0, stream=None, atmos=None, options=None):
+        """atmos: exchange -> atmosphere accumulation, dict with
+             local   : fcx.parallel.LocalAtmos of this rank
+             fields  : [(phase, surface_type, grid, name, out_array[n_atmos])]
+             shared  : optional (device_buffer[n_boundaries * stride], stride)
+        options: {name: value} for fcx_set_option."""
         self.lib = _lib.load()
         self.lf = lf
         self.T = int(num_surface_types)
@@ -61,6 +66,25 @@ class Engine:
                 _lib.check(self.lib.fcx_set_put_to(h, s, g, IDX[name], mask))
             for phase, g, name in averages:
                 _lib.check(self.lib.fcx_add_average(h, phase, g, IDX[name]))
+            if atmos is not None:
+                la = atmos["local"]
+                idx = np.ascontiguousarray(la.atmos_index, dtype=np.int32)
+                w = np.ascontiguousarray(la.weight, dtype=np.float64)
+                self._keep += [idx, w]
+                _lib.check(self.lib.fcx_set_atmos_map(h, la.n_atmos, ctypes.c_void_p(idx.ctypes.data),
+                                                      ctypes.c_void_p(w.ctypes.data)))
+                for phase, s, g, name, out in atmos["fields"]:
+                    flags = _lib.FCX_MEM_DEVICE if is_device(out) else _lib.FCX_MEM_HOST
+                    self._keep.append(out)
+                    _lib.check(self.lib.fcx_add_atmos_field(h, phase, s, g, IDX[name],
+                                                            ctypes.c_void_p(data_ptr(out)), flags))
+                if atmos.get("shared") is not None:
+                    buf, stride = atmos["shared"]
+                    self._keep.append(buf)
+                    _lib.check(self.lib.fcx_set_atmos_shared(h, ctypes.c_void_p(data_ptr(buf)), la.n_boundaries,
+                                                             stride, la.left, la.right))
+            for name, value in (options or {}).items():
+                _lib.check(self.lib.fcx_set_option(h, self.OPTIONS[name], int(value)))
             _lib.check(self.lib.fcx_commit(h))
         except Exception:
             self.lib.fcx_destroy(h)
@@ -93,7 +117,15 @@ class Engine:
         _lib.check(self.lib.fcx_algorithmic_bytes(self.h, phase, ctypes.byref(b)))
         return b.value
 
-    OPTIONS = {"cells_per_thread": 1, "max_blocks": 2, "nontemporal": 3, "specialize": 4}
+    OPTIONS = {"cells_per_thread": 1, "max_blocks": 2, "nontemporal": 3, "specialize": 4,
+               "atmos_in_run": 5}
+
+    def run_atmos(self, phase=PHASE_ALL):
+        _lib.check(self.lib.fcx_run_atmos(self.h, phase))
+
+    def atmos_finish(self):
+        """After the all-reduce of the shared boundary buffer (fcx_atmos_finish)."""
+        _lib.check(self.lib.fcx_atmos_finish(self.h))
 
     def set_option(self, name, value):
         _lib.check(self.lib.fcx_set_option(self.h, self.OPTIONS[name], int(value)))

@@ -1,0 +1,169 @@
+"""Multi-GPU layout of the flux path: contiguous cell ranges per rank and the
+exchange -> atmosphere accumulation completed by ONE all-reduce.
+
+Partition rules of the reference:
+  * apple_range: decomp_def.F90:23-31 (APPLE): rank r < P-1 owns [r*floor(N/P), +floor(N/P)),
+    the last rank the remainder; the offset/size pair is what flux_calculator declares to
+    OASIS as the APPLE partition [1, offset, size] (flux_calculator.F90:801-803).
+  * task_range: read_scrip_grid_dimensions (flux_calculator_io.F90:77-107): the cells whose
+    `task` entry equals the rank; offset = first such cell - 1, an empty task gets (0, 0).
+
+Exchange -> atmosphere accumulation: every exchange cell lies in exactly one atmosphere cell
+(the exchange grid is the intersection of the atmosphere and bottom grids), with weight
+area_x / area_a, and the exchange grid is ordered by atmosphere row, so the cells of one
+atmosphere cell are contiguous.  A rank's contiguous exchange range therefore touches a
+contiguous atmosphere range whose first and last cells may be shared with the neighbour
+ranks -- the only cross-rank exchange of the whole path.  Each rank writes its partial sums
+of those two cells into boundary slots of a [P-1][stride] buffer (zero elsewhere); one
+all-reduce (sum) over the ranks completes them.
+"""
+from dataclasses import dataclass
+
+import numpy as np
+
+
+def apple_range(n_global, rank, nranks):
+    """(offset, size) of rank's cells, decomp_def.F90:23-31 with id_jm = 1 row per cell."""
+    if not 0 <= rank < nranks:
+        raise ValueError(f"rank {rank} outside 0..{nranks - 1}")
+    part = n_global // nranks
+    offset = rank * part
+    size = part if rank < nranks - 1 else n_global - rank * part
+    return offset, size
+
+
+def task_range(task, mype):
+    """(offset, size) from the exchange-grid `task` vector (flux_calculator_io.F90:77-107)."""
+    task = np.asarray(task)
+    hit = np.nonzero(task == mype)[0]
+    if hit.size == 0:
+        return 0, 0
+    return int(hit[0]), int(hit.size)
+
+
+@dataclass
+class AtmosMap:
+    """Global exchange -> atmosphere map: atmos_index[x] non-decreasing, weight[x]."""
+    atmos_index: np.ndarray  # int32 [n_exchange]
+    weight: np.ndarray  # float64 [n_exchange]
+    n_atmos: int
+
+
+def synthetic_atmos_map(n_exchange, cells_per_atmos=4, seed=20231015):
+    """1 atmosphere cell per ~4 exchange cells: run lengths 3..5,
+    exchange cells ordered by atmosphere cell, weights = exchange area / atmosphere area."""
+    rng = np.random.Generator(np.random.PCG64([seed, 99]))
+    lengths = rng.integers(cells_per_atmos - 1, cells_per_atmos + 2, n_exchange // max(cells_per_atmos - 1, 1) + 2)
+    ends = np.cumsum(lengths)
+    n_atmos = int(np.searchsorted(ends, n_exchange, side="left")) + 1
+    idx = np.repeat(np.arange(n_atmos, dtype=np.int32), lengths[:n_atmos])[:n_exchange]
+    area = rng.uniform(0.5, 1.5, n_exchange)
+    tot = np.bincount(idx, weights=area, minlength=n_atmos)
+    w = area / tot[idx]
+    return AtmosMap(np.ascontiguousarray(idx, dtype=np.int32), np.ascontiguousarray(w), n_atmos)
+
+
+@dataclass
+class LocalAtmos:
+    """A rank's view: local atmosphere indices of its exchange range and its boundary slots."""
+    offset: int  # first exchange cell (0-based global)
+    size: int
+    atmos_offset: int  # first local atmosphere cell (global index)
+    n_atmos: int
+    atmos_index: np.ndarray  # int32 [size], 0-based local
+    weight: np.ndarray
+    left: int  # boundary slot of the first local atmosphere cell, -1 = not shared
+    right: int  # boundary slot of the last one, -1 = not shared
+    n_boundaries: int
+
+
+def local_atmos(amap: AtmosMap, rank, nranks, offset=None, size=None):
+    if offset is None:
+        offset, size = apple_range(amap.atmos_index.shape[0], rank, nranks)
+    gi = amap.atmos_index[offset: offset + size]
+    if size == 0:
+        return LocalAtmos(offset, 0, 0, 0, np.zeros(0, np.int32), np.zeros(0), -1, -1, max(nranks - 1, 0))
+    a0, a1 = int(gi[0]), int(gi[-1])
+    left = rank - 1 if (offset > 0 and amap.atmos_index[offset - 1] == a0) else -1
+    end = offset + size
+    right = rank if (end < amap.atmos_index.shape[0] and amap.atmos_index[end] == a1) else -1
+    if left >= 0 and right >= 0 and a0 == a1:
+        raise ValueError(f"rank {rank}: its {size} cells lie inside one atmosphere cell shared "
+                         "with both neighbours (shard smaller than an atmosphere cell)")
+    return LocalAtmos(offset, size, a0, a1 - a0 + 1, np.ascontiguousarray(gi - a0, dtype=np.int32),
+                      np.ascontiguousarray(amap.weight[offset: offset + size]), left, right,
+                      max(nranks - 1, 0))
+
+
+def pack_boundaries(la: LocalAtmos, partial_fields, stride):
+    """CPU form of the engine's boundary write: [n_boundaries][stride] with this rank's partial
+    sums of its shared first/last atmosphere cells (fields in columns), zero elsewhere."""
+    buf = np.zeros((la.n_boundaries, stride))
+    for f, out in enumerate(partial_fields):
+        if la.left >= 0:
+            buf[la.left, f] = out[0]
+        if la.right >= 0:
+            buf[la.right, f] = out[-1]
+    return buf
+
+
+def unpack_boundaries(la: LocalAtmos, reduced, fields):
+    """CPU form of fcx_atmos_finish: completed boundary sums back into the local fields."""
+    for f, out in enumerate(fields):
+        if la.left >= 0:
+            out[0] = reduced[la.left, f]
+        if la.right >= 0:
+            out[-1] = reduced[la.right, f]
+    return fields
+
+
+class PeriodicAtmosMap:
+    """Structured synthetic map for large sharded runs: every 16 exchange cells form 4
+    atmosphere cells of 3, 4, 5 and 4 cells (mean 4).  Any rank builds
+    its own range in O(size) without the global arrays; areas come from an integer hash of
+    the global cell index, weights = area / sum of the atmosphere cell's areas."""
+    LENGTHS = (3, 4, 5, 4)
+    PERIOD = 16
+
+    def __init__(self):
+        starts = np.cumsum((0,) + self.LENGTHS[:-1])
+        self._sub = np.repeat(np.arange(4), self.LENGTHS)  # cell in period -> sub-cell
+        self._start = starts[self._sub]  # first cell of the sub-cell inside the period
+        self._len = np.array(self.LENGTHS)[self._sub]
+
+    def index(self, x):
+        x = np.asarray(x, dtype=np.int64)
+        return (x // self.PERIOD) * 4 + self._sub[x % self.PERIOD]
+
+    @staticmethod
+    def area(x):
+        h = (np.asarray(x, dtype=np.uint64) * np.uint64(2654435761)) % np.uint64(1000003)
+        return 0.5 + h.astype(np.float64) / 1000003.0
+
+    def weight(self, x, n_global):
+        x = np.asarray(x, dtype=np.int64)
+        first = (x // self.PERIOD) * self.PERIOD + self._start[x % self.PERIOD]
+        length = self._len[x % self.PERIOD]
+        tot = np.zeros(x.shape)
+        for k in range(5):
+            y = first + k
+            tot += np.where((k < length) & (y < n_global), self.area(y), 0.0)
+        return self.area(x) / tot
+
+    def local(self, offset, size, rank, nranks, n_global):
+        x = np.arange(offset, offset + size, dtype=np.int64)
+        gi = self.index(x)
+        if size == 0:
+            return LocalAtmos(offset, 0, 0, 0, np.zeros(0, np.int32), np.zeros(0), -1, -1, max(nranks - 1, 0))
+        a0, a1 = int(gi[0]), int(gi[-1])
+        left = rank - 1 if (offset > 0 and int(self.index(offset - 1)) == a0) else -1
+        end = offset + size
+        right = rank if (end < n_global and int(self.index(end)) == a1) else -1
+        return LocalAtmos(offset, size, a0, a1 - a0 + 1, np.ascontiguousarray(gi - a0, dtype=np.int32),
+                          np.ascontiguousarray(self.weight(x, n_global)), left, right, max(nranks - 1, 0))
+
+    def global_map(self, n_global):
+        x = np.arange(n_global, dtype=np.int64)
+        idx = self.index(x)
+        return AtmosMap(np.ascontiguousarray(idx, dtype=np.int32), self.weight(x, n_global),
+                        int(idx[-1]) + 1 if n_global else 0)

@@ -141,12 +141,36 @@ int fcx_last_kernel_ms(fcx_engine *e, float *ms);
 /* algorithmic HBM bytes of one fcx_run(phase) (each distinct array read once, written once) */
 int fcx_algorithmic_bytes(fcx_engine *e, int phase, int64_t *bytes);
 
+/* ---- exchange-grid -> atmosphere accumulation ----
+ * What OASIS3-MCT does on oasis_put of the type-0 fields ('S A xxxx 00',
+ * create_namcouple.F90:92-98): out[a] = sum_x weight[x] * field[x] over the local t-grid
+ * exchange cells x of atmosphere cell a, summed in increasing x.  Ranks own contiguous
+ * exchange ranges, so only the first and last local atmosphere cells can be shared with a
+ * neighbour rank; their partial sums go to `shared` slots that ONE all-reduce (sum) over
+ * all ranks completes, after which fcx_atmos_finish writes them back. */
+/* atmos_index[x]: 0-based local atmosphere cell of exchange cell x (grid_size(1) entries) */
+int fcx_set_atmos_map(fcx_engine *e, int64_t n_atmos, const int32_t *atmos_index,
+                      const double *weight);
+/* accumulate slot (surface_type, grid, var) into out[n_atmos] at the end of `phase` */
+int fcx_add_atmos_field(fcx_engine *e, int phase, int surface_type, int grid, int var,
+                        double *out, int flags);
+/* shared: device buffer [n_boundaries][stride] (zero on entry, re-zeroed by finish); the
+ * rank's first local atmosphere cell is boundary `left` (-1: not shared), its last one
+ * boundary `right`; field f of the accumulation uses column f (f < stride) */
+int fcx_set_atmos_shared(fcx_engine *e, double *shared, int32_t n_boundaries, int32_t stride,
+                         int32_t left, int32_t right);
+/* after the all-reduce of `shared`: boundary values -> out arrays, slots re-zeroed */
+int fcx_atmos_finish(fcx_engine *e);
+/* the accumulation of `phase` on its own (fcx_run runs it unless FCX_OPT_ATMOS_IN_RUN=0) */
+int fcx_run_atmos(fcx_engine *e, int phase);
+
 /* launch tuning of the fused cells kernel (defaults are the measured best on MI355X) */
 enum fcx_option {
   FCX_OPT_CELLS_PER_THREAD = 1, /* 1 or 2 cells per lane (2: 16-B loads; default 2)       */
   FCX_OPT_MAX_BLOCKS = 2,       /* grid-stride cap in 256-thread blocks; 0 = no cap       */
   FCX_OPT_NONTEMPORAL = 3,      /* non-temporal hint on streamed loads/stores (default 1) */
-  FCX_OPT_SPECIALIZE = 4        /* T=1 CCLM/MOM5/RCO specialised kernels (default 1)      */
+  FCX_OPT_SPECIALIZE = 4,       /* T=1 CCLM/MOM5/RCO specialised kernels (default 1)      */
+  FCX_OPT_ATMOS_IN_RUN = 5      /* fcx_run also runs the atmosphere accumulation (def. 1) */
 };
 int fcx_set_option(fcx_engine *e, int option, int64_t value);
 

@@ -336,3 +336,12 @@ int fco_step_threads(fco_state *st, int nthreads) {
   return 0;
 #endif
 }
+
+void fco_atmos_accumulate(int64_t n_cells, const int32_t *atmos_index, const double *weight,
+                          const double *x_field, int64_t n_atmos, double *out) {
+  for (int64_t a = 0; a < n_atmos; ++a) out[a] = 0.0;
+  for (int64_t x = 0; x < n_cells; ++x) {
+    const int64_t a = atmos_index[x];
+    out[a] = out[a] + weight[x] * x_field[x];
+  }
+}

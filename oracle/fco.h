@@ -84,6 +84,13 @@ void fco_average_across_surface_types(fco_state *st, int which_grid, int var);
 void fco_do_regridding(fco_state *st, int var, int surface_type);
 /* datetime_helpers.py:4-13 restated: month of init_date(YYYYMMDD) + seconds */
 int  fco_current_month(int32_t init_date, int64_t seconds);
+/* Exchange-grid -> atmosphere accumulation that OASIS3-MCT performs on oasis_put of the
+ * type-0 fields ('S A xxxx 00', create_namcouple.F90:92-98, LOCTRANS MAPPING): SCRIP
+ * weight application out[a] = sum_x w[x] * x_field[x] over the exchange cells x of atmosphere
+ * cell a.  Not in the reference repository (OASIS is a sibling component): restated from the
+ * published SCRIP remap, PARITY UNPINNED.  Cells are summed in increasing x, from 0.0. */
+void fco_atmos_accumulate(int64_t n_cells, const int32_t *atmos_index, const double *weight,
+                          const double *x_field, int64_t n_atmos, double *out);
 /* one full coupling step in reference order (flux_calculator.F90:902-991), no regridding */
 void fco_step(fco_state *st);
 /* multi-threaded (OpenMP) variant of fco_step over contiguous cell ranges: the reference's

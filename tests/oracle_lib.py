@@ -64,6 +64,8 @@ def load(kind="c"):
             lib.fco_current_month.restype = ctypes.c_int
             lib.fco_step_threads.argtypes = [ctypes.POINTER(FcoState), ctypes.c_int]
             lib.fco_step.argtypes = [ctypes.POINTER(FcoState)]
+            lib.fco_atmos_accumulate.argtypes = [ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
+                                                 ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
         _libs[kind] = (lib, p)
     return _libs[kind]
 
@@ -172,3 +174,15 @@ def run_state(o, kind="c", phases=(1, 2), regrid=False):
         rg("VMOM")
         fn("distribute_shortwave_radiation_flux")(sp)
         averages(2)
+
+
+def atmos_accumulate(atmos_index, weight, x_field, n_atmos):
+    """fco_atmos_accumulate: sequential SCRIP weight application (parity unpinned)."""
+    lib, _ = load("c")
+    idx = np.ascontiguousarray(atmos_index, dtype=np.int32)
+    w = np.ascontiguousarray(weight, dtype=np.float64)
+    x = np.ascontiguousarray(x_field, dtype=np.float64)
+    out = np.empty(int(n_atmos))
+    lib.fco_atmos_accumulate(idx.shape[0], idx.ctypes.data, w.ctypes.data, x.ctypes.data,
+                             int(n_atmos), out.ctypes.data)
+    return out

@@ -1,0 +1,138 @@
+"""Row (e) on the GPU: sharded coupling steps with the exchange -> atmosphere accumulation
+kernel, the shared boundary slots and fcx_atmos_finish.
+
+* in one process: P engines on disjoint APPLE shards of one grid, their boundary buffers
+  summed on the device (what the all-reduce does), then finish;
+* in two processes on the one GPU of the box: the same through torch.distributed (gloo,
+  since RCCL refuses two ranks on one device; the 8-GPU RCCL run is bench.py's).
+Checked against the CPU oracle's single-process accumulation (tests/parity.py tolerance).
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+import oracle_lib
+from parity import assert_parity
+
+pytestmark = pytest.mark.gpu
+
+from fcx.basic import PHASE_ALL  # noqa: E402
+from fcx.parallel import local_atmos, synthetic_atmos_map  # noqa: E402
+from fcx.synthetic import build_case  # noqa: E402
+
+FIELDS = (("MEVA", 1), ("HLAT", 1), ("HSEN", 1), ("RBBR", 1), ("UMOM", 2), ("VMOM", 3))
+
+
+def reference(n, variant, seed=911):
+    case = build_case(variant, n=n, T=1, bias=True, seed=seed)
+    out = oracle_lib.run_case(case, "c", current_step_time=7200)
+    amap = synthetic_atmos_map(n)
+    ref = {name: oracle_lib.atmos_accumulate(amap.atmos_index, amap.weight, out[(1, g, name)], amap.n_atmos)
+           for name, g in FIELDS}
+    return case, amap, ref
+
+
+def shard_case(full, lo, hi, variant, seed=911):
+    case = build_case(variant, n=hi - lo, T=1, bias=True, seed=seed)
+    remap = {}
+    for key, a in full.lf.field.items():
+        if id(a) not in remap:
+            remap[id(a)] = np.ascontiguousarray(np.asarray(a)[lo:hi])
+        case.lf.field[key] = remap[id(a)]
+    init_date, corr = full.corrections
+    case.corrections = (init_date, np.ascontiguousarray(corr[lo:hi]))
+    return case
+
+
+def make_engine(case, la, shared, stride, device="cuda:0"):
+    import torch
+    from fcx.engine import Engine
+
+    outs = {name: torch.full((max(la.n_atmos, 1),), float("nan"), dtype=torch.float64, device=device)
+            for name, _ in FIELDS}
+    atmos = {"local": la, "fields": [(2, 1, g, name, outs[name]) for name, g in FIELDS],
+             "shared": (shared, stride)}
+    eng = Engine(case.lf, 1, case.methods, corrections=case.corrections, atmos=atmos)
+    return eng, outs
+
+
+@pytest.mark.parametrize("variant,world", [("CCLM", 2), ("MOM5", 4), ("RCO", 8)])
+def test_sharded_engines_one_process(variant, world):
+    import torch
+
+    n = 20_011
+    full, amap, ref = reference(n, variant)
+    stride = len(FIELDS)
+    engines = []
+    for r in range(world):
+        la = local_atmos(amap, r, world)
+        shared = torch.zeros(max(world - 1, 1) * stride, dtype=torch.float64, device="cuda:0")
+        case = shard_case(full, la.offset, la.offset + la.size, variant)
+        eng, outs = make_engine(case, la, shared, stride)
+        engines.append((la, shared, eng, outs))
+    for la, shared, eng, outs in engines:
+        eng.run(PHASE_ALL, 7200)
+        eng.synchronize()
+    total = sum(sh for _, sh, _, _ in engines)  # the all-reduce (sum) of the boundary slots
+    for la, shared, eng, outs in engines:
+        shared.copy_(total)
+        eng.atmos_finish()
+        eng.synchronize()
+        assert float(shared.abs().sum()) == 0.0  # re-zeroed for the next step
+    got = {name: np.full(amap.n_atmos, np.nan) for name, _ in FIELDS}
+    for la, shared, eng, outs in engines:
+        for name, _ in FIELDS:
+            got[name][la.atmos_offset: la.atmos_offset + la.n_atmos] = outs[name].cpu().numpy()[: la.n_atmos]
+        eng.close()
+    assert_parity(got, ref, label=f"{variant} x{world}")
+
+
+def _rank(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        n = 12_007
+        full, amap, _ = reference(n, "CCLM")
+        la = local_atmos(amap, rank, world)
+        stride = len(FIELDS)
+        shared = torch.zeros((world - 1) * stride, dtype=torch.float64, device="cuda:0")
+        case = shard_case(full, la.offset, la.offset + la.size, "CCLM")
+        eng, outs = make_engine(case, la, shared, stride)
+        eng.run(PHASE_ALL, 7200)
+        eng.synchronize()
+        dist.all_reduce(shared)  # ONE collective per step
+        eng.atmos_finish()
+        eng.synchronize()
+        q.put((rank, la.atmos_offset, {k: v.cpu().numpy()[: la.n_atmos].tolist() for k, v in outs.items()}))
+        eng.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_processes_share_one_gpu_gloo():
+    import torch.multiprocessing as mp
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    procs = [ctx.Process(target=_rank, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get() for _ in range(2)]
+    for p in procs:
+        p.join(timeout=180)
+        assert p.exitcode == 0
+    _, amap, ref = reference(12_007, "CCLM")
+    got = {name: np.full(amap.n_atmos, np.nan) for name, _ in FIELDS}
+    for rank, a0, outs in sorted(res):
+        for name, vals in outs.items():
+            got[name][a0: a0 + len(vals)] = vals
+    assert_parity(got, ref, label="2 processes")

@@ -1,0 +1,142 @@
+"""Row (e) on the CPU: APPLE / task-vector partitions, the synthetic exchange -> atmosphere
+map, and the sharded coupling step with ONE all-reduce of the shared boundary slots, run as
+world_size-2 (and 3) process groups on gloo.  The per-rank compute is the CPU oracle; the
+GPU path uses the same partition/boundary logic (tests/test_gpu_multirank.py)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+import oracle_lib
+from fcx.parallel import (apple_range, local_atmos, pack_boundaries, synthetic_atmos_map,
+                          task_range, unpack_boundaries)
+from fcx.synthetic import build_case
+from parity import assert_parity, mixed_error
+
+ATMOS_FIELDS = ("MEVA", "HLAT", "HSEN", "RBBR", "UMOM", "VMOM")
+
+
+@pytest.mark.parametrize("n,p", [(10, 1), (10, 3), (40_000_000, 8), (7, 8), (1001, 4)])
+def test_apple_ranges_cover_grid_once(n, p):
+    cover = []
+    for r in range(p):
+        off, size = apple_range(n, r, p)
+        assert size >= 0
+        cover.append((off, off + size))
+    assert cover[0][0] == 0 and cover[-1][1] == n
+    assert all(cover[i][1] == cover[i + 1][0] for i in range(p - 1))
+    assert all(apple_range(n, r, p)[1] == n // p for r in range(p - 1))  # decomp_def.F90:25-26
+
+
+def test_task_vector_rule():
+    task = np.array([0, 0, 1, 1, 1, 2])
+    assert task_range(task, 0) == (0, 2)
+    assert task_range(task, 1) == (2, 3)
+    assert task_range(task, 2) == (5, 1)
+    assert task_range(task, 3) == (0, 0)  # empty task (io:101-104)
+
+
+def test_synthetic_map_is_conservative_and_sorted():
+    m = synthetic_atmos_map(100_003)
+    assert np.all(np.diff(m.atmos_index) >= 0)
+    sums = np.bincount(m.atmos_index, weights=m.weight, minlength=m.n_atmos)
+    np.testing.assert_allclose(sums, 1.0, rtol=1e-12)
+    lengths = np.bincount(m.atmos_index)
+    assert 3.5 < lengths.mean() < 4.5 and lengths.min() >= 1
+
+
+@pytest.mark.parametrize("p", [2, 3, 8])
+def test_local_views_agree_on_shared_boundaries(p):
+    m = synthetic_atmos_map(50_001)
+    views = [local_atmos(m, r, p) for r in range(p)]
+    for r in range(p - 1):
+        assert (views[r].right == r) == (views[r + 1].left == r)
+        if views[r].right >= 0:
+            assert views[r].atmos_offset + views[r].n_atmos - 1 == views[r + 1].atmos_offset
+        else:
+            assert views[r].atmos_offset + views[r].n_atmos == views[r + 1].atmos_offset
+    assert sum(v.size for v in views) == 50_001
+
+
+def _global_reference(n, amap):
+    case = build_case("CCLM", n=n, T=1, bias=True, seed=777)
+    out = oracle_lib.run_case(case, "c", current_step_time=3600)
+    fields = {}
+    for name in ATMOS_FIELDS:
+        g = 2 if name == "UMOM" else 3 if name == "VMOM" else 1
+        fields[name] = oracle_lib.atmos_accumulate(amap.atmos_index, amap.weight, out[(1, g, name)], amap.n_atmos)
+    return case, out, fields
+
+
+def _rank_main(rank, world, port, n, q):
+    import torch.distributed as dist
+    import torch
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        amap = synthetic_atmos_map(n)
+        full, _, _ = _global_reference(n, amap)
+        la = local_atmos(amap, rank, world)
+        lo, hi = la.offset, la.offset + la.size
+        # this rank's shard: the same inputs, cut to its APPLE range
+        case = build_case("CCLM", n=la.size, T=1, bias=True, seed=777)
+        remap = {}
+        for key, a in full.lf.field.items():
+            if id(a) not in remap:
+                remap[id(a)] = np.ascontiguousarray(np.asarray(a)[lo:hi])
+            case.lf.field[key] = remap[id(a)]
+        init_date, corr = full.corrections
+        case.corrections = (init_date, np.ascontiguousarray(corr[lo:hi]))
+        out = oracle_lib.run_case(case, "c", current_step_time=3600)
+        partial = []
+        for name in ATMOS_FIELDS:
+            g = 2 if name == "UMOM" else 3 if name == "VMOM" else 1
+            partial.append(oracle_lib.atmos_accumulate(la.atmos_index, la.weight, out[(1, g, name)], la.n_atmos))
+        buf = torch.from_numpy(pack_boundaries(la, partial, len(ATMOS_FIELDS)))
+        dist.all_reduce(buf)  # the ONE collective of the step
+        unpack_boundaries(la, buf.numpy(), partial)
+        q.put((rank, la.atmos_offset, la.left, [p.tolist() for p in partial],
+               {name: out[(1, 2 if name == "UMOM" else 3 if name == "VMOM" else 1, name)][:5].tolist()
+                for name in ATMOS_FIELDS}))
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_step_with_one_allreduce_matches_single_process(world):
+    import torch.multiprocessing as mp
+
+    n = 30_011
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_main, args=(r, world, port, n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = [q.get() for _ in range(world)]
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    amap = synthetic_atmos_map(n)
+    _, _, ref = _global_reference(n, amap)
+    got = {name: np.full(amap.n_atmos, np.nan) for name in ATMOS_FIELDS}
+    for rank, a0, left, partial, _ in sorted(results):
+        for f, name in enumerate(ATMOS_FIELDS):
+            vals = np.array(partial[f])
+            if left >= 0:  # the shared first cell was completed by the previous rank too
+                assert got[name][a0] == vals[0] or np.isnan(got[name][a0])
+            got[name][a0: a0 + vals.size] = vals
+    for name in ATMOS_FIELDS:
+        assert not np.isnan(got[name]).any(), name
+        # cells owned by one rank are bit-identical; shared cells differ by association only
+        assert mixed_error(got[name], ref[name]) <= 1e-12, name
+    assert_parity({k: got[k] for k in ATMOS_FIELDS}, ref, label=f"world={world}")
