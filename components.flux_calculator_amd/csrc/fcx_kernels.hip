@@ -323,24 +323,46 @@ __global__ __launch_bounds__(256) void regrid_csr_kernel(const int32_t *__restri
   dst[d] = acc;
 }
 
-// exchange -> atmosphere accumulation: one thread per local atmosphere cell sums its
-// exchange cells in increasing order from 0.0 (the sequential SCRIP weight application),
-// all registered fields at once so each weight is read once.  The first / last cell also
-// lands in its shared boundary slot when a neighbour rank contributes to it.
+// exchange -> atmosphere accumulation (SCRIP weight application of the type-0 fields).
+// One thread per local atmosphere cell, 256 cells per block.  The block's exchange range
+// [row_ptr[a0], row_ptr[a0 + 256]) is streamed through LDS in chunks of kAtmChunk cells:
+// the whole block loads weights and fields with coalesced 8-B loads and stores the
+// products w*x per field, then every lane adds the products of its own segment in link
+// order.  acc = acc + w*x from 0.0 in increasing link order is exactly the sequential
+// weight application, so the result is bit-identical to it (no atomics, no tree order).
+constexpr int kAtmChunk = 512;
+
 __global__ __launch_bounds__(256) void atmos_kernel(const AtmosArgs a) {
-  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= a.n_atmos) return;
+  extern __shared__ double lds[];  // [nf][kAtmChunk] products
+  const int64_t a0 = (int64_t)blockIdx.x * blockDim.x;
+  const int64_t c = a0 + threadIdx.x;
+  const int64_t a_end = min(a0 + (int64_t)blockDim.x, a.n_atmos);
+  const int32_t K0 = a.row_ptr[a0], K1 = a.row_ptr[a_end];
+  const bool mine = c < a.n_atmos;
+  const int32_t k_lo = mine ? a.row_ptr[c] : 0, k_hi = mine ? a.row_ptr[c + 1] : 0;
   double acc[kMaxAtmosFields];
 #pragma unroll
   for (int f = 0; f < kMaxAtmosFields; ++f) acc[f] = 0.0;
-  const int32_t k0 = a.row_ptr[c], k1 = a.row_ptr[c + 1];
-  for (int32_t k = k0; k < k1; ++k) {
-    const int32_t xi = a.col ? a.col[k] : k;
-    const double wk = a.w[k];
+  for (int32_t C0 = K0; C0 < K1; C0 += kAtmChunk) {
+    const int32_t len = min(kAtmChunk, K1 - C0);
+    __syncthreads();
+    for (int32_t i = threadIdx.x; i < len; i += blockDim.x) {
+      const int32_t k = C0 + i;
+      const int32_t xi = a.col ? a.col[k] : k;
+      const double wk = __builtin_nontemporal_load(a.w + k);
 #pragma unroll
-    for (int f = 0; f < kMaxAtmosFields; ++f)
-      if (f < a.nf) acc[f] = acc[f] + wk * a.x[f][xi];
+      for (int f = 0; f < kMaxAtmosFields; ++f)
+        if (f < a.nf) lds[f * kAtmChunk + i] = wk * a.x[f][xi];
+    }
+    __syncthreads();
+    const int32_t lo = max(k_lo, C0), hi = min(k_hi, C0 + len);
+    for (int32_t k = lo; k < hi; ++k) {
+#pragma unroll
+      for (int f = 0; f < kMaxAtmosFields; ++f)
+        if (f < a.nf) acc[f] = acc[f] + lds[f * kAtmChunk + (k - C0)];
+    }
   }
+  if (!mine) return;
 #pragma unroll
   for (int f = 0; f < kMaxAtmosFields; ++f) {
     if (f >= a.nf) break;
@@ -428,7 +450,8 @@ int launch_regrid_csr(const int32_t *row_ptr, const int32_t *col, const double *
 int launch_atmos(const AtmosArgs &a, void *stream) {
   if (a.n_atmos <= 0 || a.nf <= 0) return 0;
   const int blocks = (int)((a.n_atmos + 255) / 256);
-  hipLaunchKernelGGL(atmos_kernel, dim3(blocks), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), a);
+  const size_t lds = (size_t)a.nf * kAtmChunk * sizeof(double);
+  hipLaunchKernelGGL(atmos_kernel, dim3(blocks), dim3(256), lds, reinterpret_cast<hipStream_t>(stream), a);
   return (int)hipGetLastError();
 }
 

@@ -73,6 +73,7 @@ def test_sharded_engines_one_process(variant, world):
         eng, outs = make_engine(case, la, shared, stride)
         engines.append((la, shared, eng, outs))
     for la, shared, eng, outs in engines:
+        eng.upload(PHASE_ALL)  # the shard's fields are host arrays
         eng.run(PHASE_ALL, 7200)
         eng.synchronize()
     total = sum(sh for _, sh, _, _ in engines)  # the all-reduce (sum) of the boundary slots
@@ -103,6 +104,7 @@ def _rank(rank, world, port, q):
         shared = torch.zeros((world - 1) * stride, dtype=torch.float64, device="cuda:0")
         case = shard_case(full, la.offset, la.offset + la.size, "CCLM")
         eng, outs = make_engine(case, la, shared, stride)
+        eng.upload(PHASE_ALL)
         eng.run(PHASE_ALL, 7200)
         eng.synchronize()
         dist.all_reduce(shared)  # ONE collective per step
