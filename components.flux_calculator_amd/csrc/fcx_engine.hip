@@ -68,6 +68,9 @@ struct Plan {
   Params *dev = nullptr;
   std::vector<int> reads, writes;  // buffer ids
   int variant = 0;                 // T=1 specialisation (LaunchConfig::variant)
+  bool atm_fused = false;          // exchange -> atmosphere accumulation inside the launch
+  AtmosFused af{};
+  int atm_nf = 0;
 };
 
 int var0(int var) { return var - 1; }
@@ -114,13 +117,17 @@ struct fcx_engine {
   std::vector<int32_t> atm_row, atm_col;
   std::vector<double> atm_w;
   bool atm_contiguous = true;
-  int32_t *d_atm_row = nullptr, *d_atm_col = nullptr;
+  int32_t *d_atm_row = nullptr, *d_atm_col = nullptr, *d_atm_idx = nullptr;
+  std::vector<int32_t> atm_idx;
+  int32_t atm_maxseg = 0;
+  double *d_atm_carry = nullptr;
   double *d_atm_w = nullptr;
   std::vector<AtmosField> atm_fields;
   double *atm_shared = nullptr;
   int32_t atm_nb = 0, atm_stride = 0, atm_left = -1, atm_right = -1;
   void *atm_pool = nullptr;
   bool atmos_in_run = true;
+  bool atm_done_fused = false;  // the last fcx_run already accumulated the atmosphere fields
 
   fcx_engine() {
     for (auto &a : slot)
@@ -214,6 +221,8 @@ extern "C" int fcx_destroy(fcx_engine *e) {
   }
   (void)hipFree(e->corr_dev);
   (void)hipFree(e->d_atm_row);
+  (void)hipFree(e->d_atm_idx);
+  (void)hipFree(e->d_atm_carry);
   (void)hipFree(e->d_atm_col);
   (void)hipFree(e->d_atm_w);
   (void)hipFree(e->atm_pool);
@@ -483,6 +492,49 @@ static bool merge_ok(const fcx_engine *e) {
   return true;
 }
 
+// The accumulation rides inside the T=1 specialised launch when every registered field of
+// the phase is one of the six fluxes that launch holds in registers (AtmosFused order).
+static void plan_fused_atmos(fcx_engine *e, Plan &pl, uint32_t stages, int phase) {
+  pl.atm_fused = false;
+  if (!pl.variant || !e->d_atm_idx || e->atm_maxseg > kTile / 2 || e->any_regrid || phase <= 0 ||
+      phase >= 1000 || !e->specialize)
+    return;
+  const TypeParams &tp = pl.host.type[0];
+  AtmosFused af{};
+  int nf = 0;
+  for (auto &f : e->atm_fields) {
+    if (!(f.phase & phase)) continue;
+    const int b = e->buf(f.s, f.g, f.var);
+    int k = -1;
+    if (f.s == 1 && f.var == FCX_MEVA && (stages & S_MEVA) && b == e->buf(1, 1, FCX_MEVA)) k = 0;
+    if (f.s == 1 && f.var == FCX_HLAT && (stages & S_HLAT) && b == e->buf(1, 1, FCX_HLAT) &&
+        (tp.m_hlat == FCX_WATER || tp.m_hlat == FCX_ICE || tp.m_hlat == FCX_ZERO))
+      k = 1;
+    if (f.s == 1 && f.var == FCX_HSEN && (stages & S_HSEN) && b == e->buf(1, 1, FCX_HSEN)) k = 2;
+    if (f.s == 1 && f.var == FCX_RBBR && (stages & S_RBBR) && b == e->buf(1, 1, FCX_RBBR) &&
+        (tp.m_rbbr == FCX_STBO || tp.m_rbbr == FCX_ZERO))
+      k = 3;
+    if (f.s == 1 && f.var == FCX_UMOM && (stages & S_UMOM) && b == e->buf(1, 2, FCX_UMOM)) k = 4;
+    if (f.s == 1 && f.var == FCX_VMOM && (stages & S_VMOM) && b == e->buf(1, 3, FCX_VMOM)) k = 5;
+    if (k < 0 || af.out[k]) return;  // not in registers (or twice): separate kernel
+    af.out[k] = f.out_dev;
+    af.x[k] = e->bufs[b].dev;
+    ++nf;
+  }
+  if (nf == 0) return;
+  af.idx = e->d_atm_idx;
+  af.w = e->d_atm_w;
+  af.carry = e->d_atm_carry;
+  af.n_atmos = e->n_atmos;
+  af.shared = e->atm_shared;
+  af.stride = e->atm_stride;
+  af.left = e->atm_left;
+  af.right = e->atm_right;
+  pl.af = af;
+  pl.atm_nf = nf;
+  pl.atm_fused = true;
+}
+
 static int build_plan(fcx_engine *e, uint32_t stages, int avg_phases, Plan &pl) {
   Params &P = pl.host;
   std::memset(&P, 0, sizeof P);
@@ -688,6 +740,7 @@ static int build_plan(fcx_engine *e, uint32_t stages, int avg_phases, Plan &pl) 
         pl.variant = v;
     }
   }
+  plan_fused_atmos(e, pl, stages, avg_phases);
   HIP_TRY(hipMalloc(&pl.dev, sizeof(Params)));
   HIP_TRY(hipMemcpy(pl.dev, &P, sizeof(Params), hipMemcpyHostToDevice));
   return FCX_OK;
@@ -748,6 +801,13 @@ extern "C" int fcx_commit(fcx_engine *e) {
     HIP_TRY(hipMalloc(&e->d_atm_w, std::max<size_t>(e->atm_w.size(), 1) * sizeof(double)));
     if (!e->atm_w.empty())
       HIP_TRY(hipMemcpy(e->d_atm_w, e->atm_w.data(), e->atm_w.size() * sizeof(double), hipMemcpyHostToDevice));
+    if (e->atm_contiguous && !e->atm_idx.empty()) {  // per-cell index for the fused path
+      HIP_TRY(hipMalloc(&e->d_atm_idx, e->atm_idx.size() * sizeof(int32_t)));
+      HIP_TRY(hipMemcpy(e->d_atm_idx, e->atm_idx.data(), e->atm_idx.size() * sizeof(int32_t),
+                        hipMemcpyHostToDevice));
+      const int64_t tiles = (e->n[0] + kTile - 1) / kTile;
+      HIP_TRY(hipMalloc(&e->d_atm_carry, (size_t)std::max<int64_t>(tiles, 1) * kFusedFields * sizeof(double)));
+    }
     if (!e->atm_contiguous) {
       HIP_TRY(hipMalloc(&e->d_atm_col, std::max<size_t>(e->atm_col.size(), 1) * sizeof(int32_t)));
       if (!e->atm_col.empty())
@@ -809,8 +869,20 @@ static int launch_plan(fcx_engine *e, Plan *pl, const double *corr_m) {
   if (!e->aligned16) lc.cells_per_thread = 1;
   lc.merged = pl->host.merged_uv != 0;
   lc.variant = (e->specialize && lc.merged) ? pl->variant : 0;
-  const int r = launch_cells(&pl->host, pl->dev, corr_m, lc, e->stream);
+  const bool fused = pl->atm_fused && lc.variant && lc.cells_per_thread == 2;
+  if (fused) {  // the shared-slot pointers may have been set after the plan was built
+    pl->af.shared = e->atm_shared;
+    pl->af.stride = e->atm_stride;
+    pl->af.left = e->atm_left;
+    pl->af.right = e->atm_right;
+  }
+  const int r = launch_cells(&pl->host, pl->dev, corr_m, lc, e->stream, fused ? &pl->af : nullptr);
   if (r) return fail(FCX_E_HIP, "cells_kernel launch: %s", hipGetErrorString((hipError_t)r));
+  if (fused) {
+    const int r2 = launch_atmos_fixup(pl->af, pl->host.n_max, e->stream);
+    if (r2) return fail(FCX_E_HIP, "atmos_fixup launch: %s", hipGetErrorString((hipError_t)r2));
+    e->atm_done_fused = true;
+  }
   return FCX_OK;
 }
 
@@ -911,6 +983,7 @@ extern "C" int fcx_run(fcx_engine *e, int phase, int32_t t) {
   const double *corr_m = month_slice(e, t, &rc);
   if (rc) return rc;
   HIP_TRY(hipEventRecord(e->ev0, e->stream));
+  e->atm_done_fused = false;
   if (!e->any_regrid) {
     Plan *pl;
     if (int r = get_plan(e, phase_stages(phase), phase, &pl)) return r;
@@ -929,7 +1002,7 @@ extern "C" int fcx_run(fcx_engine *e, int phase, int32_t t) {
     if (int r = get_plan(e, S_AVG, phase, &pl)) return r;
     if (int r = launch_plan(e, pl, nullptr)) return r;
   }
-  if (e->atmos_in_run)
+  if (e->atmos_in_run && !e->atm_done_fused)
     if (int r = run_atmos(e, phase)) return r;
   HIP_TRY(hipEventRecord(e->ev1, e->stream));
   e->timed = true;
@@ -1067,7 +1140,10 @@ extern "C" int fcx_algorithmic_bytes(fcx_engine *e, int phase, int64_t *bytes) {
   int64_t extra = 0;  // atmosphere accumulation: weights (+cols), re-read fields, outputs
   int nf = 0;
   for (auto &f : e->atm_fields) nf += (f.phase & phase) ? 1 : 0;
-  if (nf && e->n_atmos >= 0 && e->atmos_in_run) {
+  if (pl->atm_fused && e->specialize && e->launch.cells_per_thread == 2 && e->aligned16) {
+    nf = 0;  // fused: index + weight per cell, the atmosphere outputs (fluxes not re-read)
+    extra = e->n[0] * (4 + 8) + (int64_t)pl->atm_nf * e->n_atmos * 8;
+  } else if (nf && e->n_atmos >= 0 && e->atmos_in_run) {
     extra += e->n[0] * 8 + (e->atm_contiguous ? 0 : e->n[0] * 4) + (e->n_atmos + 1) * 4;
     extra += (int64_t)nf * (e->n[0] + e->n_atmos) * 8;
   }
@@ -1144,6 +1220,9 @@ extern "C" int fcx_set_atmos_map(fcx_engine *e, int64_t n_atmos, const int32_t *
     count[(size_t)idx[x] + 1]++;
   }
   e->n_atmos = n_atmos;
+  e->atm_idx.assign(idx, idx + n);
+  e->atm_maxseg = 0;
+  for (int64_t a = 0; a < n_atmos; ++a) e->atm_maxseg = std::max(e->atm_maxseg, count[(size_t)a + 1]);
   e->atm_row.assign((size_t)n_atmos + 1, 0);
   for (int64_t a = 0; a < n_atmos; ++a) e->atm_row[(size_t)a + 1] = e->atm_row[(size_t)a] + count[(size_t)a + 1];
   e->atm_contiguous = sorted;
@@ -1216,5 +1295,6 @@ extern "C" int fcx_atmos_finish(fcx_engine *e) {
 extern "C" int fcx_run_atmos(fcx_engine *e, int phase) {
   if (int r = check(e)) return r;
   if (phase < 1 || phase > 3) return fail(FCX_E_ARG, "phase %d unknown", phase);
+  if (e->atm_done_fused) return FCX_OK;  // done inside the last fcx_run
   return run_atmos(e, phase);
 }

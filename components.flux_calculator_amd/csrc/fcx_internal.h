@@ -75,9 +75,10 @@ struct LaunchConfig {
   int variant = 0;           // 0 generic, 1 CCLM, 2 MOM5, 3 RCO (T=1 specialisations)
 };
 
+struct AtmosFused;
 // corr_m: month slice [n_t] of the bias corrections (device), or nullptr
 int launch_cells(const Params *host_params, const Params *dev_params, const double *corr_m,
-                 const LaunchConfig &lc, void *stream);
+                 const LaunchConfig &lc, void *stream, const AtmosFused *atm = nullptr);
 constexpr int kMaxAtmosFields = 16;
 struct AtmosArgs {
   const int32_t *row_ptr;  // [n_atmos + 1] into the exchange cells (CSR by atmosphere cell)
@@ -92,6 +93,25 @@ struct AtmosArgs {
   double *out[kMaxAtmosFields];
 };
 int launch_atmos(const AtmosArgs &a, void *stream);
+
+// Exchange -> atmosphere accumulation fused into the T=1 cells kernel.  The six fluxes it
+// can take from registers, in this order: MEVA HLAT HSEN RBBR UMOM VMOM (out[k] nullptr =
+// not accumulated).  Every 512-cell tile of a block sums the segments that start in it;
+// a segment running past the tile end leaves its prefix sum in carry[tile][k] and
+// atmos_fixup_kernel continues it over the next tile's cells in link order.
+constexpr int kFusedFields = 6;
+constexpr int kTile = 512;  // cells per block iteration (256 lanes x 2)
+struct AtmosFused {
+  const int32_t *idx;  // local atmosphere cell of every exchange cell (non-decreasing)
+  const double *w;
+  double *out[kFusedFields];
+  const double *x[kFusedFields];  // the stored outputs (read by the fix-up only)
+  double *carry;       // [n_tiles][kFusedFields]
+  int64_t n_atmos;
+  double *shared;
+  int32_t stride, left, right;
+};
+int launch_atmos_fixup(const AtmosFused &af, int64_t n_cells, void *stream);
 int launch_atmos_finish(const AtmosArgs &a, int32_t n_boundaries, void *stream);
 
 int launch_regrid_csr(const int32_t *row_ptr, const int32_t *col, const double *w,

@@ -16,6 +16,8 @@
 // the reference's flux-major order has (the 'copy' aliases, the bias added once more per
 // aliased copy, calc:112-116) is resolved by the planner in fcx_engine.hip.
 #include <hip/hip_runtime.h>
+
+#include <algorithm>
 #include "fcx_internal.h"
 #include "fcx_physics.h"
 
@@ -84,7 +86,8 @@ template <int C, bool NT>
 __device__ __forceinline__ void momentum(int8_t m, bool north, const UVGridPtrs &g,
                                          const Vec<C> &ts, const Vec<C> &ps, const Vec<C> &u,
                                          const Vec<C> &v, const Vec<C> &vel, const Vec<C> &qs,
-                                         const Vec<C> &a, int64_t j0, int64_t n) {
+                                         const Vec<C> &a, int64_t j0, int64_t n,
+                                         Vec<C> *keep = nullptr) {
   if (!g.mom) return;
   Vec<C> out;
   if (m == FCX_ZERO) {
@@ -103,6 +106,7 @@ __device__ __forceinline__ void momentum(int8_t m, bool north, const UVGridPtrs 
     return;
   }
   ST(g.mom, j0, n, out);
+  if (keep) *keep = out;
 }
 
 // QSUR + momentum on one separate u or v grid (non-merged layout).
@@ -142,7 +146,7 @@ __device__ __forceinline__ void uv_grid(const TypeParams &tp, int k, uint32_t st
 // compile time, so the other method paths vanish from the code and its register budget.
 template <int C, bool MERGED, int VAR, bool NT>
 __device__ __forceinline__ void process(const Params *__restrict__ P, const double *__restrict__ corr_m,
-                                        int64_t j0) {
+                                        int64_t j0, Vec<C> *av = nullptr) {
   const uint32_t stages = P->stages;
   const int T = VAR ? 1 : P->num_types;
   const int64_t nt = P->n[0];
@@ -194,8 +198,10 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
         if (tp.m_rbbr == FCX_STBO) {
           FOR_C r.v[i] = rbbr_stbo(ts.v[i]);
           ST(g.rbbr, j0, nt, r);
+          if (av) av[3] = r;
         } else if (tp.m_rbbr == FCX_ZERO) {
           ST(g.rbbr, j0, nt, splat<C>(0.0));
+          if (av) av[3] = splat<C>(0.0);
         }
       }
       // ---- calc_spec_vapor_surface(t) (calc:37-49)
@@ -222,6 +228,7 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
             FOR_C me.v[i] = me.v[i] + corr.v[i];
           }
           if (g.meva) ST(g.meva, j0, nt, me);
+          if (av) av[0] = me;
         }
       }
       // ---- calc_flux_heat_latent (calc:135-152)
@@ -234,8 +241,10 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
           FOR_C h.v[i] = me.v[i] * kLs;
           ST(g.hlat, j0, nt, h);
         } else if (tp.m_hlat == FCX_ZERO) {
-          ST(g.hlat, j0, nt, splat<C>(0.0));
+          h = splat<C>(0.0);
+          ST(g.hlat, j0, nt, h);
         }
+        if (av) av[1] = h;
       }
       // ---- calc_flux_heat_sensible (calc:167-206), P3: QATM in the q_s slot
       if ((stages & S_HSEN) && g.hsen) {
@@ -249,8 +258,10 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
           FOR_C h.v[i] = hsen_rco(ta.v[i], ts.v[i], vel.v[i]);
           ST(g.hsen, j0, nt, h);
         } else if (m == FCX_ZERO) {
-          ST(g.hsen, j0, nt, splat<C>(0.0));
+          h = splat<C>(0.0);
+          ST(g.hsen, j0, nt, h);
         }
+        if (av) av[2] = h;
       }
       if constexpr (MERGED) {
         // u and v grids ARE the t grid: QSUR(u/v) = QSUR(t) (same inputs, same method),
@@ -269,8 +280,8 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
         const bool do_v = (stages & S_VMOM) && tp.uv[1].mom;
         if (do_u || do_v) {
           const Vec<C> &a = (m_mo == FCX_MOM5) ? cmom : amom;
-          if (do_u) momentum<C, NT>(m_mo, false, tp.uv[0], ts, ps, u, v, vel, qs, a, j0, nt);
-          if (do_v) momentum<C, NT>(m_mo, true, tp.uv[1], ts, ps, u, v, vel, qs, a, j0, nt);
+          if (do_u) momentum<C, NT>(m_mo, false, tp.uv[0], ts, ps, u, v, vel, qs, a, j0, nt, av ? av + 4 : nullptr);
+          if (do_v) momentum<C, NT>(m_mo, true, tp.uv[1], ts, ps, u, v, vel, qs, a, j0, nt, av ? av + 5 : nullptr);
         }
       }
       // ---- distribute_shortwave_radiation_flux (calc:355-362): RSDR_s = RSDD_0
@@ -306,6 +317,96 @@ __global__ __launch_bounds__(256) void cells_kernel(const Params *__restrict__ P
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u < units; u += stride)
     process<C, MERGED, VAR, NT>(P, corr_m, u * C);
+}
+
+// The T=1 hot path with the exchange -> atmosphere accumulation fused in (AtmosFused).
+// Block-uniform tile loop: tile t covers cells [t*kTile, (t+1)*kTile), lane l cells 2l, 2l+1.
+template <int VAR, bool NT>
+__global__ __launch_bounds__(256) void cells_atmos_kernel(const Params *__restrict__ P,
+                                                          const double *__restrict__ corr_m,
+                                                          const AtmosFused af) {
+  __shared__ int32_t s_idx[kTile];
+  __shared__ double s_p[kFusedFields][kTile];
+  const int64_t n = P->n_max;
+  const int64_t n_tiles = (n + kTile - 1) / kTile;
+  const int tid = threadIdx.x;
+  for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+    const int64_t t0 = tile * kTile;
+    const int64_t j0 = t0 + 2 * tid;
+    Vec<2> av[kFusedFields];
+#pragma unroll
+    for (int k = 0; k < kFusedFields; ++k) av[k] = splat<2>(0.0);
+    if (j0 < n) process<2, true, VAR, NT>(P, corr_m, j0, av);
+    // products w * x of this lane's two cells into LDS (sentinel index past the grid)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int64_t j = j0 + i;
+      const bool in = j < n;
+      const double wj = in ? __builtin_nontemporal_load(af.w + j) : 0.0;
+      s_idx[2 * tid + i] = in ? af.idx[j] : -1;
+#pragma unroll
+      for (int k = 0; k < kFusedFields; ++k) s_p[k][2 * tid + i] = wj * av[k].v[i];
+    }
+    __syncthreads();
+    // every segment that starts in this tile is summed here in link order
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = 2 * tid + i;
+      const int64_t j = t0 + c;
+      if (j >= n) continue;
+      const int32_t a = s_idx[c];
+      const bool starts = (c == 0) ? (j == 0 || af.idx[j - 1] != a) : (s_idx[c - 1] != a);
+      if (!starts) continue;
+      double acc[kFusedFields];
+#pragma unroll
+      for (int k = 0; k < kFusedFields; ++k) acc[k] = 0.0;
+      int e = c;
+      for (; e < kTile && s_idx[e] == a; ++e) {
+#pragma unroll
+        for (int k = 0; k < kFusedFields; ++k) acc[k] = acc[k] + s_p[k][e];
+      }
+      const bool cont = (e == kTile) && (t0 + kTile < n) && af.idx[t0 + kTile] == a;
+#pragma unroll
+      for (int k = 0; k < kFusedFields; ++k) {
+        if (!af.out[k]) continue;
+        if (cont) {
+          af.carry[tile * kFusedFields + k] = acc[k];
+        } else {
+          af.out[k][a] = acc[k];
+          if (a == 0 && af.left >= 0) af.shared[(int64_t)af.left * af.stride + k] = acc[k];
+          if (a == af.n_atmos - 1 && af.right >= 0) af.shared[(int64_t)af.right * af.stride + k] = acc[k];
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// Segments that straddle a tile boundary: continue the carried prefix sum over the next
+// tile's cells (products recomputed from the stored fluxes, same operations, same order).
+__global__ __launch_bounds__(256) void atmos_fixup_kernel(const AtmosFused af, int64_t n) {
+  const int64_t n_tiles = (n + kTile - 1) / kTile;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n_tiles - 1) return;
+  const int64_t end = (t + 1) * kTile;
+  const int32_t a = af.idx[end - 1];
+  if (af.idx[end] != a) return;
+  double acc[kFusedFields];
+#pragma unroll
+  for (int k = 0; k < kFusedFields; ++k) acc[k] = af.out[k] ? af.carry[t * kFusedFields + k] : 0.0;
+  for (int64_t x = end; x < n && af.idx[x] == a; ++x) {
+    const double wx = af.w[x];
+#pragma unroll
+    for (int k = 0; k < kFusedFields; ++k)
+      if (af.out[k]) acc[k] = acc[k] + wx * af.x[k][x];
+  }
+#pragma unroll
+  for (int k = 0; k < kFusedFields; ++k) {
+    if (!af.out[k]) continue;
+    af.out[k][a] = acc[k];
+    if (a == 0 && af.left >= 0) af.shared[(int64_t)af.left * af.stride + k] = acc[k];
+    if (a == af.n_atmos - 1 && af.right >= 0) af.shared[(int64_t)af.right * af.stride + k] = acc[k];
+  }
 }
 
 // do_regridding (basic:463-522) as CSR-by-destination: row d holds the links with
@@ -425,9 +526,29 @@ static void launch_c(const LaunchConfig &lc, int blocks, hipStream_t s, const Pa
   }
 }
 
+template <int VAR>
+static void launch_atm(bool nt, int blocks, hipStream_t s, const Params *dp, const double *corr_m,
+                       const AtmosFused &af) {
+  if (nt)
+    hipLaunchKernelGGL((cells_atmos_kernel<VAR, true>), dim3(blocks), dim3(256), 0, s, dp, corr_m, af);
+  else
+    hipLaunchKernelGGL((cells_atmos_kernel<VAR, false>), dim3(blocks), dim3(256), 0, s, dp, corr_m, af);
+}
+
 int launch_cells(const Params *hp, const Params *dp, const double *corr_m, const LaunchConfig &lc,
-                 void *stream) {
+                 void *stream, const AtmosFused *atm) {
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (atm) {  // fused accumulation: T=1 specialised merged kernel, 2 cells per lane
+    const int64_t tiles = (hp->n_max + kTile - 1) / kTile;
+    const int blocks = (int)std::max<int64_t>(1, lc.max_blocks > 0 ? std::min<int64_t>(tiles, lc.max_blocks) : tiles);
+    switch (lc.variant) {
+      case 1: launch_atm<1>(lc.nontemporal, blocks, s, dp, corr_m, *atm); break;
+      case 2: launch_atm<2>(lc.nontemporal, blocks, s, dp, corr_m, *atm); break;
+      case 3: launch_atm<3>(lc.nontemporal, blocks, s, dp, corr_m, *atm); break;
+      default: return (int)hipErrorInvalidValue;
+    }
+    return (int)hipGetLastError();
+  }
   const int c = lc.cells_per_thread == 1 ? 1 : 2;
   const int64_t units = (hp->n_max + c - 1) / c;
   const int blocks = grid_for(units, lc.max_blocks);
@@ -459,6 +580,15 @@ int launch_atmos_finish(const AtmosArgs &a, int32_t n_boundaries, void *stream) 
   if (!a.shared) return 0;
   hipLaunchKernelGGL(atmos_finish_kernel, dim3(1), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
                      a, n_boundaries);
+  return (int)hipGetLastError();
+}
+
+int launch_atmos_fixup(const AtmosFused &af, int64_t n, void *stream) {
+  const int64_t tiles = (n + kTile - 1) / kTile;
+  if (tiles < 2) return 0;
+  const int blocks = (int)((tiles - 1 + 255) / 256);
+  hipLaunchKernelGGL(atmos_fixup_kernel, dim3(blocks), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     af, n);
   return (int)hipGetLastError();
 }
 

@@ -46,20 +46,60 @@ def shard_case(full, lo, hi, variant, seed=911):
     return case
 
 
-def make_engine(case, la, shared, stride, device="cuda:0"):
+def make_engine(case, la, shared, stride, device="cuda:0", fused=True):
     import torch
     from fcx.engine import Engine
 
     outs = {name: torch.full((max(la.n_atmos, 1),), float("nan"), dtype=torch.float64, device=device)
             for name, _ in FIELDS}
     atmos = {"local": la, "fields": [(2, 1, g, name, outs[name]) for name, g in FIELDS],
-             "shared": (shared, stride)}
-    eng = Engine(case.lf, 1, case.methods, corrections=case.corrections, atmos=atmos)
+             "shared": (shared, stride) if shared is not None else None}
+    # specialize=0 turns the T=1 kernels (and with them the fused accumulation) off
+    eng = Engine(case.lf, 1, case.methods, corrections=case.corrections, atmos=atmos,
+                 options=None if fused else {"specialize": 0})
     return eng, outs
 
 
+@pytest.mark.parametrize("fused", [True, False])
+@pytest.mark.parametrize("variant", ["CCLM", "MOM5", "RCO"])
+def test_atmos_accumulation_bit_exact_single_rank(variant, fused):
+    """One rank owns every cell: fused (tile sums + carried prefixes) and separate (LDS
+    kernel) accumulation both reproduce the sequential SCRIP sum bit for bit."""
+    n = 70_001  # > 100 tiles of 512 cells, segments straddling tile boundaries
+    full, amap, ref = reference(n, variant)
+    la = local_atmos(amap, 0, 1)
+    eng, outs = make_engine(full, la, None, len(FIELDS), fused=fused)
+    eng.upload(PHASE_ALL)
+    eng.run(PHASE_ALL, 7200)
+    eng.synchronize()
+    for name, _ in FIELDS:
+        np.testing.assert_array_equal(outs[name].cpu().numpy(), ref[name], err_msg=name)
+    eng.close()
+
+
+def test_atmos_unsorted_map_uses_csr():
+    """A map whose exchange cells are not ordered by atmosphere cell (CSR with columns)."""
+    n = 9_001
+    full, amap, _ = reference(n, "CCLM")
+    perm = np.random.default_rng(5).permutation(amap.n_atmos).astype(np.int32)
+    idx = perm[amap.atmos_index]
+    from fcx.parallel import LocalAtmos
+
+    la = LocalAtmos(0, n, 0, amap.n_atmos, idx, amap.weight, -1, -1, 0)
+    out = oracle_lib.run_case(full, "c", current_step_time=7200)
+    eng, outs = make_engine(full, la, None, len(FIELDS))
+    eng.upload(PHASE_ALL)
+    eng.run(PHASE_ALL, 7200)
+    eng.synchronize()
+    for name, g in FIELDS:
+        ref = oracle_lib.atmos_accumulate(idx, amap.weight, out[(1, g, name)], amap.n_atmos)
+        np.testing.assert_array_equal(outs[name].cpu().numpy(), ref, err_msg=name)
+    eng.close()
+
+
+@pytest.mark.parametrize("fused", [True, False])
 @pytest.mark.parametrize("variant,world", [("CCLM", 2), ("MOM5", 4), ("RCO", 8)])
-def test_sharded_engines_one_process(variant, world):
+def test_sharded_engines_one_process(variant, world, fused):
     import torch
 
     n = 20_011
@@ -70,7 +110,7 @@ def test_sharded_engines_one_process(variant, world):
         la = local_atmos(amap, r, world)
         shared = torch.zeros(max(world - 1, 1) * stride, dtype=torch.float64, device="cuda:0")
         case = shard_case(full, la.offset, la.offset + la.size, variant)
-        eng, outs = make_engine(case, la, shared, stride)
+        eng, outs = make_engine(case, la, shared, stride, fused=fused)
         engines.append((la, shared, eng, outs))
     for la, shared, eng, outs in engines:
         eng.upload(PHASE_ALL)  # the shard's fields are host arrays
