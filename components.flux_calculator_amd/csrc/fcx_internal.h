@@ -96,11 +96,11 @@ int launch_atmos(const AtmosArgs &a, void *stream);
 
 // Exchange -> atmosphere accumulation fused into the T=1 cells kernel.  The six fluxes it
 // can take from registers, in this order: MEVA HLAT HSEN RBBR UMOM VMOM (out[k] nullptr =
-// not accumulated).  Every 512-cell tile of a block sums the segments that start in it;
+// not accumulated).  Every 128-cell wave tile sums the segments that start in it;
 // a segment running past the tile end leaves its prefix sum in carry[tile][k] and
 // atmos_fixup_kernel continues it over the next tile's cells in link order.
 constexpr int kFusedFields = 6;
-constexpr int kTile = 512;  // cells per block iteration (256 lanes x 2)
+constexpr int kTile = 128;  // cells per wave iteration (64 lanes x 2)
 struct AtmosFused {
   const int32_t *idx;  // local atmosphere cell of every exchange cell (non-decreasing)
   const double *w;

@@ -320,65 +320,112 @@ __global__ __launch_bounds__(256) void cells_kernel(const Params *__restrict__ P
 }
 
 // The T=1 hot path with the exchange -> atmosphere accumulation fused in (AtmosFused).
-// Block-uniform tile loop: tile t covers cells [t*kTile, (t+1)*kTile), lane l cells 2l, 2l+1.
+// Wave-uniform loop over 128-cell wave tiles (lane l: cells 2l, 2l+1).  After the fluxes,
+// each lane forms the products w*x of its two cells; a lane holding the first cell of an
+// atmosphere segment sums the segment forward through its neighbours' products
+// (__shfl_down over up to kSegLanes lanes, no LDS, no block barrier) in link order.
+// A segment that runs past the wave tile leaves its prefix in carry[tile] for the fix-up.
+constexpr int kSegLanes = 4;  // segments of up to 2*kSegLanes+1 cells (planner checks)
+
 template <int VAR, bool NT>
 __global__ __launch_bounds__(256) void cells_atmos_kernel(const Params *__restrict__ P,
                                                           const double *__restrict__ corr_m,
                                                           const AtmosFused af) {
-  __shared__ int32_t s_idx[kTile];
-  __shared__ double s_p[kFusedFields][kTile];
   const int64_t n = P->n_max;
   const int64_t n_tiles = (n + kTile - 1) / kTile;
-  const int tid = threadIdx.x;
-  for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+  const int lane = threadIdx.x & 63;
+  const int64_t waves = (int64_t)gridDim.x * (blockDim.x >> 6);
+  const int64_t wave0 = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  for (int64_t tile = wave0; tile < n_tiles; tile += waves) {
     const int64_t t0 = tile * kTile;
-    const int64_t j0 = t0 + 2 * tid;
+    const int64_t j0 = t0 + 2 * lane;
     Vec<2> av[kFusedFields];
 #pragma unroll
     for (int k = 0; k < kFusedFields; ++k) av[k] = splat<2>(0.0);
     if (j0 < n) process<2, true, VAR, NT>(P, corr_m, j0, av);
-    // products w * x of this lane's two cells into LDS (sentinel index past the grid)
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int64_t j = j0 + i;
-      const bool in = j < n;
-      const double wj = in ? __builtin_nontemporal_load(af.w + j) : 0.0;
-      s_idx[2 * tid + i] = in ? af.idx[j] : -1;
-#pragma unroll
-      for (int k = 0; k < kFusedFields; ++k) s_p[k][2 * tid + i] = wj * av[k].v[i];
+    // products and atmosphere cells of this lane's two cells (-1: past the grid)
+    int32_t a0 = -1, a1 = -1;
+    double w0 = 0.0, w1 = 0.0;
+    if (j0 + 2 <= n) {
+      const int2 ii = *reinterpret_cast<const int2 *>(af.idx + j0);
+      const d2 ww = __builtin_nontemporal_load(reinterpret_cast<const d2 *>(af.w + j0));
+      a0 = ii.x; a1 = ii.y; w0 = ww[0]; w1 = ww[1];
+    } else if (j0 < n) {
+      a0 = af.idx[j0];
+      w0 = af.w[j0];
     }
-    __syncthreads();
-    // every segment that starts in this tile is summed here in link order
+    double p0[kFusedFields], p1[kFusedFields];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int c = 2 * tid + i;
-      const int64_t j = t0 + c;
-      if (j >= n) continue;
-      const int32_t a = s_idx[c];
-      const bool starts = (c == 0) ? (j == 0 || af.idx[j - 1] != a) : (s_idx[c - 1] != a);
-      if (!starts) continue;
-      double acc[kFusedFields];
+    for (int k = 0; k < kFusedFields; ++k) {
+      p0[k] = w0 * av[k].v[0];
+      p1[k] = w1 * av[k].v[1];
+    }
+    // segment starts: slot 0 compares with the previous cell (previous lane's slot 1)
+    const int32_t prev_a1 = __shfl_up(a1, 1);
+    const int32_t before = (lane == 0) ? ((j0 > 0 && j0 <= n) ? af.idx[j0 - 1] : -2) : prev_a1;
+    const bool start0 = a0 >= 0 && a0 != before;
+    const bool start1 = a1 >= 0 && a1 != a0;
+    double acc0[kFusedFields], acc1[kFusedFields];
 #pragma unroll
-      for (int k = 0; k < kFusedFields; ++k) acc[k] = 0.0;
-      int e = c;
-      for (; e < kTile && s_idx[e] == a; ++e) {
+    for (int k = 0; k < kFusedFields; ++k) {
+      acc0[k] = 0.0 + p0[k];
+      acc1[k] = 0.0 + p1[k];
+    }
+    const bool run0 = start0 && a1 == a0;  // the slot-0 segment also covers own slot 1
+    if (run0) {
 #pragma unroll
-        for (int k = 0; k < kFusedFields; ++k) acc[k] = acc[k] + s_p[k][e];
+      for (int k = 0; k < kFusedFields; ++k) acc0[k] = acc0[k] + p1[k];
+    }
+    // does the segment contain the tile's last cell (lane 63, slot 1)?
+    bool reach0 = lane == 63 && run0, reach1 = lane == 63 && start1;
+    bool live0 = run0, live1 = start1;  // still matching at the current neighbour lane
+#pragma unroll
+    for (int d = 1; d <= kSegLanes; ++d) {
+      const int32_t na0 = __shfl_down(a0, d), na1 = __shfl_down(a1, d);
+      const bool inwave = lane + d < 64;
+      const bool m00 = live0 && inwave && na0 == a0;
+      const bool m01 = m00 && na1 == a0;
+      const bool m10 = live1 && inwave && na0 == a1;
+      const bool m11 = m10 && na1 == a1;
+#pragma unroll
+      for (int k = 0; k < kFusedFields; ++k) {
+        const double q0 = __shfl_down(p0[k], d), q1 = __shfl_down(p1[k], d);
+        if (m00) acc0[k] = acc0[k] + q0;
+        if (m01) acc0[k] = acc0[k] + q1;
+        if (m10) acc1[k] = acc1[k] + q0;
+        if (m11) acc1[k] = acc1[k] + q1;
       }
-      const bool cont = (e == kTile) && (t0 + kTile < n) && af.idx[t0 + kTile] == a;
+      if (lane + d == 63) {
+        reach0 = reach0 || m01;
+        reach1 = reach1 || m11;
+      }
+      live0 = m01;
+      live1 = m11;
+    }
+    // a segment that contains the tile's last cell and the next cell continues there
+    const int64_t tend = t0 + kTile;
+    const int32_t next_a = (tend < n) ? af.idx[tend] : -3;
+    const bool end0 = start0 && reach0 && next_a == a0;
+    const bool end1 = start1 && reach1 && next_a == a1;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const bool st = s == 0 ? start0 : start1;
+      if (!st) continue;
+      const int32_t a = s == 0 ? a0 : a1;
+      const bool cont = s == 0 ? end0 : end1;
 #pragma unroll
       for (int k = 0; k < kFusedFields; ++k) {
         if (!af.out[k]) continue;
+        const double v = s == 0 ? acc0[k] : acc1[k];
         if (cont) {
-          af.carry[tile * kFusedFields + k] = acc[k];
+          af.carry[tile * kFusedFields + k] = v;
         } else {
-          af.out[k][a] = acc[k];
-          if (a == 0 && af.left >= 0) af.shared[(int64_t)af.left * af.stride + k] = acc[k];
-          if (a == af.n_atmos - 1 && af.right >= 0) af.shared[(int64_t)af.right * af.stride + k] = acc[k];
+          af.out[k][a] = v;
+          if (a == 0 && af.left >= 0) af.shared[(int64_t)af.left * af.stride + k] = v;
+          if (a == af.n_atmos - 1 && af.right >= 0) af.shared[(int64_t)af.right * af.stride + k] = v;
         }
       }
     }
-    __syncthreads();
   }
 }
 
