@@ -82,12 +82,17 @@ __device__ __forceinline__ Vec<C> splat(double a) {
 #define ST(p, j, n, x) st<C, NT>(p, j, n, x)
 
 // Momentum of one (type, u- or v-grid) cell group; `north` selects VMOM.
-template <int C, bool NT>
+struct NoEmit {
+  template <int C>
+  __device__ __forceinline__ void operator()(int, const Vec<C> &) const {}
+};
+
+template <int C, bool NT, class Emit = NoEmit>
 __device__ __forceinline__ void momentum(int8_t m, bool north, const UVGridPtrs &g,
                                          const Vec<C> &ts, const Vec<C> &ps, const Vec<C> &u,
                                          const Vec<C> &v, const Vec<C> &vel, const Vec<C> &qs,
                                          const Vec<C> &a, int64_t j0, int64_t n,
-                                         Vec<C> *keep = nullptr) {
+                                         const Emit &emit = Emit(), int slot = -1) {
   if (!g.mom) return;
   Vec<C> out;
   if (m == FCX_ZERO) {
@@ -106,7 +111,7 @@ __device__ __forceinline__ void momentum(int8_t m, bool north, const UVGridPtrs 
     return;
   }
   ST(g.mom, j0, n, out);
-  if (keep) *keep = out;
+  if (slot >= 0) emit(slot, out);
 }
 
 // QSUR + momentum on one separate u or v grid (non-merged layout).
@@ -144,9 +149,9 @@ __device__ __forceinline__ void uv_grid(const TypeParams &tp, int k, uint32_t st
 // VAR: 0 = generic (any T, methods read from the parameter block); 1/2/3 = the T=1 hot
 // path of the CCLM / MOM5 / RCO variant with QSUR/MEVA/HSEN/momentum methods fixed at
 // compile time, so the other method paths vanish from the code and its register budget.
-template <int C, bool MERGED, int VAR, bool NT>
+template <int C, bool MERGED, int VAR, bool NT, class Emit = NoEmit>
 __device__ __forceinline__ void process(const Params *__restrict__ P, const double *__restrict__ corr_m,
-                                        int64_t j0, Vec<C> *av = nullptr) {
+                                        int64_t j0, const Emit &emit = Emit()) {
   const uint32_t stages = P->stages;
   const int T = VAR ? 1 : P->num_types;
   const int64_t nt = P->n[0];
@@ -198,10 +203,10 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
         if (tp.m_rbbr == FCX_STBO) {
           FOR_C r.v[i] = rbbr_stbo(ts.v[i]);
           ST(g.rbbr, j0, nt, r);
-          if (av) av[3] = r;
+          emit(3, r);
         } else if (tp.m_rbbr == FCX_ZERO) {
           ST(g.rbbr, j0, nt, splat<C>(0.0));
-          if (av) av[3] = splat<C>(0.0);
+          emit(3, splat<C>(0.0));
         }
       }
       // ---- calc_spec_vapor_surface(t) (calc:37-49)
@@ -228,7 +233,7 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
             FOR_C me.v[i] = me.v[i] + corr.v[i];
           }
           if (g.meva) ST(g.meva, j0, nt, me);
-          if (av) av[0] = me;
+          emit(0, me);
         }
       }
       // ---- calc_flux_heat_latent (calc:135-152)
@@ -244,7 +249,7 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
           h = splat<C>(0.0);
           ST(g.hlat, j0, nt, h);
         }
-        if (av) av[1] = h;
+        if (tp.m_hlat == FCX_WATER || tp.m_hlat == FCX_ICE || tp.m_hlat == FCX_ZERO) emit(1, h);
       }
       // ---- calc_flux_heat_sensible (calc:167-206), P3: QATM in the q_s slot
       if ((stages & S_HSEN) && g.hsen) {
@@ -261,7 +266,7 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
           h = splat<C>(0.0);
           ST(g.hsen, j0, nt, h);
         }
-        if (av) av[2] = h;
+        if (m == FCX_CCLM || m == FCX_MOM5 || m == FCX_RCO || m == FCX_ZERO) emit(2, h);
       }
       if constexpr (MERGED) {
         // u and v grids ARE the t grid: QSUR(u/v) = QSUR(t) (same inputs, same method),
@@ -280,8 +285,8 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
         const bool do_v = (stages & S_VMOM) && tp.uv[1].mom;
         if (do_u || do_v) {
           const Vec<C> &a = (m_mo == FCX_MOM5) ? cmom : amom;
-          if (do_u) momentum<C, NT>(m_mo, false, tp.uv[0], ts, ps, u, v, vel, qs, a, j0, nt, av ? av + 4 : nullptr);
-          if (do_v) momentum<C, NT>(m_mo, true, tp.uv[1], ts, ps, u, v, vel, qs, a, j0, nt, av ? av + 5 : nullptr);
+          if (do_u) momentum<C, NT, Emit>(m_mo, false, tp.uv[0], ts, ps, u, v, vel, qs, a, j0, nt, emit, 4);
+          if (do_v) momentum<C, NT, Emit>(m_mo, true, tp.uv[1], ts, ps, u, v, vel, qs, a, j0, nt, emit, 5);
         }
       }
       // ---- distribute_shortwave_radiation_flux (calc:355-362): RSDR_s = RSDD_0
@@ -320,112 +325,92 @@ __global__ __launch_bounds__(256) void cells_kernel(const Params *__restrict__ P
 }
 
 // The T=1 hot path with the exchange -> atmosphere accumulation fused in (AtmosFused).
-// Wave-uniform loop over 128-cell wave tiles (lane l: cells 2l, 2l+1).  After the fluxes,
-// each lane forms the products w*x of its two cells; a lane holding the first cell of an
-// atmosphere segment sums the segment forward through its neighbours' products
-// (__shfl_down over up to kSegLanes lanes, no LDS, no block barrier) in link order.
-// A segment that runs past the wave tile leaves its prefix in carry[tile] for the fix-up.
-constexpr int kSegLanes = 4;  // segments of up to 2*kSegLanes+1 cells (planner checks)
+// Wave-uniform loop over 128-cell wave tiles (lane l: cells 2l, 2l+1).  Each flux is
+// turned into the product w*x the moment it is produced and parked in the wave's own LDS
+// region (nothing extra stays live in registers); after the cell pass a wave-local fence,
+// then every lane holding the first cell of an atmosphere segment sums the segment from LDS
+// in link order.  A segment that runs past the wave tile leaves its prefix in carry[tile].
+struct LdsEmit {
+  double *p;  // this wave's [kFusedFields][kTile] products
+  double w0, w1;
+  int c;      // 2 * lane
+  template <int C>
+  __device__ __forceinline__ void operator()(int k, const Vec<C> &x) const {
+    p[k * kTile + c] = w0 * x.v[0];
+    p[k * kTile + c + 1] = w1 * x.v[1];
+  }
+};
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 
 template <int VAR, bool NT>
 __global__ __launch_bounds__(256) void cells_atmos_kernel(const Params *__restrict__ P,
                                                           const double *__restrict__ corr_m,
                                                           const AtmosFused af) {
+  __shared__ double s_p[4][kFusedFields * kTile];
+  __shared__ int32_t s_idx[4][kTile];
   const int64_t n = P->n_max;
   const int64_t n_tiles = (n + kTile - 1) / kTile;
-  const int lane = threadIdx.x & 63;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  double *wp = s_p[wv];
+  int32_t *wi = s_idx[wv];
   const int64_t waves = (int64_t)gridDim.x * (blockDim.x >> 6);
-  const int64_t wave0 = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int64_t wave0 = (int64_t)blockIdx.x * (blockDim.x >> 6) + wv;
   for (int64_t tile = wave0; tile < n_tiles; tile += waves) {
     const int64_t t0 = tile * kTile;
     const int64_t j0 = t0 + 2 * lane;
-    Vec<2> av[kFusedFields];
-#pragma unroll
-    for (int k = 0; k < kFusedFields; ++k) av[k] = splat<2>(0.0);
-    if (j0 < n) process<2, true, VAR, NT>(P, corr_m, j0, av);
-    // products and atmosphere cells of this lane's two cells (-1: past the grid)
+    LdsEmit emit{wp, 0.0, 0.0, 2 * lane};
     int32_t a0 = -1, a1 = -1;
-    double w0 = 0.0, w1 = 0.0;
     if (j0 + 2 <= n) {
       const int2 ii = *reinterpret_cast<const int2 *>(af.idx + j0);
       const d2 ww = __builtin_nontemporal_load(reinterpret_cast<const d2 *>(af.w + j0));
-      a0 = ii.x; a1 = ii.y; w0 = ww[0]; w1 = ww[1];
+      a0 = ii.x;
+      a1 = ii.y;
+      emit.w0 = ww[0];
+      emit.w1 = ww[1];
     } else if (j0 < n) {
       a0 = af.idx[j0];
-      w0 = af.w[j0];
+      emit.w0 = af.w[j0];
     }
-    double p0[kFusedFields], p1[kFusedFields];
-#pragma unroll
-    for (int k = 0; k < kFusedFields; ++k) {
-      p0[k] = w0 * av[k].v[0];
-      p1[k] = w1 * av[k].v[1];
-    }
-    // segment starts: slot 0 compares with the previous cell (previous lane's slot 1)
-    const int32_t prev_a1 = __shfl_up(a1, 1);
-    const int32_t before = (lane == 0) ? ((j0 > 0 && j0 <= n) ? af.idx[j0 - 1] : -2) : prev_a1;
-    const bool start0 = a0 >= 0 && a0 != before;
-    const bool start1 = a1 >= 0 && a1 != a0;
-    double acc0[kFusedFields], acc1[kFusedFields];
-#pragma unroll
-    for (int k = 0; k < kFusedFields; ++k) {
-      acc0[k] = 0.0 + p0[k];
-      acc1[k] = 0.0 + p1[k];
-    }
-    const bool run0 = start0 && a1 == a0;  // the slot-0 segment also covers own slot 1
-    if (run0) {
-#pragma unroll
-      for (int k = 0; k < kFusedFields; ++k) acc0[k] = acc0[k] + p1[k];
-    }
-    // does the segment contain the tile's last cell (lane 63, slot 1)?
-    bool reach0 = lane == 63 && run0, reach1 = lane == 63 && start1;
-    bool live0 = run0, live1 = start1;  // still matching at the current neighbour lane
-#pragma unroll
-    for (int d = 1; d <= kSegLanes; ++d) {
-      const int32_t na0 = __shfl_down(a0, d), na1 = __shfl_down(a1, d);
-      const bool inwave = lane + d < 64;
-      const bool m00 = live0 && inwave && na0 == a0;
-      const bool m01 = m00 && na1 == a0;
-      const bool m10 = live1 && inwave && na0 == a1;
-      const bool m11 = m10 && na1 == a1;
-#pragma unroll
-      for (int k = 0; k < kFusedFields; ++k) {
-        const double q0 = __shfl_down(p0[k], d), q1 = __shfl_down(p1[k], d);
-        if (m00) acc0[k] = acc0[k] + q0;
-        if (m01) acc0[k] = acc0[k] + q1;
-        if (m10) acc1[k] = acc1[k] + q0;
-        if (m11) acc1[k] = acc1[k] + q1;
-      }
-      if (lane + d == 63) {
-        reach0 = reach0 || m01;
-        reach1 = reach1 || m11;
-      }
-      live0 = m01;
-      live1 = m11;
-    }
-    // a segment that contains the tile's last cell and the next cell continues there
+    wi[2 * lane] = a0;
+    wi[2 * lane + 1] = a1;
+    if (j0 < n) process<2, true, VAR, NT>(P, corr_m, j0, emit);
+    wave_sync();  // the wave's LDS products are visible to all its lanes
     const int64_t tend = t0 + kTile;
     const int32_t next_a = (tend < n) ? af.idx[tend] : -3;
-    const bool end0 = start0 && reach0 && next_a == a0;
-    const bool end1 = start1 && reach1 && next_a == a1;
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const bool st = s == 0 ? start0 : start1;
-      if (!st) continue;
-      const int32_t a = s == 0 ? a0 : a1;
-      const bool cont = s == 0 ? end0 : end1;
+    for (int i = 0; i < 2; ++i) {
+      const int c = 2 * lane + i;
+      const int32_t a = wi[c];
+      if (a < 0) continue;
+      const int32_t before = (c == 0) ? (t0 > 0 ? af.idx[t0 - 1] : -2) : wi[c - 1];
+      if (before == a) continue;  // not the first cell of its segment
+      double acc[kFusedFields];
+#pragma unroll
+      for (int k = 0; k < kFusedFields; ++k) acc[k] = 0.0;
+      int e = c;
+      for (; e < kTile && wi[e] == a; ++e) {
+#pragma unroll
+        for (int k = 0; k < kFusedFields; ++k) acc[k] = acc[k] + wp[k * kTile + e];
+      }
+      const bool cont = e == kTile && next_a == a;
 #pragma unroll
       for (int k = 0; k < kFusedFields; ++k) {
         if (!af.out[k]) continue;
-        const double v = s == 0 ? acc0[k] : acc1[k];
         if (cont) {
-          af.carry[tile * kFusedFields + k] = v;
+          af.carry[tile * kFusedFields + k] = acc[k];
         } else {
-          af.out[k][a] = v;
-          if (a == 0 && af.left >= 0) af.shared[(int64_t)af.left * af.stride + k] = v;
-          if (a == af.n_atmos - 1 && af.right >= 0) af.shared[(int64_t)af.right * af.stride + k] = v;
+          af.out[k][a] = acc[k];
+          if (a == 0 && af.left >= 0) af.shared[(int64_t)af.left * af.stride + k] = acc[k];
+          if (a == af.n_atmos - 1 && af.right >= 0) af.shared[(int64_t)af.right * af.stride + k] = acc[k];
         }
       }
     }
+    wave_sync();  // every lane is done reading before the next tile overwrites the region
   }
 }
 
