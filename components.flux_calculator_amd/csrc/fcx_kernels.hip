@@ -336,8 +336,8 @@ struct LdsEmit {
   int c;      // 2 * lane
   template <int C>
   __device__ __forceinline__ void operator()(int k, const Vec<C> &x) const {
-    p[k * kTile + c] = w0 * x.v[0];
-    p[k * kTile + c + 1] = w1 * x.v[1];
+    const d2 q = {w0 * x.v[0], w1 * x.v[1]};  // one 16-B LDS store per field
+    *reinterpret_cast<d2 *>(p + k * kTile + c) = q;
   }
 };
 
