@@ -49,6 +49,8 @@ def parse():
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--atmos", type=int, default=1,
                    help="exchange->atmosphere accumulation (+ one RCCL all-reduce when N>1)")
+    p.add_argument("--precision", choices=("f64", "f32"), default="f64",
+                   help="f32: the fp32 cell-pass variant (config 5; no atmosphere accumulation)")
     return p.parse_args()
 
 
@@ -101,7 +103,13 @@ def main():
     from fcx.basic import PHASE_ALL, PHASE_NORMAL
     from fcx.engine import Engine
     from fcx.parallel import PeriodicAtmosMap, apple_range
-    from fcx.synthetic import BASE_SEED, build_case, inputs_for_bench
+    from fcx.synthetic import BASE_SEED, as_dtype, build_case, inputs_for_bench
+    sys.path.insert(0, os.path.join(ROOT, "components.flux_calculator_amd", "bench"))
+    from pmc_traffic import traffic_key
+
+    f32 = args.precision == "f32"
+    if f32:
+        args.atmos = 0  # the accumulation runs in fp64 only (fcx.h fcx_set_precision)
 
     # this rank's APPLE range of the global grid (decomp_def.F90:23-31): weak scaling,
     # every rank owns args.cells cells; the seed follows the global offset
@@ -111,6 +119,8 @@ def main():
     assert size == n
     host = inputs_for_bench(n, seed=BASE_SEED + offset)
     data = {k: torch.as_tensor(v).to(dev) for k, v in host.items()}
+    if f32:  # inputs rounded once; every variant's case shares them
+        data = {k: v.float() for k, v in data.items()}
     del host
     stream = torch.cuda.current_stream(dev)
 
@@ -125,6 +135,8 @@ def main():
     for i, v in enumerate(variants):
         c = build_case(v, n=n, T=args.types, bias=args.bias, device=dev,
                        data=data if args.types == 1 else None)
+        if f32:
+            c = as_dtype(c, "float32")
         atmos = None
         if la is not None:
             outs = {name: torch.empty(max(la.n_atmos, 1), dtype=torch.float64, device=dev)
@@ -137,10 +149,9 @@ def main():
                    options={"atmos_in_run": 0})
         cases.append(c)
         engines.append(e)
-    alg_bytes = [e.algorithmic_bytes(PHASE_ALL) for e in engines]  # the cells kernel alone
-    atm_bytes = 0
-    if la is not None:  # weights + re-read fields + atmosphere outputs, per variant
-        atm_bytes = n * 8 + (la.n_atmos + 1) * 4 + stride * (n + la.n_atmos) * 8
+    # algorithmic bytes of one fcx_run: every distinct field array read once / written once,
+    # plus (fused accumulation) 4+8 B/cell of atmosphere index and weight and the outputs
+    alg_bytes = [e.algorithmic_bytes(PHASE_ALL) for e in engines]
 
     def step(t, events=None):
         for i, e in enumerate(engines):
@@ -197,8 +208,8 @@ def main():
     if os.path.exists(tfile):
         try:
             t = json.load(open(tfile))
-            key = f"{variants[dom]}:{n}:T{args.types}:bias{int(args.bias)}"
-            traffic = t.get(key)
+            traffic = t.get(traffic_key(variants[dom], n, args.types, args.bias, la is not None,
+                                        args.precision))
         except Exception:
             traffic = None
 
@@ -213,12 +224,13 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f64",
+        "dtype": args.precision,
         "data": "synthetic (SURVEY.md 8d distributions, seeded PCG64)",
         "config": {
-            "workload": "config3/4: synthetic exchange grid, CCLM+MOM5+RCO fused flux kernels "
-                        "back-to-back per coupling step + exchange->atmosphere accumulation, "
-                        "inputs HBM-resident",
+            "workload": ("config3/4: synthetic exchange grid, CCLM+MOM5+RCO fused flux kernels "
+                         "back-to-back per coupling step"
+                         + (" + exchange->atmosphere accumulation" if la is not None else "")
+                         + (", fp32 variant (config 5)" if f32 else "") + ", inputs HBM-resident"),
             "cells_per_gpu": n,
             "cells_per_step": cells_per_step,
             "variants": list(variants),
@@ -229,11 +241,11 @@ def main():
             "atmos_accumulation": (f"6 fluxes -> {la.n_atmos} atmosphere cells per GPU (1 per ~4 "
                                    "exchange cells), one all-reduce of the shared boundary cells per step"
                                    if la is not None else "off"),
-            "atmos_alg_bytes_per_variant": int(atm_bytes),
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": f"cells_kernel[{variants[dom]}]",
+            "kernel": (f"cells_atmos_kernel[{variants[dom]}]+atmos_fixup" if la is not None
+                       else f"cells_kernel[{variants[dom]}]"),
             "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",

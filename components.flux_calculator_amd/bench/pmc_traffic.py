@@ -22,17 +22,32 @@ from collections import defaultdict
 VARIANTS = {"1": "CCLM", "2": "MOM5", "3": "RCO", "0": "generic"}
 
 
+def kernel_key(name):
+    """(variant, atmos fused, dtype) of a cells kernel, or None for any other kernel."""
+    m = re.search(r"cells_kernel<(\d), (true|false), (\d), (true|false), (double|float)>", name)
+    if m:
+        return VARIANTS[m.group(3)], 0, "f64" if m.group(5) == "double" else "f32"
+    m = re.search(r"cells_atmos_kernel<(\d), (true|false)>", name)
+    if m:
+        return VARIANTS[m.group(1)], 1, "f64"
+    return None
+
+
 def read_counter(d, name):
     rows = []
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         rows += [r for r in csv.DictReader(open(f)) if r.get("Counter_Name") == name]
     per = defaultdict(list)
     for r in rows:
-        m = re.search(r"cells_kernel<(\d), (true|false), (\d), (true|false)>", r["Kernel_Name"])
-        if not m:
-            continue
-        per[VARIANTS[m.group(3)]].append(float(r["Counter_Value"]))
+        k = kernel_key(r["Kernel_Name"])
+        if k is not None:
+            per[k].append(float(r["Counter_Value"]))
     return per
+
+
+def traffic_key(variant, cells, types, bias, atmos, dtype):
+    """profiles/traffic.json key (bench.py looks the dominant kernel up by it)."""
+    return f"{variant}:{cells}:T{types}:bias{int(bias)}:atmos{int(atmos)}:{dtype}"
 
 
 def main():
@@ -47,13 +62,16 @@ def main():
     fetch = read_counter(os.path.join(a.dir, "fetch"), "FETCH_SIZE")
     write = read_counter(os.path.join(a.dir, "write"), "WRITE_SIZE")
     out = json.load(open(a.out)) if os.path.exists(a.out) else {}
-    for v in sorted(set(fetch) & set(write)):
-        f = sum(fetch[v]) / len(fetch[v]) * 1024 * 2  # KiB -> B, gfx950 x2 read correction
-        w = sum(write[v]) / len(write[v]) * 1024
-        key = f"{v}:{a.cells}:T{a.types}:bias{a.bias}"
+    for k in sorted(set(fetch) & set(write)):
+        v, atm, dt = k
+        # KiB -> B, gfx950 x2 read correction (calibrated for 16 B/lane streaming reads; the
+        # fused kernel's 8 B/lane atmosphere-index reads are 4 of its ~150 B/cell)
+        f = sum(fetch[k]) / len(fetch[k]) * 1024 * 2
+        w = sum(write[k]) / len(write[k]) * 1024
+        key = traffic_key(v, a.cells, a.types, a.bias, atm, dt)
         out[key] = round(f + w)
         print(key, "read", round(f / a.cells, 2), "B/cell", "write", round(w / a.cells, 2), "B/cell",
-              "launches", len(fetch[v]))
+              "launches", len(fetch[k]))
     json.dump(out, open(a.out, "w"), indent=1, sort_keys=True)
 
 

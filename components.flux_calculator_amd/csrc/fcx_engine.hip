@@ -92,11 +92,13 @@ struct fcx_engine {
   bool committed = false;
   bool any_regrid = false;
   bool aligned16 = true;
+  bool f32 = false;       // FCX_PRECISION_F32: float fields, fp32 kernels
+  size_t esize = 8;       // bytes per field element
   // bias corrections (bias_corrections.F90)
   bool lcorr = false;
   int32_t init_date = 0;
   std::vector<double> corr_mm;  // [12][n_t]
-  double *corr_dev = nullptr;
+  void *corr_dev = nullptr;  // [12][n_t] in the engine precision
   Csr rg[4];
   std::vector<std::pair<int, std::pair<int, int>>> averages;  // (phase, (grid, var))
   std::map<std::pair<uint32_t, int>, Plan> plans;               // (stages, avg phase mask)
@@ -758,10 +760,26 @@ static int get_plan(fcx_engine *e, uint32_t stages, int avg_phases, Plan **pl) {
   return FCX_OK;
 }
 
+extern "C" int fcx_set_precision(fcx_engine *e, int precision) {
+  if (!e) return fail(FCX_E_ARG, "NULL engine");
+  if (e->committed) return fail(FCX_E_STATE, "engine already committed");
+  if (precision != FCX_PRECISION_F64 && precision != FCX_PRECISION_F32)
+    return fail(FCX_E_ARG, "precision %d unknown", precision);
+  e->f32 = precision == FCX_PRECISION_F32;
+  e->esize = e->f32 ? sizeof(float) : sizeof(double);
+  return FCX_OK;
+}
+
 extern "C" int fcx_commit(fcx_engine *e) {
   if (!e) return fail(FCX_E_ARG, "NULL engine");
   if (e->committed) return FCX_OK;
   if (int r = validate(e)) return r;
+  if (e->f32) {
+    bool rg = e->any_regrid;
+    for (auto &c : e->rg) rg = rg || c.set;
+    if (rg) return fail(FCX_E_UNSUPPORTED, "fp32 engine: regridding runs in fp64 only");
+    if (e->n_atmos >= 0) return fail(FCX_E_UNSUPPORTED, "fp32 engine: the atmosphere accumulation runs in fp64 only");
+  }
   if (int r = gpu_init(e)) return r;
   // one pooled allocation for all host-bound mirrors, 256-B aligned sub-buffers
   size_t total = 0;
@@ -769,7 +787,7 @@ extern "C" int fcx_commit(fcx_engine *e) {
   for (size_t b = 0; b < e->bufs.size(); ++b) {
     if (e->bufs[b].external) continue;
     off[b] = total;
-    total += ((size_t)e->bufs[b].n * sizeof(double) + 255) / 256 * 256;
+    total += ((size_t)e->bufs[b].n * e->esize + 255) / 256 * 256;
   }
   if (total) {
     hipError_t err = hipMalloc(&e->pool, total);
@@ -779,9 +797,14 @@ extern "C" int fcx_commit(fcx_engine *e) {
       if (!e->bufs[b].external) e->bufs[b].dev = reinterpret_cast<double *>((char *)e->pool + off[b]);
   }
   if (e->lcorr) {
-    HIP_TRY(hipMalloc(&e->corr_dev, std::max<size_t>(e->corr_mm.size(), 1) * sizeof(double)));
-    HIP_TRY(hipMemcpy(e->corr_dev, e->corr_mm.data(), e->corr_mm.size() * sizeof(double),
-                      hipMemcpyHostToDevice));
+    HIP_TRY(hipMalloc(&e->corr_dev, std::max<size_t>(e->corr_mm.size(), 1) * e->esize));
+    if (e->f32) {  // rounded once; the fp32 kernels add them in fp32
+      std::vector<float> cf(e->corr_mm.begin(), e->corr_mm.end());
+      HIP_TRY(hipMemcpy(e->corr_dev, cf.data(), cf.size() * sizeof(float), hipMemcpyHostToDevice));
+    } else {
+      HIP_TRY(hipMemcpy(e->corr_dev, e->corr_mm.data(), e->corr_mm.size() * sizeof(double),
+                        hipMemcpyHostToDevice));
+    }
   }
   for (auto &c : e->rg) {
     if (!c.set) continue;
@@ -848,7 +871,7 @@ static const double *month_slice(fcx_engine *e, int32_t t, int *rc) {
   if (!e->lcorr) return nullptr;
   int32_t m = 0;
   if ((*rc = fcx_current_month(e->init_date, t, &m)) != FCX_OK) return nullptr;
-  return e->corr_dev + (size_t)(m - 1) * e->n[0];
+  return reinterpret_cast<const double *>((const char *)e->corr_dev + (size_t)(m - 1) * e->n[0] * e->esize);
 }
 
 static int copy_bufs(fcx_engine *e, const std::vector<int> &ids, bool h2d) {
@@ -856,9 +879,9 @@ static int copy_bufs(fcx_engine *e, const std::vector<int> &ids, bool h2d) {
     const Buffer &bf = e->bufs[b];
     if (bf.external || bf.n == 0) continue;
     if (h2d)
-      HIP_TRY(hipMemcpyAsync(bf.dev, bf.host, bf.n * sizeof(double), hipMemcpyHostToDevice, e->stream));
+      HIP_TRY(hipMemcpyAsync(bf.dev, bf.host, bf.n * e->esize, hipMemcpyHostToDevice, e->stream));
     else
-      HIP_TRY(hipMemcpyAsync(bf.host, bf.dev, bf.n * sizeof(double), hipMemcpyDeviceToHost, e->stream));
+      HIP_TRY(hipMemcpyAsync(bf.host, bf.dev, bf.n * e->esize, hipMemcpyDeviceToHost, e->stream));
   }
   return FCX_OK;
 }
@@ -869,6 +892,7 @@ static int launch_plan(fcx_engine *e, Plan *pl, const double *corr_m) {
   if (!e->aligned16) lc.cells_per_thread = 1;
   lc.merged = pl->host.merged_uv != 0;
   lc.variant = (e->specialize && lc.merged) ? pl->variant : 0;
+  lc.f32 = e->f32;
   const bool fused = pl->atm_fused && lc.variant && lc.cells_per_thread == 2;
   if (fused) {  // the shared-slot pointers may have been set after the plan was built
     pl->af.shared = e->atm_shared;
@@ -1147,7 +1171,7 @@ extern "C" int fcx_algorithmic_bytes(fcx_engine *e, int phase, int64_t *bytes) {
     extra += e->n[0] * 8 + (e->atm_contiguous ? 0 : e->n[0] * 4) + (e->n_atmos + 1) * 4;
     extra += (int64_t)nf * (e->n[0] + e->n_atmos) * 8;
   }
-  *bytes = b * (int64_t)sizeof(double) + extra;
+  *bytes = b * (int64_t)e->esize + extra;
   return FCX_OK;
 }
 

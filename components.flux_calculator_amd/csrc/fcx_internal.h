@@ -73,6 +73,7 @@ struct LaunchConfig {
   bool nontemporal = true;   // non-temporal hint on the streamed loads/stores
   bool merged = false;       // u/v grids are the t grid
   int variant = 0;           // 0 generic, 1 CCLM, 2 MOM5, 3 RCO (T=1 specialisations)
+  bool f32 = false;          // fp32 fields (FCX_PRECISION_F32): 4 cells per lane
 };
 
 struct AtmosFused;

@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 #include "fcx_internal.h"
 #include "fcx_physics.h"
 
@@ -25,38 +26,46 @@
 
 namespace fcx {
 
-template <int C>
+// C cells of one lane in the arithmetic type R.  The fp64 path holds 2 cells per lane and
+// the fp32 path 4, so one lane's access to an array is a single 16-B dwordx4 either way.
+template <int C, class R = double>
 struct Vec {
-  double v[C];
+  R v[C];
 };
 
 typedef double d2 __attribute__((ext_vector_type(2)));
+typedef float f4 __attribute__((ext_vector_type(4)));
 
 // NT: streamed once -> non-temporal hint (the arrays are read once and written once per
-// step; the 256 MB Infinity Cache cannot hold a 10M-cell step anyway)
-template <int C, bool NT>
-__device__ __forceinline__ Vec<C> ld(const double *__restrict__ p, int64_t j0, int64_t n) {
-  Vec<C> r;
-  if constexpr (C == 2) {
-    if (j0 + 2 <= n) {
-      const d2 *q = reinterpret_cast<const d2 *>(p + j0);
-      const d2 t = NT ? __builtin_nontemporal_load(q) : *q;
-      r.v[0] = t[0];
-      r.v[1] = t[1];
+// step; the 256 MB Infinity Cache cannot hold a 10M-cell step anyway).  Out-of-range lanes
+// of a partial vector read 1 (keeps exp/pow/division of the dead lanes finite).
+template <int C, bool NT, class R>
+__device__ __forceinline__ Vec<C, R> ld(const R *__restrict__ p, int64_t j0, int64_t n) {
+  Vec<C, R> r;
+  if constexpr (C * sizeof(R) == 16) {
+    if (j0 + C <= n) {
+      using V = typename std::conditional<sizeof(R) == 8, d2, f4>::type;
+      const V *q = reinterpret_cast<const V *>(p + j0);
+      const V t = NT ? __builtin_nontemporal_load(q) : *q;
+#pragma unroll
+      for (int i = 0; i < C; ++i) r.v[i] = t[i];
       return r;
     }
   }
 #pragma unroll
-  for (int i = 0; i < C; ++i) r.v[i] = (j0 + i < n) ? p[j0 + i] : 1.0;
+  for (int i = 0; i < C; ++i) r.v[i] = (j0 + i < n) ? p[j0 + i] : R(1);
   return r;
 }
 
-template <int C, bool NT>
-__device__ __forceinline__ void st(double *__restrict__ p, int64_t j0, int64_t n, const Vec<C> &x) {
-  if constexpr (C == 2) {
-    if (j0 + 2 <= n) {
-      d2 *q = reinterpret_cast<d2 *>(p + j0);
-      const d2 t = {x.v[0], x.v[1]};
+template <int C, bool NT, class R>
+__device__ __forceinline__ void st(R *__restrict__ p, int64_t j0, int64_t n, const Vec<C, R> &x) {
+  if constexpr (C * sizeof(R) == 16) {
+    if (j0 + C <= n) {
+      using V = typename std::conditional<sizeof(R) == 8, d2, f4>::type;
+      V *q = reinterpret_cast<V *>(p + j0);
+      V t;
+#pragma unroll
+      for (int i = 0; i < C; ++i) t[i] = x.v[i];
       if (NT)
         __builtin_nontemporal_store(t, q);
       else
@@ -69,42 +78,44 @@ __device__ __forceinline__ void st(double *__restrict__ p, int64_t j0, int64_t n
     if (j0 + i < n) p[j0 + i] = x.v[i];
 }
 
-template <int C>
-__device__ __forceinline__ Vec<C> splat(double a) {
-  Vec<C> r;
+template <int C, class R>
+__device__ __forceinline__ Vec<C, R> splat(R a) {
+  Vec<C, R> r;
 #pragma unroll
   for (int i = 0; i < C; ++i) r.v[i] = a;
   return r;
 }
 
+// The parameter block holds every field pointer as double*; in the fp32 engine the same
+// pointers address float arrays, so every access reinterprets them as R*.
 #define FOR_C _Pragma("unroll") for (int i = 0; i < C; ++i)
-#define LD(p, j, n) ld<C, NT>(p, j, n)
-#define ST(p, j, n, x) st<C, NT>(p, j, n, x)
+#define LD(p, j, n) ld<C, NT, R>(reinterpret_cast<const R *>(p), j, n)
+#define ST(p, j, n, ...) st<C, NT, R>(reinterpret_cast<R *>(p), j, n, __VA_ARGS__)
 
 // Momentum of one (type, u- or v-grid) cell group; `north` selects VMOM.
 struct NoEmit {
-  template <int C>
-  __device__ __forceinline__ void operator()(int, const Vec<C> &) const {}
+  template <int C, class R>
+  __device__ __forceinline__ void operator()(int, const Vec<C, R> &) const {}
 };
 
-template <int C, bool NT, class Emit = NoEmit>
+template <int C, bool NT, class R, class Emit = NoEmit>
 __device__ __forceinline__ void momentum(int8_t m, bool north, const UVGridPtrs &g,
-                                         const Vec<C> &ts, const Vec<C> &ps, const Vec<C> &u,
-                                         const Vec<C> &v, const Vec<C> &vel, const Vec<C> &qs,
-                                         const Vec<C> &a, int64_t j0, int64_t n,
+                                         const Vec<C, R> &ts, const Vec<C, R> &ps, const Vec<C, R> &u,
+                                         const Vec<C, R> &v, const Vec<C, R> &vel, const Vec<C, R> &qs,
+                                         const Vec<C, R> &a, int64_t j0, int64_t n,
                                          const Emit &emit = Emit(), int slot = -1) {
   if (!g.mom) return;
-  Vec<C> out;
+  Vec<C, R> out;
   if (m == FCX_ZERO) {
-    out = splat<C>(0.0);
+    out = splat<C, R>(R(0));
   } else if (m == FCX_CCLM || m == FCX_MOM5) {
     FOR_C {
-      const double rate = mom_cclm_rate(a.v[i], ps.v[i], qs.v[i], ts.v[i], vel.v[i]);
+      const R rate = mom_cclm_rate(a.v[i], ps.v[i], qs.v[i], ts.v[i], vel.v[i]);
       out.v[i] = -(rate * (north ? v.v[i] : u.v[i]));
     }
   } else if (m == FCX_RCO) {
     FOR_C {
-      const double rate = mom_rco_rate(vel.v[i]);
+      const R rate = mom_rco_rate(vel.v[i]);
       out.v[i] = -(rate * (north ? v.v[i] : u.v[i]));
     }
   } else {
@@ -115,7 +126,7 @@ __device__ __forceinline__ void momentum(int8_t m, bool north, const UVGridPtrs 
 }
 
 // QSUR + momentum on one separate u or v grid (non-merged layout).
-template <int C, bool NT>
+template <int C, bool NT, class R>
 __device__ __forceinline__ void uv_grid(const TypeParams &tp, int k, uint32_t stages, int64_t j0,
                                         int64_t n) {
   const UVGridPtrs &g = tp.uv[k];
@@ -124,7 +135,7 @@ __device__ __forceinline__ void uv_grid(const TypeParams &tp, int k, uint32_t st
   const bool do_q = (stages & s_qsur) && tp.m_qsur[1 + k] == FCX_CCLM && g.qsur;
   const bool do_m = (stages & s_mom) && g.mom;
   if (!do_q && !do_m) return;
-  Vec<C> ts = {}, fi = {}, ps = {}, u = {}, v = {}, a = {}, qs = {};
+  Vec<C, R> ts = {}, fi = {}, ps = {}, u = {}, v = {}, a = {}, qs = {};
   if (g.tsur) ts = LD(g.tsur, j0, n);
   if (g.psur) ps = LD(g.psur, j0, n);
   if (do_q) fi = LD(g.fice, j0, n);
@@ -140,25 +151,25 @@ __device__ __forceinline__ void uv_grid(const TypeParams &tp, int k, uint32_t st
     ST(g.qsur, j0, n, qs);
   }
   if (do_m) {
-    Vec<C> vel;
+    Vec<C, R> vel;
     FOR_C vel.v[i] = wind(u.v[i], v.v[i]);
-    momentum<C, NT>(tp.m_mom, k == 1, g, ts, ps, u, v, vel, qs, a, j0, n);
+    momentum<C, NT, R>(tp.m_mom, k == 1, g, ts, ps, u, v, vel, qs, a, j0, n);
   }
 }
 
 // VAR: 0 = generic (any T, methods read from the parameter block); 1/2/3 = the T=1 hot
 // path of the CCLM / MOM5 / RCO variant with QSUR/MEVA/HSEN/momentum methods fixed at
 // compile time, so the other method paths vanish from the code and its register budget.
-template <int C, bool MERGED, int VAR, bool NT, class Emit = NoEmit>
+template <int C, bool MERGED, int VAR, bool NT, class R = double, class Emit = NoEmit>
 __device__ __forceinline__ void process(const Params *__restrict__ P, const double *__restrict__ corr_m,
                                         int64_t j0, const Emit &emit = Emit()) {
   const uint32_t stages = P->stages;
   const int T = VAR ? 1 : P->num_types;
   const int64_t nt = P->n[0];
   const bool do_t = j0 < nt;
-  Vec<C> corr = {};
+  Vec<C, R> corr = {};
   if (do_t && corr_m && (stages & S_MEVA)) corr = LD(corr_m, j0, nt);
-  Vec<C> rsdd = {};
+  Vec<C, R> rsdd = {};
   if (do_t && P->rsdd0 && (stages & S_RSDR)) rsdd = LD(P->rsdd0, j0, nt);
 
   for (int s = 0; s < T; ++s) {
@@ -173,7 +184,7 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
     const int8_t m_mo = VAR ? kVarMethod : tp.m_mom;
     if (do_t) {
       // ---- load every t-grid input this type needs (before any store of this type)
-      Vec<C> ts = {}, fi = {}, ps = {}, pa = {}, qa = {}, ta = {}, u = {}, v = {}, amoi = {},
+      Vec<C, R> ts = {}, fi = {}, ps = {}, pa = {}, qa = {}, ta = {}, u = {}, v = {}, amoi = {},
              cmoi = {}, chea = {}, qs = {}, me = {};
       if (g.tsur) ts = LD(g.tsur, j0, nt);
       if (g.fice) fi = LD(g.fice, j0, nt);
@@ -188,25 +199,25 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
       if (g.chea) chea = LD(g.chea, j0, nt);
       if (g.qsur_in) qs = LD(g.qsur_in, j0, nt);
       if (g.meva_in) me = LD(g.meva_in, j0, nt);
-      Vec<C> amom = {}, cmom = {};
+      Vec<C, R> amom = {}, cmom = {};
       if constexpr (MERGED) {
         const UVGridPtrs &gu = tp.uv[0];
         if (gu.amom) amom = LD(gu.amom, j0, nt);
         if (gu.cmom) cmom = LD(gu.cmom, j0, nt);
       }
-      Vec<C> vel;
+      Vec<C, R> vel;
       FOR_C vel.v[i] = wind(u.v[i], v.v[i]);
 
       // ---- calc_flux_radiation_blackbody (calc:331-343)
       if ((stages & S_RBBR) && g.rbbr) {
-        Vec<C> r;
+        Vec<C, R> r;
         if (tp.m_rbbr == FCX_STBO) {
           FOR_C r.v[i] = rbbr_stbo(ts.v[i]);
           ST(g.rbbr, j0, nt, r);
           emit(3, r);
         } else if (tp.m_rbbr == FCX_ZERO) {
-          ST(g.rbbr, j0, nt, splat<C>(0.0));
-          emit(3, splat<C>(0.0));
+          ST(g.rbbr, j0, nt, splat<C, R>(R(0)));
+          emit(3, splat<C, R>(R(0)));
         }
       }
       // ---- calc_spec_vapor_surface(t) (calc:37-49)
@@ -219,9 +230,9 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
         const int8_t m = m_me;
         bool have = true;
         if (m == FCX_ZERO) {
-          me = splat<C>(0.0);
+          me = splat<C, R>(R(0));
         } else if (m == FCX_CCLM || m == FCX_MOM5) {
-          const Vec<C> &a = (m == FCX_CCLM) ? amoi : cmoi;
+          const Vec<C, R> &a = (m == FCX_CCLM) ? amoi : cmoi;
           FOR_C me.v[i] = meva_cclm(a.v[i], ps.v[i], qa.v[i], qs.v[i], ta.v[i], vel.v[i]);
         } else if (m == FCX_RCO) {
           FOR_C me.v[i] = meva_rco(qa.v[i], ts.v[i], vel.v[i]);
@@ -238,15 +249,15 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
       }
       // ---- calc_flux_heat_latent (calc:135-152)
       if ((stages & S_HLAT) && g.hlat) {
-        Vec<C> h;
+        Vec<C, R> h;
         if (tp.m_hlat == FCX_WATER) {
-          FOR_C h.v[i] = me.v[i] * kLv;
+          FOR_C h.v[i] = me.v[i] * R(kLv);
           ST(g.hlat, j0, nt, h);
         } else if (tp.m_hlat == FCX_ICE) {
-          FOR_C h.v[i] = me.v[i] * kLs;
+          FOR_C h.v[i] = me.v[i] * R(kLs);
           ST(g.hlat, j0, nt, h);
         } else if (tp.m_hlat == FCX_ZERO) {
-          h = splat<C>(0.0);
+          h = splat<C, R>(R(0));
           ST(g.hlat, j0, nt, h);
         }
         if (tp.m_hlat == FCX_WATER || tp.m_hlat == FCX_ICE || tp.m_hlat == FCX_ZERO) emit(1, h);
@@ -254,16 +265,16 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
       // ---- calc_flux_heat_sensible (calc:167-206), P3: QATM in the q_s slot
       if ((stages & S_HSEN) && g.hsen) {
         const int8_t m = m_hs;
-        Vec<C> h;
+        Vec<C, R> h;
         if (m == FCX_CCLM || m == FCX_MOM5) {
-          const Vec<C> &a = (m == FCX_CCLM) ? amoi : chea;
+          const Vec<C, R> &a = (m == FCX_CCLM) ? amoi : chea;
           FOR_C h.v[i] = hsen_cclm(a.v[i], pa.v[i], ps.v[i], qa.v[i], ta.v[i], ts.v[i], vel.v[i]);
           ST(g.hsen, j0, nt, h);
         } else if (m == FCX_RCO) {
           FOR_C h.v[i] = hsen_rco(ta.v[i], ts.v[i], vel.v[i]);
           ST(g.hsen, j0, nt, h);
         } else if (m == FCX_ZERO) {
-          h = splat<C>(0.0);
+          h = splat<C, R>(R(0));
           ST(g.hsen, j0, nt, h);
         }
         if (m == FCX_CCLM || m == FCX_MOM5 || m == FCX_RCO || m == FCX_ZERO) emit(2, h);
@@ -284,17 +295,17 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
         const bool do_u = (stages & S_UMOM) && tp.uv[0].mom;
         const bool do_v = (stages & S_VMOM) && tp.uv[1].mom;
         if (do_u || do_v) {
-          const Vec<C> &a = (m_mo == FCX_MOM5) ? cmom : amom;
-          if (do_u) momentum<C, NT, Emit>(m_mo, false, tp.uv[0], ts, ps, u, v, vel, qs, a, j0, nt, emit, 4);
-          if (do_v) momentum<C, NT, Emit>(m_mo, true, tp.uv[1], ts, ps, u, v, vel, qs, a, j0, nt, emit, 5);
+          const Vec<C, R> &a = (m_mo == FCX_MOM5) ? cmom : amom;
+          if (do_u) momentum<C, NT, R, Emit>(m_mo, false, tp.uv[0], ts, ps, u, v, vel, qs, a, j0, nt, emit, 4);
+          if (do_v) momentum<C, NT, R, Emit>(m_mo, true, tp.uv[1], ts, ps, u, v, vel, qs, a, j0, nt, emit, 5);
         }
       }
       // ---- distribute_shortwave_radiation_flux (calc:355-362): RSDR_s = RSDD_0
       if ((stages & S_RSDR) && g.rsdr) ST(g.rsdr, j0, nt, rsdd);
     }
     if constexpr (!MERGED) {
-      if (j0 < P->n[1]) uv_grid<C, NT>(tp, 0, stages, j0, P->n[1]);
-      if (j0 < P->n[2]) uv_grid<C, NT>(tp, 1, stages, j0, P->n[2]);
+      if (j0 < P->n[1]) uv_grid<C, NT, R>(tp, 0, stages, j0, P->n[1]);
+      if (j0 < P->n[2]) uv_grid<C, NT, R>(tp, 1, stages, j0, P->n[2]);
     }
   }
 
@@ -304,10 +315,10 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
       const AvgEntry &ae = P->avg[e];
       const int64_t n = P->n[ae.grid];
       if (j0 >= n) continue;
-      Vec<C> acc = splat<C>(0.0);
+      Vec<C, R> acc = splat<C, R>(R(0));
       for (int s = 0; s < T; ++s) {
-        const Vec<C> x = LD(ae.x[s], j0, n);
-        const Vec<C> f = LD(ae.fare[s], j0, n);
+        const Vec<C, R> x = LD(ae.x[s], j0, n);
+        const Vec<C, R> f = LD(ae.fare[s], j0, n);
         FOR_C acc.v[i] = acc.v[i] + x.v[i] * f.v[i];
       }
       ST(ae.x0, j0, n, acc);
@@ -315,13 +326,13 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
   }
 }
 
-template <int C, bool MERGED, int VAR, bool NT>
+template <int C, bool MERGED, int VAR, bool NT, class R>
 __global__ __launch_bounds__(256) void cells_kernel(const Params *__restrict__ P,
                                                     const double *__restrict__ corr_m) {
   const int64_t units = (P->n_max + C - 1) / C;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u < units; u += stride)
-    process<C, MERGED, VAR, NT>(P, corr_m, u * C);
+    process<C, MERGED, VAR, NT, R>(P, corr_m, u * C);
 }
 
 // The T=1 hot path with the exchange -> atmosphere accumulation fused in (AtmosFused).
@@ -334,8 +345,8 @@ struct LdsEmit {
   double *p;  // this wave's [kFusedFields][kTile] products
   double w0, w1;
   int c;      // 2 * lane
-  template <int C>
-  __device__ __forceinline__ void operator()(int k, const Vec<C> &x) const {
+  template <int C, class R>
+  __device__ __forceinline__ void operator()(int k, const Vec<C, R> &x) const {
     const d2 q = {w0 * x.v[0], w1 * x.v[1]};  // one 16-B LDS store per field
     *reinterpret_cast<d2 *>(p + k * kTile + c) = q;
   }
@@ -378,7 +389,7 @@ __global__ __launch_bounds__(256) void cells_atmos_kernel(const Params *__restri
     }
     wi[2 * lane] = a0;
     wi[2 * lane + 1] = a1;
-    if (j0 < n) process<2, true, VAR, NT>(P, corr_m, j0, emit);
+    if (j0 < n) process<2, true, VAR, NT, double>(P, corr_m, j0, emit);
     wave_sync();  // the wave's LDS products are visible to all its lanes
     const int64_t tend = t0 + kTile;
     const int32_t next_a = (tend < n) ? af.idx[tend] : -3;
@@ -530,31 +541,31 @@ static int grid_for(int64_t units, int max_blocks = 256 * 8) {
   return (int)blocks;
 }
 
-template <int C, bool MERGED, int VAR, bool NT>
+template <int C, bool MERGED, int VAR, bool NT, class R>
 static void launch_one(int blocks, hipStream_t s, const Params *dp, const double *corr_m) {
-  hipLaunchKernelGGL((cells_kernel<C, MERGED, VAR, NT>), dim3(blocks), dim3(256), 0, s, dp, corr_m);
+  hipLaunchKernelGGL((cells_kernel<C, MERGED, VAR, NT, R>), dim3(blocks), dim3(256), 0, s, dp, corr_m);
 }
 
-template <int C, bool MERGED, int VAR>
+template <int C, bool MERGED, int VAR, class R>
 static void launch_nt(bool nt, int blocks, hipStream_t s, const Params *dp, const double *corr_m) {
   if (nt)
-    launch_one<C, MERGED, VAR, true>(blocks, s, dp, corr_m);
+    launch_one<C, MERGED, VAR, true, R>(blocks, s, dp, corr_m);
   else
-    launch_one<C, MERGED, VAR, false>(blocks, s, dp, corr_m);
+    launch_one<C, MERGED, VAR, false, R>(blocks, s, dp, corr_m);
 }
 
-template <int C>
+template <int C, class R>
 static void launch_c(const LaunchConfig &lc, int blocks, hipStream_t s, const Params *dp,
                      const double *corr_m) {
   if (!lc.merged) {
-    launch_nt<C, false, 0>(lc.nontemporal, blocks, s, dp, corr_m);
+    launch_nt<C, false, 0, R>(lc.nontemporal, blocks, s, dp, corr_m);
     return;
   }
   switch (lc.variant) {
-    case 1: launch_nt<C, true, 1>(lc.nontemporal, blocks, s, dp, corr_m); break;
-    case 2: launch_nt<C, true, 2>(lc.nontemporal, blocks, s, dp, corr_m); break;
-    case 3: launch_nt<C, true, 3>(lc.nontemporal, blocks, s, dp, corr_m); break;
-    default: launch_nt<C, true, 0>(lc.nontemporal, blocks, s, dp, corr_m); break;
+    case 1: launch_nt<C, true, 1, R>(lc.nontemporal, blocks, s, dp, corr_m); break;
+    case 2: launch_nt<C, true, 2, R>(lc.nontemporal, blocks, s, dp, corr_m); break;
+    case 3: launch_nt<C, true, 3, R>(lc.nontemporal, blocks, s, dp, corr_m); break;
+    default: launch_nt<C, true, 0, R>(lc.nontemporal, blocks, s, dp, corr_m); break;
   }
 }
 
@@ -581,13 +592,21 @@ int launch_cells(const Params *hp, const Params *dp, const double *corr_m, const
     }
     return (int)hipGetLastError();
   }
-  const int c = lc.cells_per_thread == 1 ? 1 : 2;
+  // vector width: 16 B per lane and array (2 fp64 or 4 fp32 cells), or 1 cell when the
+  // caller's arrays are not 16-B aligned
+  const int c = lc.cells_per_thread == 1 ? 1 : lc.f32 ? 4 : 2;
   const int64_t units = (hp->n_max + c - 1) / c;
   const int blocks = grid_for(units, lc.max_blocks);
-  if (c == 2)
-    launch_c<2>(lc, blocks, s, dp, corr_m);
-  else
-    launch_c<1>(lc, blocks, s, dp, corr_m);
+  if (lc.f32) {
+    if (c == 4)
+      launch_c<4, float>(lc, blocks, s, dp, corr_m);
+    else
+      launch_c<1, float>(lc, blocks, s, dp, corr_m);
+  } else if (c == 2) {
+    launch_c<2, double>(lc, blocks, s, dp, corr_m);
+  } else {
+    launch_c<1, double>(lc, blocks, s, dp, corr_m);
+  }
   return (int)hipGetLastError();
 }
 

@@ -11,6 +11,7 @@ MODULE fcx_c_api
   INTEGER(c_int), PARAMETER :: FCX_PHASE_EARLY = 1, FCX_PHASE_NORMAL = 2, FCX_PHASE_ALL = 3
   INTEGER(c_int), PARAMETER :: FCX_MEM_HOST = 0, FCX_MEM_DEVICE = 1, FCX_ALLOCATED = 2
   INTEGER(c_int), PARAMETER :: FCX_CORR_CELL_MAJOR = 0, FCX_CORR_MONTH_MAJOR = 1
+  INTEGER(c_int), PARAMETER :: FCX_PRECISION_F64 = 0, FCX_PRECISION_F32 = 1
   ! which_* tables (enum fcx_flux)
   INTEGER(c_int), PARAMETER :: FCX_SPEC_VAPOR_SURFACE_T = 0, FCX_SPEC_VAPOR_SURFACE_U = 1, &
                                FCX_SPEC_VAPOR_SURFACE_V = 2, FCX_FLUX_MASS_EVAP = 3, &
@@ -92,6 +93,12 @@ MODULE fcx_c_api
       TYPE(c_ptr), VALUE :: engine
       INTEGER(c_int), VALUE :: phase, grid, var
       INTEGER(c_int) :: fcx_add_average
+    END FUNCTION
+    FUNCTION fcx_set_precision(engine, precision) BIND(C, name='fcx_set_precision')
+      IMPORT :: c_int, c_ptr
+      TYPE(c_ptr), VALUE :: engine
+      INTEGER(c_int), VALUE :: precision
+      INTEGER(c_int) :: fcx_set_precision
     END FUNCTION
     FUNCTION fcx_commit(engine) BIND(C, name='fcx_commit')
       IMPORT :: c_int, c_ptr

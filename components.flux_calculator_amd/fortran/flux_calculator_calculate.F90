@@ -92,12 +92,15 @@ CONTAINS
         INTEGER(c_int32_t) :: gs(3)
         INTEGER(c_int) :: dev, flags, mask
         INTEGER :: s, g, v
+        REAL(c_double), ALLOCATABLE, TARGET :: corr_d(:,:)
 
         IF (c_associated(engine)) CALL fcx_detach()
         gs = INT(grid_size(1:3), c_int32_t)
         dev = 0
         IF (PRESENT(device)) dev = INT(device, c_int)
         CALL check(fcx_create(dev, INT(num_surface_types, c_int), gs, engine), 'fcx_create')
+        ! the NO_USE_DOUBLE_PRECISION build (basic:21-25) keeps REAL(4) fields: fp32 engine
+        IF (wp == c_float) CALL check(fcx_set_precision(engine, FCX_PRECISION_F32), 'fcx_set_precision')
 
         CALL set_table(FCX_SPEC_VAPOR_SURFACE_T, which_spec_vapor_surface_t, my_bottom_model, num_surface_types)
         CALL set_table(FCX_SPEC_VAPOR_SURFACE_U, which_spec_vapor_surface_u, my_bottom_model, num_surface_types)
@@ -133,10 +136,13 @@ CONTAINS
 
         ! bias_corrections: corrections(E_MASS_EVAP_CORRECTION, :, :) is (12, grid_size(1))
         IF (lcorrection .AND. PRESENT(corrections_mass_evap)) THEN
+            ! the C ABI takes the corrections as double (copied at the call)
+            corr_d = REAL(corrections_mass_evap, c_double)
             CALL check(fcx_set_corrections(engine, 1_c_int, INT(correction_init_date, c_int32_t),  &
-                                           c_loc(corrections_mass_evap(1,1)),                    &
+                                           c_loc(corr_d(1,1)),                                   &
                                            INT(grid_size(1), c_int64_t), FCX_CORR_CELL_MAJOR),    &
                        'fcx_set_corrections')
+            DEALLOCATE(corr_d)
         ENDIF
 
         IF (PRESENT(regrid_u_to_t_matrix)) CALL set_matrix(FCX_U_TO_T, regrid_u_to_t_matrix)

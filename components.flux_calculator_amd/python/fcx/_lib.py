@@ -15,6 +15,8 @@ FCX_MEM_DEVICE = 0x1
 FCX_ALLOCATED = 0x2
 FCX_CORR_CELL_MAJOR = 0
 FCX_CORR_MONTH_MAJOR = 1
+FCX_PRECISION_F64 = 0
+FCX_PRECISION_F32 = 1
 
 # every symbol declared in include/fcx.h: (name, restype, argtypes)
 _c = ctypes
@@ -37,6 +39,7 @@ SIGNATURES = [
     ("fcx_set_regrid_matrix", _I, [_P, _I, _I64, _P, _P, _P]),
     ("fcx_set_put_to", _I, [_P, _I, _I, _I, _I]),
     ("fcx_add_average", _I, [_P, _I, _I, _I]),
+    ("fcx_set_precision", _I, [_P, _I]),
     ("fcx_commit", _I, [_P]),
     ("fcx_upload", _I, [_P, _I]),
     ("fcx_run", _I, [_P, _I, _I32]),

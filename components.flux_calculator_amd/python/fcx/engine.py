@@ -5,7 +5,7 @@ import numpy as np
 
 from . import _lib
 from .basic import FLUX_ID, IDX, METHOD_ID, PHASE_ALL, PHASE_EARLY, PHASE_NORMAL
-from .local_field import LocalFields, data_ptr, is_device
+from .local_field import LocalFields, data_ptr, dtype_name, is_device
 
 
 class Engine:
@@ -36,6 +36,10 @@ class Engine:
         try:
             if stream is not None:
                 _lib.check(self.lib.fcx_set_stream(h, ctypes.c_void_p(stream)))
+            dtype = getattr(lf, "dtype", "float64")
+            self.precision = dtype
+            _lib.check(self.lib.fcx_set_precision(
+                h, _lib.FCX_PRECISION_F32 if dtype == "float32" else _lib.FCX_PRECISION_F64))
             for table, per_type in self.methods.items():
                 for s, m in enumerate(per_type[: self.T], start=1):
                     mid = METHOD_ID[m.rstrip()] if isinstance(m, str) else int(m)
@@ -44,6 +48,8 @@ class Engine:
                 flags = (_lib.FCX_MEM_DEVICE if is_device(a) else _lib.FCX_MEM_HOST)
                 if alloc:
                     flags |= _lib.FCX_ALLOCATED
+                if dtype_name(a) != dtype:
+                    raise TypeError(f"slot {(s, g, var)}: {dtype_name(a)} array in a {dtype} LocalFields")
                 n = a.shape[0]
                 _lib.check(self.lib.fcx_bind_field(h, s, g, var, ctypes.c_void_p(data_ptr(a)), n, flags))
             if corrections is not None:

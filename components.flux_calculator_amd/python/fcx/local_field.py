@@ -4,7 +4,8 @@ The reference keeps one 1-D REAL(wp) POINTER array per (surface type, grid, vari
 (flux_calculator_basic.F90:86-103, flux_calculator.F90:159) and expresses sharing by
 pointer aliasing.  LocalFields does the same: a slot holds an array object, and aliasing is
 holding the SAME object in several slots.  Arrays are numpy float64 (host, as Fortran owns
-them) or torch CUDA float64 tensors (device-resident use, zero copy).
+them) or torch CUDA float64 tensors (device-resident use, zero copy); a LocalFields built
+with dtype="float32" holds float32 arrays for the fp32 engine (FCX_PRECISION_F32).
 """
 import numpy as np
 
@@ -21,10 +22,18 @@ def is_device(a):
     return not isinstance(a, np.ndarray)
 
 
+def dtype_name(a):
+    """'float64' / 'float32' / ... of a numpy array or torch tensor."""
+    return str(a.dtype).replace("torch.", "")
+
+
 class LocalFields:
-    def __init__(self, grid_size, device=None):
+    def __init__(self, grid_size, device=None, dtype="float64"):
+        if dtype not in ("float64", "float32"):
+            raise ValueError(f"dtype {dtype}: float64 or float32")
         self.grid_size = [int(n) for n in grid_size]
         self.device = device  # None: numpy host arrays; else a torch device
+        self.dtype = dtype
         self.field = {}  # (s, g, name) -> array
         self.allocated = set()  # (s, g, name) with realarray%allocated = .TRUE.
         self.put_to = {}  # (s, g, name) -> bitmask t=1,u=2,v=4
@@ -32,13 +41,13 @@ class LocalFields:
     # ---- helpers
     def _new(self, n, value=None):
         if self.device is None:
-            a = np.empty(n, dtype=np.float64)
+            a = np.empty(n, dtype=self.dtype)
             if value is not None:
                 a[:] = value
             return a
         import torch
 
-        a = torch.empty(n, dtype=torch.float64, device=self.device)
+        a = torch.empty(n, dtype=getattr(torch, self.dtype), device=self.device)
         if value is not None:
             a.fill_(value)
         return a
@@ -96,4 +105,22 @@ class LocalFields:
         return a.detach().cpu().numpy()
 
 
-__all__ = ["LocalFields", "data_ptr", "is_device", "VARNAMES", "MAX_SURFACE_TYPES"]
+    def astype(self, dtype):
+        """A copy with every array converted to dtype (rounded once), aliases kept."""
+        new = LocalFields(self.grid_size, self.device, dtype)
+        conv = {}
+        for key, a in self.field.items():
+            if id(a) not in conv:
+                if isinstance(a, np.ndarray):
+                    conv[id(a)] = np.ascontiguousarray(a, dtype=dtype)
+                else:
+                    import torch
+
+                    conv[id(a)] = a.to(getattr(torch, dtype)).contiguous()
+            new.field[key] = conv[id(a)]
+        new.allocated = set(self.allocated)
+        new.put_to = dict(self.put_to)
+        return new
+
+
+__all__ = ["LocalFields", "data_ptr", "dtype_name", "is_device", "VARNAMES", "MAX_SURFACE_TYPES"]

@@ -243,6 +243,18 @@ def build_case(variant="CCLM", n=4096, T=1, bias=False, sep_grids=None, rsdr=Fal
                 outputs=outputs)
 
 
+def as_dtype(case, dtype):
+    """The same case with every field array rounded once to dtype (aliases kept): the fp32
+    variant of SURVEY.md 8d config 5, and (as_dtype(c32, 'float64')) the exactly widened
+    inputs its fp64 oracle runs on."""
+    import copy
+
+    new = copy.copy(case)
+    new.lf = case.lf.astype(dtype)
+    new.name = f"{case.name}_{dtype}"
+    return new
+
+
 def _to_dev(a, device):
     import torch
 

@@ -110,6 +110,15 @@ int fcx_set_put_to(fcx_engine *e, int surface_type, int grid, int var, int mask)
  * 911-918 early, 1001-1008 normal).  Follows the P7 trigger: only applied when the type-0
  * array is FCX_ALLOCATED and surface type 2 exists. */
 int fcx_add_average(fcx_engine *e, int phase, int grid, int var);
+/* arithmetic/storage type of the engine's fields.  FCX_PRECISION_F64 (default) is the
+ * reference's -r8 build (build_hlrnb.sh:26).  FCX_PRECISION_F32: every pointer given to
+ * fcx_bind_field / fcx_add_atmos_field / returned by fcx_device_ptr addresses float arrays
+ * (the double* parameter type then only carries the address) and the kernels compute in
+ * fp32 -- the SURVEY.md 8d config-5 variant, half the HBM bytes per cell.  Corrections are
+ * still passed as double and rounded once at commit.  Not with regridding or the
+ * atmosphere accumulation (FCX_E_UNSUPPORTED at commit).  Call before fcx_commit. */
+enum fcx_precision { FCX_PRECISION_F64 = 0, FCX_PRECISION_F32 = 1 };
+int fcx_set_precision(fcx_engine *e, int precision);
 /* validate (flux_calculator_prepare.F90 rules), allocate device mirrors, build plans */
 int fcx_commit(fcx_engine *e);
 

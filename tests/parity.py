@@ -6,6 +6,10 @@ q_s - q_a or T_s - T_a*EF cancel).  Integer/index results are compared bit-exact
 import numpy as np
 
 FP64_TOL = 1e-10
+# fp32 variant ("fp32: report only").  Its error is reported against
+# the fp64 oracle on the same (float32-rounded) inputs; the gate below is a sanity bound on
+# the norm-wise error max|x - ref| / ||ref||_inf, not a parity claim.
+FP32_NORM_GATE = 1e-5
 
 
 def mixed_error(x, ref):
@@ -33,3 +37,28 @@ def assert_parity(got: dict, ref: dict, tol=FP64_TOL, label=""):
     bad = {k: v for k, v in worst.items() if not v <= tol}
     assert not bad, f"{label}: fields over tolerance {tol}: {bad}"
     return worst
+
+
+def norm_error(x, ref):
+    """max_j |x - x_ref| / ||x_ref||_inf (norm-wise; the fp32 report)."""
+    x = np.asarray(x, dtype=np.float64)
+    ref = np.asarray(ref, dtype=np.float64)
+    if ref.size == 0:
+        return 0.0
+    if not np.all(np.isfinite(x) == np.isfinite(ref)):
+        return np.inf
+    fin = np.isfinite(ref)
+    top = np.max(np.abs(ref[fin])) if fin.any() else 0.0
+    return float(np.max(np.abs(x[fin] - ref[fin])) / (top if top > 0 else 1.0))
+
+
+def error_report(got: dict, ref: dict):
+    """{field: (norm-wise error, mixed error, elementwise max relative error)}"""
+    out = {}
+    for key, r in ref.items():
+        g = np.asarray(got[key], dtype=np.float64)
+        r = np.asarray(r, dtype=np.float64)
+        nz = np.abs(r) > 0
+        rel = float(np.max(np.abs(g[nz] - r[nz]) / np.abs(r[nz]))) if nz.any() else 0.0
+        out[key] = (norm_error(g, r), mixed_error(g, r), rel)
+    return out

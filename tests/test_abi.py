@@ -107,3 +107,39 @@ def test_engine_calls_before_commit_fail_cleanly():
     assert b"fcx_commit" in lib.fcx_last_error()
     assert lib.fcx_create(0, 11, gs, ctypes.byref(h)) == 1  # > MAX_SURFACE_TYPES
     lib.fcx_destroy(h)
+
+
+def test_fp32_engine_refuses_regrid_and_atmosphere_before_any_hip_call():
+    """FCX_PRECISION_F32 covers the cell pass only: regridding and the atmosphere
+    accumulation stay fp64 (FCX_E_UNSUPPORTED at commit, before the device is touched)."""
+    from fcx.parallel import local_atmos, synthetic_atmos_map
+    from fcx.synthetic import as_dtype
+
+    c32 = as_dtype(build_case("CCLM", n=64, T=1), "float32")
+    amap = synthetic_atmos_map(64)
+    out = np.zeros(amap.n_atmos)
+    atmos = {"local": local_atmos(amap, 0, 1), "fields": [(2, 1, 1, "MEVA", out)]}
+    with pytest.raises(_lib.FcxError) as ei:
+        Engine(c32.lf, 1, c32.methods, atmos=atmos)
+    assert ei.value.status == 3 and "fp32" in str(ei.value)
+    m = (np.array([1], np.int32), np.array([1], np.int32), np.ones(1))
+    with pytest.raises(_lib.FcxError) as ei:
+        Engine(c32.lf, 1, c32.methods, regrid={"matrices": {0: m}})
+    assert ei.value.status == 3
+
+
+def test_mixed_precision_bindings_rejected():
+    case = build_case("CCLM", n=64, T=1)
+    case.lf.dtype = "float32"  # float64 arrays in a float32 LocalFields
+    with pytest.raises(TypeError):
+        Engine(case.lf, 1, case.methods)
+
+
+def test_set_precision_validates():
+    lib = _lib.load()
+    h = ctypes.c_void_p()
+    gs = (ctypes.c_int32 * 3)(10, 10, 10)
+    _lib.check(lib.fcx_create(0, 1, gs, ctypes.byref(h)))
+    assert lib.fcx_set_precision(h, 2) == 1
+    assert lib.fcx_set_precision(h, _lib.FCX_PRECISION_F32) == 0
+    lib.fcx_destroy(h)
