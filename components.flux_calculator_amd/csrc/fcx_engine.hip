@@ -130,6 +130,12 @@ struct fcx_engine {
   void *atm_pool = nullptr;
   bool atmos_in_run = true;
   bool atm_done_fused = false;  // the last fcx_run already accumulated the atmosphere fields
+  // host-bound steps: page-locked caller arrays and the H2D / compute / D2H pipeline
+  bool pin_host = true;
+  int chunks = 8;                                   // fcx_step pipeline depth (1 = off)
+  std::vector<std::pair<char *, size_t>> pinned;    // hipHostRegister'ed page ranges
+  hipStream_t s_in = nullptr, s_out = nullptr;      // copy streams of the pipeline
+  std::vector<hipEvent_t> ev_in, ev_comp;           // per chunk
 
   fcx_engine() {
     for (auto &a : slot)
@@ -231,6 +237,11 @@ extern "C" int fcx_destroy(fcx_engine *e) {
   (void)hipFree(e->pool);
   if (e->ev0) (void)hipEventDestroy(e->ev0);
   if (e->ev1) (void)hipEventDestroy(e->ev1);
+  for (hipEvent_t ev : e->ev_in) (void)hipEventDestroy(ev);
+  for (hipEvent_t ev : e->ev_comp) (void)hipEventDestroy(ev);
+  if (e->s_in) (void)hipStreamDestroy(e->s_in);
+  if (e->s_out) (void)hipStreamDestroy(e->s_out);
+  for (auto &r : e->pinned) (void)hipHostUnregister(r.first);
   if (e->own_stream && e->stream) (void)hipStreamDestroy(e->stream);
   delete e;
   return FCX_OK;
@@ -258,6 +269,8 @@ static int gpu_init(fcx_engine *e) {
   }
   HIP_TRY(hipEventCreate(&e->ev0));
   HIP_TRY(hipEventCreate(&e->ev1));
+  HIP_TRY(hipStreamCreateWithFlags(&e->s_in, hipStreamNonBlocking));
+  HIP_TRY(hipStreamCreateWithFlags(&e->s_out, hipStreamNonBlocking));
   e->gpu_ready = true;
   return FCX_OK;
 }
@@ -760,6 +773,40 @@ static int get_plan(fcx_engine *e, uint32_t stages, int avg_phases, Plan **pl) {
   return FCX_OK;
 }
 
+// Page-lock the caller's host arrays once (hipHostRegister of their exact byte ranges,
+// merged where arrays overlap): the per-step H2D/D2H then run as DMA at the link rate and
+// overlap with compute.  The ranges are not rounded out to pages: a registered range that
+// swallowed the head of some other allocation would make the runtime treat that memory as
+// part of ours and reject copies running past our end.  A range the runtime refuses stays
+// pageable (its copies are still correct, only staged).
+static void pin_host_arrays(fcx_engine *e) {
+  std::vector<std::pair<uintptr_t, uintptr_t>> r;
+  auto add = [&](const void *p, size_t bytes) {
+    if (!p || !bytes) return;
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    r.push_back({a, a + bytes});
+  };
+  for (auto &bf : e->bufs)
+    if (!bf.external) add(bf.host, (size_t)bf.n * e->esize);
+  for (auto &f : e->atm_fields)
+    if (!f.external) add(f.out_host, (size_t)std::max<int64_t>(e->n_atmos, 0) * sizeof(double));
+  std::sort(r.begin(), r.end());
+  std::vector<std::pair<uintptr_t, uintptr_t>> m;
+  for (auto &x : r) {
+    if (!m.empty() && x.first < m.back().second)
+      m.back().second = std::max(m.back().second, x.second);
+    else
+      m.push_back(x);
+  }
+  for (auto &x : m) {
+    char *p = reinterpret_cast<char *>(x.first);
+    if (hipHostRegister(p, x.second - x.first, hipHostRegisterDefault) == hipSuccess)
+      e->pinned.push_back({p, x.second - x.first});
+    else
+      (void)hipGetLastError();  // e.g. already registered by the caller: leave it
+  }
+}
+
 extern "C" int fcx_set_precision(fcx_engine *e, int precision) {
   if (!e) return fail(FCX_E_ARG, "NULL engine");
   if (e->committed) return fail(FCX_E_STATE, "engine already committed");
@@ -850,6 +897,7 @@ extern "C" int fcx_commit(fcx_engine *e) {
         }
     }
   }
+  if (e->pin_host) pin_host_arrays(e);
   e->committed = true;
   return FCX_OK;
 }
@@ -886,9 +934,12 @@ static int copy_bufs(fcx_engine *e, const std::vector<int> &ids, bool h2d) {
   return FCX_OK;
 }
 
-static int launch_plan(fcx_engine *e, Plan *pl, const double *corr_m) {
+static int launch_plan(fcx_engine *e, Plan *pl, const double *corr_m, int64_t lo = 0, int64_t hi = -1,
+                       bool fixup = true) {
   if (pl->host.n_max <= 0) return FCX_OK;
   LaunchConfig lc = e->launch;
+  lc.lo = lo;
+  lc.hi = hi;
   if (!e->aligned16) lc.cells_per_thread = 1;
   lc.merged = pl->host.merged_uv != 0;
   lc.variant = (e->specialize && lc.merged) ? pl->variant : 0;
@@ -902,11 +953,11 @@ static int launch_plan(fcx_engine *e, Plan *pl, const double *corr_m) {
   }
   const int r = launch_cells(&pl->host, pl->dev, corr_m, lc, e->stream, fused ? &pl->af : nullptr);
   if (r) return fail(FCX_E_HIP, "cells_kernel launch: %s", hipGetErrorString((hipError_t)r));
-  if (fused) {
+  if (fused && fixup) {
     const int r2 = launch_atmos_fixup(pl->af, pl->host.n_max, e->stream);
     if (r2) return fail(FCX_E_HIP, "atmos_fixup launch: %s", hipGetErrorString((hipError_t)r2));
-    e->atm_done_fused = true;
   }
+  if (fused) e->atm_done_fused = true;
   return FCX_OK;
 }
 
@@ -1033,7 +1084,86 @@ extern "C" int fcx_run(fcx_engine *e, int phase, int32_t t) {
   return FCX_OK;
 }
 
+// copy the part [lo, hi) of a host-bound buffer (the last chunk also takes the array tail)
+static int copy_slice(fcx_engine *e, const Buffer &bf, int64_t lo, int64_t hi, bool last, bool h2d,
+                      hipStream_t s) {
+  if (bf.external || bf.n == 0) return FCX_OK;
+  const int64_t a = std::min(lo, bf.n), z = last ? bf.n : std::min(hi, bf.n);
+  if (z <= a) return FCX_OK;
+  const size_t off = (size_t)a * e->esize, bytes = (size_t)(z - a) * e->esize;
+  char *dev = reinterpret_cast<char *>(bf.dev) + off, *host = reinterpret_cast<char *>(bf.host) + off;
+  if (h2d)
+    HIP_TRY(hipMemcpyAsync(dev, host, bytes, hipMemcpyHostToDevice, s));
+  else
+    HIP_TRY(hipMemcpyAsync(host, dev, bytes, hipMemcpyDeviceToHost, s));
+  return FCX_OK;
+}
+
+// fcx_step of a host-bound engine as a 3-stage pipeline over cell chunks: H2D of chunk k+1
+// (s_in), the cells kernel of chunk k (engine stream) and D2H of chunk k-1 (s_out) overlap,
+// so a step costs ~max(H2D bytes, D2H bytes) / link rate instead of their sum plus compute.
+// The accumulation fix-up / separate kernel and the atmosphere outputs follow the last chunk.
+static int step_pipelined(fcx_engine *e, int phase, int32_t t, Plan *pl) {
+  int rc;
+  const double *corr_m = month_slice(e, t, &rc);
+  if (rc) return rc;
+  const int64_t n = pl->host.n_max;
+  const int64_t per = ((n + e->chunks - 1) / e->chunks + kChunkAlign - 1) / kChunkAlign * kChunkAlign;
+  const int K = (int)((n + per - 1) / per);
+  while ((int)e->ev_in.size() < K) {
+    hipEvent_t a, b;
+    HIP_TRY(hipEventCreateWithFlags(&a, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&b, hipEventDisableTiming));
+    e->ev_in.push_back(a);
+    e->ev_comp.push_back(b);
+  }
+  HIP_TRY(hipEventRecord(e->ev0, e->s_in));
+  e->atm_done_fused = false;
+  for (int k = 0; k < K; ++k) {
+    const int64_t lo = k * per, hi = std::min(n, lo + per);
+    const bool last = k == K - 1;
+    for (int b : pl->reads)
+      if (int r = copy_slice(e, e->bufs[b], lo, hi, last, true, e->s_in)) return r;
+    HIP_TRY(hipEventRecord(e->ev_in[k], e->s_in));
+    HIP_TRY(hipStreamWaitEvent(e->stream, e->ev_in[k], 0));
+    if (int r = launch_plan(e, pl, corr_m, lo, hi, last)) return r;
+    HIP_TRY(hipEventRecord(e->ev_comp[k], e->stream));
+    HIP_TRY(hipStreamWaitEvent(e->s_out, e->ev_comp[k], 0));
+    for (int b : pl->writes)
+      if (int r = copy_slice(e, e->bufs[b], lo, hi, last, false, e->s_out)) return r;
+  }
+  if (e->atmos_in_run && !e->atm_done_fused)
+    if (int r = run_atmos(e, phase)) return r;
+  HIP_TRY(hipEventRecord(e->ev_comp[K - 1], e->stream));
+  HIP_TRY(hipStreamWaitEvent(e->s_out, e->ev_comp[K - 1], 0));
+  if (e->atmos_in_run || e->atm_done_fused)
+    for (auto &f : e->atm_fields)
+      if ((f.phase & phase) && !f.external && e->n_atmos > 0)
+        HIP_TRY(hipMemcpyAsync(f.out_host, f.out_dev, e->n_atmos * sizeof(double), hipMemcpyDeviceToHost,
+                               e->s_out));
+  HIP_TRY(hipEventRecord(e->ev1, e->s_out));
+  e->timed = true;
+  HIP_TRY(hipStreamSynchronize(e->s_out));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  return FCX_OK;
+}
+
+static bool host_bound(const fcx_engine *e, const Plan *pl) {
+  for (int b : pl->reads)
+    if (!e->bufs[b].external) return true;
+  for (int b : pl->writes)
+    if (!e->bufs[b].external) return true;
+  return false;
+}
+
 extern "C" int fcx_step(fcx_engine *e, int phase, int32_t t) {
+  if (int r = check(e)) return r;
+  if (phase < 1 || phase > 3) return fail(FCX_E_ARG, "phase %d unknown", phase);
+  if (e->chunks > 1 && !e->any_regrid) {
+    Plan *pl;
+    if (int r = get_plan(e, phase_stages(phase), phase, &pl)) return r;
+    if (host_bound(e, pl) && pl->host.n_max >= 2 * kChunkAlign) return step_pipelined(e, phase, t, pl);
+  }
   if (int r = fcx_upload(e, phase)) return r;
   if (int r = fcx_run(e, phase, t)) return r;
   if (int r = fcx_download(e, phase)) return r;
@@ -1152,6 +1282,14 @@ extern "C" int fcx_last_kernel_ms(fcx_engine *e, float *ms) {
   return FCX_OK;
 }
 
+extern "C" int fcx_pinned_bytes(fcx_engine *e, int64_t *bytes) {
+  if (!e || !bytes) return fail(FCX_E_ARG, "NULL argument");
+  int64_t b = 0;
+  for (auto &r : e->pinned) b += (int64_t)r.second;
+  *bytes = b;
+  return FCX_OK;
+}
+
 extern "C" int fcx_algorithmic_bytes(fcx_engine *e, int phase, int64_t *bytes) {
   if (int r = check(e)) return r;
   if (!bytes || phase < 1 || phase > 3) return fail(FCX_E_ARG, "bad arguments");
@@ -1221,6 +1359,14 @@ extern "C" int fcx_set_option(fcx_engine *e, int option, int64_t value) {
       return FCX_OK;
     case FCX_OPT_ATMOS_IN_RUN:
       e->atmos_in_run = value != 0;
+      return FCX_OK;
+    case FCX_OPT_PIN_HOST:
+      if (e->committed) return fail(FCX_E_STATE, "pin_host is applied at fcx_commit");
+      e->pin_host = value != 0;
+      return FCX_OK;
+    case FCX_OPT_PIPELINE_CHUNKS:
+      if (value < 1 || value > 1024) return fail(FCX_E_ARG, "pipeline chunks %lld outside 1..1024", (long long)value);
+      e->chunks = (int)value;
       return FCX_OK;
     default:
       return fail(FCX_E_ARG, "option %d unknown", option);

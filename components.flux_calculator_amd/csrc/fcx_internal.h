@@ -74,7 +74,10 @@ struct LaunchConfig {
   bool merged = false;       // u/v grids are the t grid
   int variant = 0;           // 0 generic, 1 CCLM, 2 MOM5, 3 RCO (T=1 specialisations)
   bool f32 = false;          // fp32 fields (FCX_PRECISION_F32): 4 cells per lane
+  int64_t lo = 0, hi = -1;   // cell range of this launch (lo a multiple of kChunkAlign;
+                             // hi < 0: to n_max) -- the pipelined host-bound step
 };
+constexpr int64_t kChunkAlign = 1024;  // chunk boundaries: whole wave tiles and vectors
 
 struct AtmosFused;
 // corr_m: month slice [n_t] of the bias corrections (device), or nullptr

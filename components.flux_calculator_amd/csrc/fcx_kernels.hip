@@ -326,12 +326,14 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
   }
 }
 
+// cells [lo, hi) of the plan (lo a multiple of C), grid-stride over C-cell units
 template <int C, bool MERGED, int VAR, bool NT, class R>
 __global__ __launch_bounds__(256) void cells_kernel(const Params *__restrict__ P,
-                                                    const double *__restrict__ corr_m) {
-  const int64_t units = (P->n_max + C - 1) / C;
+                                                    const double *__restrict__ corr_m, int64_t lo,
+                                                    int64_t hi) {
+  const int64_t u_end = (hi + C - 1) / C;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u < units; u += stride)
+  for (int64_t u = lo / C + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u < u_end; u += stride)
     process<C, MERGED, VAR, NT, R>(P, corr_m, u * C);
 }
 
@@ -361,17 +363,17 @@ __device__ __forceinline__ void wave_sync() {
 template <int VAR, bool NT>
 __global__ __launch_bounds__(256) void cells_atmos_kernel(const Params *__restrict__ P,
                                                           const double *__restrict__ corr_m,
-                                                          const AtmosFused af) {
+                                                          const AtmosFused af, int64_t lo, int64_t hi) {
   __shared__ double s_p[4][kFusedFields * kTile];
   __shared__ int32_t s_idx[4][kTile];
   const int64_t n = P->n_max;
-  const int64_t n_tiles = (n + kTile - 1) / kTile;
+  const int64_t n_tiles = (hi + kTile - 1) / kTile;  // tiles [lo/kTile, n_tiles) of this launch
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   double *wp = s_p[wv];
   int32_t *wi = s_idx[wv];
   const int64_t waves = (int64_t)gridDim.x * (blockDim.x >> 6);
   const int64_t wave0 = (int64_t)blockIdx.x * (blockDim.x >> 6) + wv;
-  for (int64_t tile = wave0; tile < n_tiles; tile += waves) {
+  for (int64_t tile = lo / kTile + wave0; tile < n_tiles; tile += waves) {
     const int64_t t0 = tile * kTile;
     const int64_t j0 = t0 + 2 * lane;
     LdsEmit emit{wp, 0.0, 0.0, 2 * lane};
@@ -542,52 +544,57 @@ static int grid_for(int64_t units, int max_blocks = 256 * 8) {
 }
 
 template <int C, bool MERGED, int VAR, bool NT, class R>
-static void launch_one(int blocks, hipStream_t s, const Params *dp, const double *corr_m) {
-  hipLaunchKernelGGL((cells_kernel<C, MERGED, VAR, NT, R>), dim3(blocks), dim3(256), 0, s, dp, corr_m);
+static void launch_one(int blocks, hipStream_t s, const Params *dp, const double *corr_m, int64_t lo,
+                       int64_t hi) {
+  hipLaunchKernelGGL((cells_kernel<C, MERGED, VAR, NT, R>), dim3(blocks), dim3(256), 0, s, dp, corr_m, lo, hi);
 }
 
 template <int C, bool MERGED, int VAR, class R>
-static void launch_nt(bool nt, int blocks, hipStream_t s, const Params *dp, const double *corr_m) {
+static void launch_nt(bool nt, int blocks, hipStream_t s, const Params *dp, const double *corr_m,
+                      int64_t lo, int64_t hi) {
   if (nt)
-    launch_one<C, MERGED, VAR, true, R>(blocks, s, dp, corr_m);
+    launch_one<C, MERGED, VAR, true, R>(blocks, s, dp, corr_m, lo, hi);
   else
-    launch_one<C, MERGED, VAR, false, R>(blocks, s, dp, corr_m);
+    launch_one<C, MERGED, VAR, false, R>(blocks, s, dp, corr_m, lo, hi);
 }
 
 template <int C, class R>
 static void launch_c(const LaunchConfig &lc, int blocks, hipStream_t s, const Params *dp,
-                     const double *corr_m) {
+                     const double *corr_m, int64_t lo, int64_t hi) {
   if (!lc.merged) {
-    launch_nt<C, false, 0, R>(lc.nontemporal, blocks, s, dp, corr_m);
+    launch_nt<C, false, 0, R>(lc.nontemporal, blocks, s, dp, corr_m, lo, hi);
     return;
   }
   switch (lc.variant) {
-    case 1: launch_nt<C, true, 1, R>(lc.nontemporal, blocks, s, dp, corr_m); break;
-    case 2: launch_nt<C, true, 2, R>(lc.nontemporal, blocks, s, dp, corr_m); break;
-    case 3: launch_nt<C, true, 3, R>(lc.nontemporal, blocks, s, dp, corr_m); break;
-    default: launch_nt<C, true, 0, R>(lc.nontemporal, blocks, s, dp, corr_m); break;
+    case 1: launch_nt<C, true, 1, R>(lc.nontemporal, blocks, s, dp, corr_m, lo, hi); break;
+    case 2: launch_nt<C, true, 2, R>(lc.nontemporal, blocks, s, dp, corr_m, lo, hi); break;
+    case 3: launch_nt<C, true, 3, R>(lc.nontemporal, blocks, s, dp, corr_m, lo, hi); break;
+    default: launch_nt<C, true, 0, R>(lc.nontemporal, blocks, s, dp, corr_m, lo, hi); break;
   }
 }
 
 template <int VAR>
 static void launch_atm(bool nt, int blocks, hipStream_t s, const Params *dp, const double *corr_m,
-                       const AtmosFused &af) {
+                       const AtmosFused &af, int64_t lo, int64_t hi) {
   if (nt)
-    hipLaunchKernelGGL((cells_atmos_kernel<VAR, true>), dim3(blocks), dim3(256), 0, s, dp, corr_m, af);
+    hipLaunchKernelGGL((cells_atmos_kernel<VAR, true>), dim3(blocks), dim3(256), 0, s, dp, corr_m, af, lo, hi);
   else
-    hipLaunchKernelGGL((cells_atmos_kernel<VAR, false>), dim3(blocks), dim3(256), 0, s, dp, corr_m, af);
+    hipLaunchKernelGGL((cells_atmos_kernel<VAR, false>), dim3(blocks), dim3(256), 0, s, dp, corr_m, af, lo, hi);
 }
 
 int launch_cells(const Params *hp, const Params *dp, const double *corr_m, const LaunchConfig &lc,
                  void *stream, const AtmosFused *atm) {
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int64_t lo = lc.lo, hi = lc.hi < 0 ? hp->n_max : std::min<int64_t>(lc.hi, hp->n_max);
+  if (lo % kChunkAlign || lo < 0) return (int)hipErrorInvalidValue;
+  if (hi <= lo) return 0;
   if (atm) {  // fused accumulation: T=1 specialised merged kernel, 2 cells per lane
-    const int64_t tiles = (hp->n_max + kTile - 1) / kTile;
+    const int64_t tiles = (hi - lo + kTile - 1) / kTile;
     const int blocks = (int)std::max<int64_t>(1, lc.max_blocks > 0 ? std::min<int64_t>(tiles, lc.max_blocks) : tiles);
     switch (lc.variant) {
-      case 1: launch_atm<1>(lc.nontemporal, blocks, s, dp, corr_m, *atm); break;
-      case 2: launch_atm<2>(lc.nontemporal, blocks, s, dp, corr_m, *atm); break;
-      case 3: launch_atm<3>(lc.nontemporal, blocks, s, dp, corr_m, *atm); break;
+      case 1: launch_atm<1>(lc.nontemporal, blocks, s, dp, corr_m, *atm, lo, hi); break;
+      case 2: launch_atm<2>(lc.nontemporal, blocks, s, dp, corr_m, *atm, lo, hi); break;
+      case 3: launch_atm<3>(lc.nontemporal, blocks, s, dp, corr_m, *atm, lo, hi); break;
       default: return (int)hipErrorInvalidValue;
     }
     return (int)hipGetLastError();
@@ -595,17 +602,17 @@ int launch_cells(const Params *hp, const Params *dp, const double *corr_m, const
   // vector width: 16 B per lane and array (2 fp64 or 4 fp32 cells), or 1 cell when the
   // caller's arrays are not 16-B aligned
   const int c = lc.cells_per_thread == 1 ? 1 : lc.f32 ? 4 : 2;
-  const int64_t units = (hp->n_max + c - 1) / c;
+  const int64_t units = (hi - lo + c - 1) / c;
   const int blocks = grid_for(units, lc.max_blocks);
   if (lc.f32) {
     if (c == 4)
-      launch_c<4, float>(lc, blocks, s, dp, corr_m);
+      launch_c<4, float>(lc, blocks, s, dp, corr_m, lo, hi);
     else
-      launch_c<1, float>(lc, blocks, s, dp, corr_m);
+      launch_c<1, float>(lc, blocks, s, dp, corr_m, lo, hi);
   } else if (c == 2) {
-    launch_c<2, double>(lc, blocks, s, dp, corr_m);
+    launch_c<2, double>(lc, blocks, s, dp, corr_m, lo, hi);
   } else {
-    launch_c<1, double>(lc, blocks, s, dp, corr_m);
+    launch_c<1, double>(lc, blocks, s, dp, corr_m, lo, hi);
   }
   return (int)hipGetLastError();
 }

@@ -58,6 +58,7 @@ SIGNATURES = [
     ("fcx_do_regridding", _I, [_P, _I, _I]),
     ("fcx_device_ptr", _I, [_P, _I, _I, _I, _c.POINTER(_DP)]),
     ("fcx_last_kernel_ms", _I, [_P, _c.POINTER(_c.c_float)]),
+    ("fcx_pinned_bytes", _I, [_P, _P]),
     ("fcx_algorithmic_bytes", _I, [_P, _I, _c.POINTER(_I64)]),
     ("fcx_set_option", _I, [_P, _I, _I64]),
     ("fcx_set_atmos_map", _I, [_P, _I64, _P, _P]),

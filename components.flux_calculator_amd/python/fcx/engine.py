@@ -123,8 +123,13 @@ class Engine:
         _lib.check(self.lib.fcx_algorithmic_bytes(self.h, phase, ctypes.byref(b)))
         return b.value
 
+    def pinned_bytes(self):
+        b = ctypes.c_int64()
+        _lib.check(self.lib.fcx_pinned_bytes(self.h, ctypes.byref(b)))
+        return b.value
+
     OPTIONS = {"cells_per_thread": 1, "max_blocks": 2, "nontemporal": 3, "specialize": 4,
-               "atmos_in_run": 5}
+               "atmos_in_run": 5, "pin_host": 6, "pipeline_chunks": 7}
 
     def run_atmos(self, phase=PHASE_ALL):
         _lib.check(self.lib.fcx_run_atmos(self.h, phase))

@@ -126,7 +126,8 @@ int fcx_commit(fcx_engine *e);
 int fcx_upload(fcx_engine *e, int phase);   /* H2D of host-bound inputs of the phase  */
 int fcx_run(fcx_engine *e, int phase, int32_t current_step_time); /* device compute  */
 int fcx_download(fcx_engine *e, int phase); /* D2H of host-bound outputs of the phase */
-int fcx_step(fcx_engine *e, int phase, int32_t current_step_time); /* the three above */
+/* the three above; with host-bound fields pipelined over cell chunks (FCX_OPT_PIPELINE_CHUNKS) */
+int fcx_step(fcx_engine *e, int phase, int32_t current_step_time);
 int fcx_synchronize(fcx_engine *e);
 
 /* ---- per call: the reference subroutines one by one (exact drop-in semantics; each
@@ -147,6 +148,8 @@ int fcx_do_regridding(fcx_engine *e, int var, int surface_type);           /* ba
 int fcx_device_ptr(fcx_engine *e, int surface_type, int grid, int var, double **dptr);
 /* device time (hipEvents on the engine stream) of the kernels of the last fcx_run */
 int fcx_last_kernel_ms(fcx_engine *e, float *ms);
+/* bytes of caller host memory page-locked by this engine (FCX_OPT_PIN_HOST) */
+int fcx_pinned_bytes(fcx_engine *e, int64_t *bytes);
 /* algorithmic HBM bytes of one fcx_run(phase) (each distinct array read once, written once) */
 int fcx_algorithmic_bytes(fcx_engine *e, int phase, int64_t *bytes);
 
@@ -179,7 +182,10 @@ enum fcx_option {
   FCX_OPT_MAX_BLOCKS = 2,       /* grid-stride cap in 256-thread blocks; 0 = no cap       */
   FCX_OPT_NONTEMPORAL = 3,      /* non-temporal hint on streamed loads/stores (default 1) */
   FCX_OPT_SPECIALIZE = 4,       /* T=1 CCLM/MOM5/RCO specialised kernels (default 1)      */
-  FCX_OPT_ATMOS_IN_RUN = 5      /* fcx_run also runs the atmosphere accumulation (def. 1) */
+  FCX_OPT_ATMOS_IN_RUN = 5,     /* fcx_run also runs the atmosphere accumulation (def. 1) */
+  FCX_OPT_PIN_HOST = 6,         /* page-lock the bound host arrays at fcx_commit (def. 1)  */
+  FCX_OPT_PIPELINE_CHUNKS = 7   /* fcx_step of host-bound fields: H2D/compute/D2H overlap
+                                   over this many cell chunks (default 8; 1 = sequential) */
 };
 int fcx_set_option(fcx_engine *e, int option, int64_t value);
 
