@@ -61,7 +61,8 @@ SWEEP = [("pageable, sequential", {"pin_host": 0, "pipeline_chunks": 1}),
          ("pinned, sequential", {"pin_host": 1, "pipeline_chunks": 1}),
          ("pinned, 4 chunks", {"pin_host": 1, "pipeline_chunks": 4}),
          ("pinned, 8 chunks", {"pin_host": 1, "pipeline_chunks": 8}),
-         ("pinned, 16 chunks", {"pin_host": 1, "pipeline_chunks": 16})]
+         ("pinned, 16 chunks", {"pin_host": 1, "pipeline_chunks": 16}),
+         ("zero-copy", {"zero_copy": 1})]
 N_IN = {"CCLM": 10, "MOM5": 11, "RCO": 5}
 N_OUT = {"CCLM": 7, "MOM5": 7, "RCO": 6}
 

@@ -1,0 +1,119 @@
+#!/usr/bin/env python3
+"""Config 2 of SURVEY.md 8d: the Baltic-size exchange grid (N = 32,768 cells, T = 1, all
+fluxes fused) on one MI355X.  The working set (~4.5 MB per variant) is LLC-resident, so the
+step is latency-bound: report microseconds per step, not an HBM fraction.
+
+  device   fields HBM-resident (torch tensors): fcx_run of CCLM, MOM5 and RCO back-to-back,
+           wall time per step over many steps (host launch cost included) and the kernels'
+           HIP-event time
+  host     fields in host arrays (the Fortran host's view): fcx_step per variant, through
+           device mirrors (H2D, kernel, D2H, synchronise) and zero-copy (the kernel reads and
+           writes the page-locked host arrays in place; the default at this size)
+  cpu      the reference flux_lib (oracle/_ref, else the C port) on one core, same cells
+
+  python components.flux_calculator_amd/bench/latency.py [--cells 32768] [--steps 2000]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.join(ROOT, "components.flux_calculator_amd", "python"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+VARIANTS = ("CCLM", "MOM5", "RCO")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--cells", type=int, default=32_768)
+    ap.add_argument("--steps", type=int, default=2000)
+    ap.add_argument("--bias", type=int, default=1)
+    a = ap.parse_args()
+
+    import torch
+    from fcx.basic import PHASE_ALL
+    from fcx.engine import Engine
+    from fcx.synthetic import build_case, inputs_for_bench
+
+    n = a.cells
+    host = inputs_for_bench(n)
+    out = {"cells": n, "steps": a.steps, "bias": bool(a.bias)}
+
+    # ---- device-resident: the three variants back-to-back per step
+    data = {k: torch.as_tensor(v).to("cuda:0") for k, v in host.items()}
+    stream = torch.cuda.current_stream()
+    engines = []
+    for v in VARIANTS:
+        c = build_case(v, n=n, T=1, bias=bool(a.bias), device="cuda:0", data=data)
+        engines.append(Engine(c.lf, 1, c.methods, corrections=c.corrections, stream=stream.cuda_stream))
+    for k in range(50):
+        for e in engines:
+            e.run(PHASE_ALL, k * 3600)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(a.steps):
+        for e in engines:
+            e.run(PHASE_ALL, k * 3600)
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - t0) / a.steps * 1e6
+    kern = {}
+    for v, e in zip(VARIANTS, engines):
+        ts = []
+        for k in range(200):
+            e.run(PHASE_ALL, k * 3600)
+            ts.append(e.last_kernel_ms() * 1e3)
+        kern[v] = round(float(np.median(ts)), 2)
+    for e in engines:
+        e.close()
+    out["device"] = {"us_per_step_3_variants": round(wall, 2), "kernel_us_median": kern,
+                     "Mcells_per_s": round(3 * n / wall, 1)}
+
+    # ---- host-bound: fcx_step per variant (upload, run, download, synchronise)
+    for mode, opts in (("host_mirrors", {"zero_copy": 0}), ("host_zero_copy", {"zero_copy": 1})):
+        hb = {}
+        for v in VARIANTS:
+            c = build_case(v, n=n, T=1, bias=bool(a.bias), data=host)
+            e = Engine(c.lf, 1, c.methods, corrections=c.corrections, options=opts)
+            for k in range(50):
+                e.step(PHASE_ALL, k * 3600)
+            ts = []
+            for k in range(min(a.steps, 1000)):
+                t0 = time.perf_counter()
+                e.step(PHASE_ALL, k * 3600)
+                ts.append(time.perf_counter() - t0)
+            e.run(PHASE_ALL, 0)
+            e.synchronize()
+            kms = e.last_kernel_ms()
+            e.close()
+            hb[v] = {"us_per_step_median": round(float(np.median(ts)) * 1e6, 1),
+                     "us_per_step_p90": round(float(np.percentile(ts, 90)) * 1e6, 1),
+                     "kernel_us": round(kms * 1e3, 1)}
+        out[mode] = hb
+
+    # ---- the reference on one core, same cells
+    import oracle_lib
+
+    kind = "ref" if oracle_lib.load("ref") is not None else "c"
+    cpu = {}
+    for v in VARIANTS:
+        c = build_case(v, n=n, T=1, bias=bool(a.bias), data=host)
+        st = oracle_lib.OracleState(c, 0)
+        oracle_lib.run_state(st, kind)
+        ts = []
+        for _ in range(20):
+            t0 = time.perf_counter()
+            oracle_lib.run_state(st, kind)
+            ts.append(time.perf_counter() - t0)
+        cpu[v] = round(float(np.median(ts)) * 1e6, 1)
+    out["cpu_1core_us_per_step"] = cpu
+    out["cpu_kind"] = "reference" if kind == "ref" else "port"
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -133,6 +133,9 @@ struct fcx_engine {
   // host-bound steps: page-locked caller arrays and the H2D / compute / D2H pipeline
   bool pin_host = true;
   int chunks = 8;                                   // fcx_step pipeline depth (1 = off)
+  int64_t min_chunk = 256 * 1024;                   // cells per chunk at least (~2 MB/array)
+  int zero_copy = 2;  // kernels use the host arrays in place: 0 off, 1 on, 2 auto (small grids)
+  bool zc_active = false;
   std::vector<std::pair<char *, size_t>> pinned;    // hipHostRegister'ed page ranges
   hipStream_t s_in = nullptr, s_out = nullptr;      // copy streams of the pipeline
   std::vector<hipEvent_t> ev_in, ev_comp;           // per chunk
@@ -798,12 +801,51 @@ static void pin_host_arrays(fcx_engine *e) {
     else
       m.push_back(x);
   }
+  const unsigned flags = e->zc_active ? hipHostRegisterMapped : hipHostRegisterDefault;
   for (auto &x : m) {
     char *p = reinterpret_cast<char *>(x.first);
-    if (hipHostRegister(p, x.second - x.first, hipHostRegisterDefault) == hipSuccess)
+    if (hipHostRegister(p, x.second - x.first, flags) == hipSuccess)
       e->pinned.push_back({p, x.second - x.first});
     else
       (void)hipGetLastError();  // e.g. already registered by the caller: leave it
+  }
+}
+
+// Zero-copy (FCX_OPT_ZERO_COPY): a host array inside a page-locked range is used by the
+// kernels in place through its device-visible address -- no device mirror, no copy call;
+// the cells kernel streams it over the host link.  For the latency-bound small grids this
+// replaces ~17 copy calls per step by one launch.  Arrays whose range was not registered
+// keep a mirror.
+static void map_host_arrays(fcx_engine *e) {
+  auto mapped = [&](void *host) -> void * {
+    const uintptr_t h = reinterpret_cast<uintptr_t>(host);
+    for (auto &r : e->pinned) {
+      const uintptr_t a = reinterpret_cast<uintptr_t>(r.first);
+      if (h >= a && h < a + r.second) {
+        void *d = nullptr;
+        if (hipHostGetDevicePointer(&d, r.first, 0) != hipSuccess || !d) {
+          (void)hipGetLastError();
+          return nullptr;
+        }
+        return reinterpret_cast<char *>(d) + (h - a);
+      }
+    }
+    return nullptr;
+  };
+  for (auto &bf : e->bufs) {
+    if (bf.external || !bf.host) continue;
+    if (void *d = mapped(bf.host)) {
+      bf.dev = reinterpret_cast<double *>(d);
+      bf.external = true;  // the engine neither owns nor copies it
+      if (reinterpret_cast<uintptr_t>(d) % 16) e->aligned16 = false;
+    }
+  }
+  for (auto &f : e->atm_fields) {
+    if (f.external || !f.out_host) continue;
+    if (void *d = mapped(f.out_host)) {
+      f.out_dev = reinterpret_cast<double *>(d);
+      f.external = true;
+    }
   }
 }
 
@@ -828,6 +870,12 @@ extern "C" int fcx_commit(fcx_engine *e) {
     if (e->n_atmos >= 0) return fail(FCX_E_UNSUPPORTED, "fp32 engine: the atmosphere accumulation runs in fp64 only");
   }
   if (int r = gpu_init(e)) return r;
+  // auto: zero-copy exactly where the pipelined step would not apply (grids below two
+  // chunks), i.e. where the step is latency-bound and per-array copies dominate it
+  const int64_t n_big = std::max(e->n[0], std::max(e->n[1], e->n[2]));
+  e->zc_active = e->zero_copy == 1 || (e->zero_copy == 2 && n_big < 2 * e->min_chunk);
+  if (e->pin_host || e->zc_active) pin_host_arrays(e);
+  if (e->zc_active) map_host_arrays(e);
   // one pooled allocation for all host-bound mirrors, 256-B aligned sub-buffers
   size_t total = 0;
   std::vector<size_t> off(e->bufs.size(), 0);
@@ -897,7 +945,6 @@ extern "C" int fcx_commit(fcx_engine *e) {
         }
     }
   }
-  if (e->pin_host) pin_host_arrays(e);
   e->committed = true;
   return FCX_OK;
 }
@@ -1108,7 +1155,10 @@ static int step_pipelined(fcx_engine *e, int phase, int32_t t, Plan *pl) {
   const double *corr_m = month_slice(e, t, &rc);
   if (rc) return rc;
   const int64_t n = pl->host.n_max;
-  const int64_t per = ((n + e->chunks - 1) / e->chunks + kChunkAlign - 1) / kChunkAlign * kChunkAlign;
+  // chunks of at least kMinChunk cells: a chunk costs one copy call per array and one launch,
+  // which only pays off once the chunk's copies are well above the call latency
+  const int64_t want = std::max<int64_t>((n + e->chunks - 1) / e->chunks, e->min_chunk);
+  const int64_t per = (want + kChunkAlign - 1) / kChunkAlign * kChunkAlign;
   const int K = (int)((n + per - 1) / per);
   while ((int)e->ev_in.size() < K) {
     hipEvent_t a, b;
@@ -1162,7 +1212,7 @@ extern "C" int fcx_step(fcx_engine *e, int phase, int32_t t) {
   if (e->chunks > 1 && !e->any_regrid) {
     Plan *pl;
     if (int r = get_plan(e, phase_stages(phase), phase, &pl)) return r;
-    if (host_bound(e, pl) && pl->host.n_max >= 2 * kChunkAlign) return step_pipelined(e, phase, t, pl);
+    if (host_bound(e, pl) && pl->host.n_max >= 2 * e->min_chunk) return step_pipelined(e, phase, t, pl);
   }
   if (int r = fcx_upload(e, phase)) return r;
   if (int r = fcx_run(e, phase, t)) return r;
@@ -1363,6 +1413,17 @@ extern "C" int fcx_set_option(fcx_engine *e, int option, int64_t value) {
     case FCX_OPT_PIN_HOST:
       if (e->committed) return fail(FCX_E_STATE, "pin_host is applied at fcx_commit");
       e->pin_host = value != 0;
+      return FCX_OK;
+    case FCX_OPT_ZERO_COPY:
+      if (e->committed) return fail(FCX_E_STATE, "zero_copy is applied at fcx_commit");
+      if (value < 0 || value > 2) return fail(FCX_E_ARG, "zero_copy: 0 off, 1 on, 2 auto");
+      e->zero_copy = (int)value;
+      return FCX_OK;
+    case FCX_OPT_PIPELINE_MIN_CHUNK:
+      if (value < kChunkAlign || value % kChunkAlign)
+        return fail(FCX_E_ARG, "pipeline min chunk %lld: a positive multiple of %lld cells", (long long)value,
+                    (long long)kChunkAlign);
+      e->min_chunk = value;
       return FCX_OK;
     case FCX_OPT_PIPELINE_CHUNKS:
       if (value < 1 || value > 1024) return fail(FCX_E_ARG, "pipeline chunks %lld outside 1..1024", (long long)value);

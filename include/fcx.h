@@ -184,8 +184,14 @@ enum fcx_option {
   FCX_OPT_SPECIALIZE = 4,       /* T=1 CCLM/MOM5/RCO specialised kernels (default 1)      */
   FCX_OPT_ATMOS_IN_RUN = 5,     /* fcx_run also runs the atmosphere accumulation (def. 1) */
   FCX_OPT_PIN_HOST = 6,         /* page-lock the bound host arrays at fcx_commit (def. 1)  */
-  FCX_OPT_PIPELINE_CHUNKS = 7   /* fcx_step of host-bound fields: H2D/compute/D2H overlap
+  FCX_OPT_PIPELINE_CHUNKS = 7,  /* fcx_step of host-bound fields: H2D/compute/D2H overlap
                                    over this many cell chunks (default 8; 1 = sequential) */
+  FCX_OPT_PIPELINE_MIN_CHUNK = 8, /* ... of at least this many cells (multiple of 1024;
+                                   default 262144: smaller grids take the sequential step) */
+  FCX_OPT_ZERO_COPY = 9         /* host-bound fields read/written by the kernels in place
+                                   through the host link (page-locked, mapped): no mirrors,
+                                   no copy calls.  0 off, 1 on, 2 auto (default): on when
+                                   every grid is below 2 x PIPELINE_MIN_CHUNK cells */
 };
 int fcx_set_option(fcx_engine *e, int option, int64_t value);
 

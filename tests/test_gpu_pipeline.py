@@ -30,6 +30,8 @@ def run(case, options, atmos_n=None):
         atmos = {"local": local_atmos(amap, 0, 1),
                  "fields": [(2, 1, 1, "MEVA", outs["MEVA"]), (2, 1, 1, "HSEN", outs["HSEN"]),
                             (2, 1, 2, "UMOM", outs["UMOM"])]}
+    # small test grids: let the pipeline cut chunks down to 1024 cells
+    options = {"pipeline_min_chunk": 1024, **options}
     eng = Engine(case.lf, case.num_surface_types, case.methods, corrections=case.corrections,
                  averages=case.averages, atmos=atmos, options=options)
     eng.step(PHASE_ALL, STEP_T)
@@ -80,3 +82,91 @@ def test_pinned_small_arrays_sharing_pages():
     a = run(case, {"pipeline_chunks": 2})
     b = run(case, {"pipeline_chunks": 1, "pin_host": 0})
     same_bits(a, b)
+
+
+def test_default_min_chunk_keeps_small_grids_sequential():
+    """Below 2 x 256K cells the default engine maps the host arrays (zero-copy auto) instead of
+    pipelining copies; same bits as the mirrored sequential step."""
+    case = build_case("RCO", n=70_000, T=1)
+    for k in case.outputs:
+        case.lf.field[k][:] = np.nan
+    eng = Engine(case.lf, 1, case.methods)
+    eng.step(PHASE_ALL, STEP_T)
+    a = {k: np.array(case.lf.field[k], copy=True) for k in case.outputs}
+    eng.close()
+    same_bits(a, run(case, {"pipeline_chunks": 1}))
+
+
+def steps_with_changing_inputs(case, options, steps=3):
+    """Several fcx_steps, the host rewriting every input between them (as oasis_get does):
+    zero-copy kernels must see each step's fresh host data and leave their writes visible."""
+    eng = Engine(case.lf, case.num_surface_types, case.methods, corrections=case.corrections,
+                 averages=case.averages, options=options)
+    inputs = [k for k in case.lf.field if k not in case.outputs]
+    seen, res = set(), []
+    orig = {}
+    for k in inputs:
+        a = case.lf.field[k]
+        if id(a) not in seen:
+            seen.add(id(a))
+            orig[id(a)] = a.copy()
+    for step in range(steps):
+        for k in inputs:
+            a = case.lf.field[k]
+            if k[2] in ("TSUR", "TATM", "UATM", "VATM", "QATM"):
+                a[:] = orig[id(a)] * (1.0 + 1e-3 * step)  # inputs of this step
+        for k in case.outputs:
+            case.lf.field[k][:] = np.nan
+        eng.step(PHASE_ALL, STEP_T + 3600 * step)
+        res.append({k: np.array(case.lf.field[k], copy=True) for k in case.outputs})
+    eng.close()
+    for k in inputs:  # restore
+        a = case.lf.field[k]
+        a[:] = orig[id(a)]
+    return res
+
+
+@pytest.mark.parametrize("variant", ["CCLM", "MOM5", "RCO"])
+def test_zero_copy_matches_mirrors_over_steps(variant):
+    case = build_case(variant, n=40_001, T=1, bias=True)
+    zc = steps_with_changing_inputs(case, {"zero_copy": 1})
+    mir = steps_with_changing_inputs(case, {"zero_copy": 0, "pipeline_chunks": 1})
+    for a, b in zip(zc, mir):
+        same_bits(a, b)
+    assert not any(np.isnan(v).any() for v in zc[-1].values())
+
+
+def test_zero_copy_generic_separate_grids_averages_and_atmosphere():
+    case = build_case("CCLM", n=9_001, T=3, sep_grids=(8_999, 9_011), bias=True)
+    same_bits(run(case, {"zero_copy": 1}), run(case, {"zero_copy": 0}))
+    ref = oracle_lib.run_case(case, "c", current_step_time=STEP_T)
+    assert_parity(run(case, {"zero_copy": 1}), ref, label="zero-copy T3 sep")
+    c1 = build_case("MOM5", n=30_001, T=1, bias=True)
+    same_bits(run(c1, {"zero_copy": 1}, atmos_n=30_001), run(c1, {"zero_copy": 0}, atmos_n=30_001))
+
+
+def test_zero_copy_per_call_dropin():
+    """The per-call reference subroutines on a zero-copy engine (no copies at all)."""
+    from fcx.basic import IDX
+
+    case = build_case("CCLM", n=5_003, T=2, bias=True)
+    ref = oracle_lib.run_case(case, "c", current_step_time=STEP_T)
+    for k in case.outputs:
+        case.lf.field[k][:] = np.nan
+    eng = Engine(case.lf, 2, case.methods, corrections=case.corrections, averages=case.averages,
+                 options={"zero_copy": 1})
+    assert eng.pinned_bytes() > 0
+    lib, h = eng.lib, eng.h
+    assert lib.fcx_calc_flux_radiation_blackbody(h) == 0
+    for g in (1, 2, 3):
+        assert lib.fcx_calc_spec_vapor_surface(h, g) == 0
+    assert lib.fcx_calc_flux_mass_evap(h, STEP_T) == 0
+    assert lib.fcx_calc_flux_heat_latent(h) == 0
+    assert lib.fcx_calc_flux_heat_sensible(h) == 0
+    assert lib.fcx_calc_flux_momentum_east(h, 2) == 0
+    assert lib.fcx_calc_flux_momentum_north(h, 3) == 0
+    for ph, g, name in case.averages:
+        assert lib.fcx_average_across_surface_types(h, g, IDX[name]) == 0
+    got = {k: np.array(case.lf.field[k], copy=True) for k in case.outputs}
+    eng.close()
+    assert_parity(got, ref, label="zero-copy per call")
