@@ -340,9 +340,12 @@ __global__ __launch_bounds__(256) void cells_kernel(const Params *__restrict__ P
 // The T=1 hot path with the exchange -> atmosphere accumulation fused in (AtmosFused).
 // Wave-uniform loop over 128-cell wave tiles (lane l: cells 2l, 2l+1).  Each flux is
 // turned into the product w*x the moment it is produced and parked in the wave's own LDS
-// region (nothing extra stays live in registers); after the cell pass a wave-local fence,
-// then every lane holding the first cell of an atmosphere segment sums the segment from LDS
-// in link order.  A segment that runs past the wave tile leaves its prefix in carry[tile].
+// region (nothing extra stays live in registers).  Segment boundaries come from two wave
+// ballots of "this cell's atmosphere cell differs from the previous one": the lane holding
+// a segment's first cell finds the segment end with a count-trailing-zeros, so after a
+// wave-local fence it sums the segment's products from LDS in link order with a known trip
+// count (no index re-reads, no dependent loop exit).  A segment that runs past the wave
+// tile leaves its prefix in carry[tile].
 struct LdsEmit {
   double *p;  // this wave's [kFusedFields][kTile] products
   double w0, w1;
@@ -360,24 +363,27 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// lowest set bit index of m, 64 if none
+__device__ __forceinline__ int first_bit(uint64_t m) { return m ? __builtin_ctzll(m) : 64; }
+
 template <int VAR, bool NT>
 __global__ __launch_bounds__(256) void cells_atmos_kernel(const Params *__restrict__ P,
                                                           const double *__restrict__ corr_m,
                                                           const AtmosFused af, int64_t lo, int64_t hi) {
   __shared__ double s_p[4][kFusedFields * kTile];
-  __shared__ int32_t s_idx[4][kTile];
   const int64_t n = P->n_max;
   const int64_t n_tiles = (hi + kTile - 1) / kTile;  // tiles [lo/kTile, n_tiles) of this launch
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   double *wp = s_p[wv];
-  int32_t *wi = s_idx[wv];
   const int64_t waves = (int64_t)gridDim.x * (blockDim.x >> 6);
   const int64_t wave0 = (int64_t)blockIdx.x * (blockDim.x >> 6) + wv;
+  const uint64_t at_or_above = ~0ull << lane;
+  const uint64_t above = lane == 63 ? 0ull : (~0ull << (lane + 1));
   for (int64_t tile = lo / kTile + wave0; tile < n_tiles; tile += waves) {
     const int64_t t0 = tile * kTile;
     const int64_t j0 = t0 + 2 * lane;
     LdsEmit emit{wp, 0.0, 0.0, 2 * lane};
-    int32_t a0 = -1, a1 = -1;
+    int32_t a0 = -1, a1 = -1;  // -1: past the grid end
     if (j0 + 2 <= n) {
       const int2 ii = *reinterpret_cast<const int2 *>(af.idx + j0);
       const d2 ww = __builtin_nontemporal_load(reinterpret_cast<const d2 *>(af.w + j0));
@@ -389,28 +395,35 @@ __global__ __launch_bounds__(256) void cells_atmos_kernel(const Params *__restri
       a0 = af.idx[j0];
       emit.w0 = af.w[j0];
     }
-    wi[2 * lane] = a0;
-    wi[2 * lane + 1] = a1;
-    if (j0 < n) process<2, true, VAR, NT, double>(P, corr_m, j0, emit);
-    wave_sync();  // the wave's LDS products are visible to all its lanes
+    const int32_t prev_tile = t0 > 0 ? af.idx[t0 - 1] : -2;  // wave-uniform loads
     const int64_t tend = t0 + kTile;
     const int32_t next_a = (tend < n) ? af.idx[tend] : -3;
+    if (j0 < n) process<2, true, VAR, NT, double>(P, corr_m, j0, emit);
+    // segment starts: cell 2l+i begins a segment when its atmosphere cell differs from the
+    // previous cell's (the first cell past the grid end also "starts", which ends the last
+    // real segment)
+    int32_t prev = __shfl_up(a1, 1);
+    if (lane == 0) prev = prev_tile;
+    const bool s0 = a0 != prev, s1 = a1 != a0;
+    const uint64_t m0 = __ballot(s0), m1 = __ballot(s1);
+    wave_sync();  // the wave's LDS products are visible to all its lanes
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
+      const int32_t a = i ? a1 : a0;
+      if (!(i ? s1 : s0) || a < 0) continue;
       const int c = 2 * lane + i;
-      const int32_t a = wi[c];
-      if (a < 0) continue;
-      const int32_t before = (c == 0) ? (t0 > 0 ? af.idx[t0 - 1] : -2) : wi[c - 1];
-      if (before == a) continue;  // not the first cell of its segment
+      // next start after cell c: an even cell 2j (j > l) or an odd cell 2j+1 (j >= l for
+      // c even, j > l for c odd)
+      const int e_end = min(2 * first_bit(m0 & above), 2 * first_bit(m1 & (i ? above : at_or_above)) + 1);
+      const int end = min(e_end, kTile);
       double acc[kFusedFields];
 #pragma unroll
       for (int k = 0; k < kFusedFields; ++k) acc[k] = 0.0;
-      int e = c;
-      for (; e < kTile && wi[e] == a; ++e) {
+      for (int e = c; e < end; ++e) {
 #pragma unroll
         for (int k = 0; k < kFusedFields; ++k) acc[k] = acc[k] + wp[k * kTile + e];
       }
-      const bool cont = e == kTile && next_a == a;
+      const bool cont = end == kTile && next_a == a;
 #pragma unroll
       for (int k = 0; k < kFusedFields; ++k) {
         if (!af.out[k]) continue;
