@@ -146,7 +146,10 @@ def main():
                      "shared": (shared[i * nb * stride:], stride) if nb else None}
         e = Engine(c.lf, c.num_surface_types, c.methods, corrections=c.corrections,
                    averages=c.averages, device=local_rank, stream=stream.cuda_stream, atmos=atmos,
-                   options={"atmos_in_run": 0})
+                   # per-kernel times come from the bench's own events on the same stream;
+                   # the engine's internal ones would add a second event pair per launch
+                   # (measured +2.5 % per step, components.flux_calculator_amd/bench/event_probe.py)
+                   options={"atmos_in_run": 0, "timing": 0})
         cases.append(c)
         engines.append(e)
     # algorithmic bytes of one fcx_run: every distinct field array read once / written once,

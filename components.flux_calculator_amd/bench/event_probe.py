@@ -1,0 +1,80 @@
+#!/usr/bin/env python3
+"""Does timing perturb the step?  The bench's coupling step (CCLM, MOM5, RCO fused kernels
+back-to-back, 10M cells, fields in HBM) timed by wall clock over many steps, with and
+without HIP events recorded between the kernels, and with the engines' own per-run events
+on or off (FCX_OPT_TIMING).  Interleaved rounds, medians.
+
+  python components.flux_calculator_amd/bench/event_probe.py [--cells N] [--steps K]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.join(ROOT, "components.flux_calculator_amd", "python"))
+ATM = (("MEVA", 1), ("HLAT", 1), ("HSEN", 1), ("RBBR", 1), ("UMOM", 2), ("VMOM", 3))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--cells", type=int, default=10_000_000)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--rounds", type=int, default=5)
+    a = ap.parse_args()
+    import torch
+
+    from fcx.basic import PHASE_ALL, PHASE_NORMAL
+    from fcx.engine import Engine
+    from fcx.parallel import PeriodicAtmosMap
+    from fcx.synthetic import build_case, inputs_for_bench
+
+    n = a.cells
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.current_stream(dev)
+    data = {k: torch.as_tensor(v).to(dev) for k, v in inputs_for_bench(n).items()}
+    la = PeriodicAtmosMap().local(0, n, 0, 1, n)
+    engines = []
+    for v in ("CCLM", "MOM5", "RCO"):
+        c = build_case(v, n=n, T=1, device=dev, data=data)
+        outs = [torch.empty(la.n_atmos, dtype=torch.float64, device=dev) for _ in ATM]
+        atmos = {"local": la, "fields": [(PHASE_NORMAL, 1, g, name, o) for (name, g), o in zip(ATM, outs)]}
+        engines.append((c, outs, Engine(c.lf, 1, c.methods, device=0, stream=stream.cuda_stream,
+                                        atmos=atmos, options={"atmos_in_run": 0})))
+
+    def run(mode):
+        torch_events = mode in ("torch_events", "both")
+        fcx_timing = mode in ("fcx_timing", "both")
+        for _, _, e in engines:
+            e.set_option("timing", int(fcx_timing))
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in engines]
+        for _, _, e in engines:
+            e.run(PHASE_ALL, 0)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for k in range(a.steps):
+            for i, (_, _, e) in enumerate(engines):
+                if torch_events:
+                    evs[i][0].record(stream)
+                e.run(PHASE_ALL, k * 3600)
+                if torch_events:
+                    evs[i][1].record(stream)
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / a.steps * 1e3
+
+    modes = ["none", "torch_events", "fcx_timing", "both"]
+    res = {m: [] for m in modes}
+    for r in range(a.rounds):
+        order = list(modes)
+        np.random.default_rng(r).shuffle(order)
+        for m in order:
+            res[m].append(run(m))
+    out = {m: round(float(np.median(v)), 4) for m, v in res.items()}
+    print(json.dumps({"ms_per_step_median": out, "cells": n, "steps": a.steps, "rounds": a.rounds}))
+
+
+if __name__ == "__main__":
+    main()

@@ -136,6 +136,7 @@ struct fcx_engine {
   int64_t min_chunk = 256 * 1024;                   // cells per chunk at least (~2 MB/array)
   int zero_copy = 2;  // kernels use the host arrays in place: 0 off, 1 on, 2 auto (small grids)
   bool zc_active = false;
+  bool timing = true;  // ev0/ev1 around every run (fcx_last_kernel_ms)
   std::vector<std::pair<char *, size_t>> pinned;    // hipHostRegister'ed page ranges
   hipStream_t s_in = nullptr, s_out = nullptr;      // copy streams of the pipeline
   std::vector<hipEvent_t> ev_in, ev_comp;           // per chunk
@@ -1104,7 +1105,7 @@ extern "C" int fcx_run(fcx_engine *e, int phase, int32_t t) {
   int rc;
   const double *corr_m = month_slice(e, t, &rc);
   if (rc) return rc;
-  HIP_TRY(hipEventRecord(e->ev0, e->stream));
+  if (e->timing) HIP_TRY(hipEventRecord(e->ev0, e->stream));
   e->atm_done_fused = false;
   if (!e->any_regrid) {
     Plan *pl;
@@ -1126,8 +1127,8 @@ extern "C" int fcx_run(fcx_engine *e, int phase, int32_t t) {
   }
   if (e->atmos_in_run && !e->atm_done_fused)
     if (int r = run_atmos(e, phase)) return r;
-  HIP_TRY(hipEventRecord(e->ev1, e->stream));
-  e->timed = true;
+  if (e->timing) HIP_TRY(hipEventRecord(e->ev1, e->stream));
+  e->timed = e->timing;
   return FCX_OK;
 }
 
@@ -1167,7 +1168,7 @@ static int step_pipelined(fcx_engine *e, int phase, int32_t t, Plan *pl) {
     e->ev_in.push_back(a);
     e->ev_comp.push_back(b);
   }
-  HIP_TRY(hipEventRecord(e->ev0, e->s_in));
+  if (e->timing) HIP_TRY(hipEventRecord(e->ev0, e->s_in));
   e->atm_done_fused = false;
   for (int k = 0; k < K; ++k) {
     const int64_t lo = k * per, hi = std::min(n, lo + per);
@@ -1191,8 +1192,8 @@ static int step_pipelined(fcx_engine *e, int phase, int32_t t, Plan *pl) {
       if ((f.phase & phase) && !f.external && e->n_atmos > 0)
         HIP_TRY(hipMemcpyAsync(f.out_host, f.out_dev, e->n_atmos * sizeof(double), hipMemcpyDeviceToHost,
                                e->s_out));
-  HIP_TRY(hipEventRecord(e->ev1, e->s_out));
-  e->timed = true;
+  if (e->timing) HIP_TRY(hipEventRecord(e->ev1, e->s_out));
+  e->timed = e->timing;
   HIP_TRY(hipStreamSynchronize(e->s_out));
   HIP_TRY(hipStreamSynchronize(e->stream));
   return FCX_OK;
@@ -1235,10 +1236,10 @@ static int per_call(fcx_engine *e, uint32_t stages, int avg_phases, int32_t t) {
   const double *corr_m = (stages & S_MEVA) ? month_slice(e, t, &rc) : nullptr;
   if ((stages & S_MEVA) && rc) return rc;
   if (int r = copy_bufs(e, pl->reads, true)) return r;
-  HIP_TRY(hipEventRecord(e->ev0, e->stream));
+  if (e->timing) HIP_TRY(hipEventRecord(e->ev0, e->stream));
   if (int r = launch_plan(e, pl, corr_m)) return r;
-  HIP_TRY(hipEventRecord(e->ev1, e->stream));
-  e->timed = true;
+  if (e->timing) HIP_TRY(hipEventRecord(e->ev1, e->stream));
+  e->timed = e->timing;
   if (int r = copy_bufs(e, pl->writes, false)) return r;
   return fcx_synchronize(e);
 }
@@ -1413,6 +1414,10 @@ extern "C" int fcx_set_option(fcx_engine *e, int option, int64_t value) {
     case FCX_OPT_PIN_HOST:
       if (e->committed) return fail(FCX_E_STATE, "pin_host is applied at fcx_commit");
       e->pin_host = value != 0;
+      return FCX_OK;
+    case FCX_OPT_TIMING:
+      e->timing = value != 0;
+      if (!e->timing) e->timed = false;
       return FCX_OK;
     case FCX_OPT_ZERO_COPY:
       if (e->committed) return fail(FCX_E_STATE, "zero_copy is applied at fcx_commit");

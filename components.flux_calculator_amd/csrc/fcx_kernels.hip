@@ -346,14 +346,21 @@ __global__ __launch_bounds__(256) void cells_kernel(const Params *__restrict__ P
 // wave-local fence it sums the segment's products from LDS in link order with a known trip
 // count (no index re-reads, no dependent loop exit).  A segment that runs past the wave
 // tile leaves its prefix in carry[tile].
+// LDS row of one field: the products of cell e sit at slot(e) = e + 2*(e/16), i.e. one
+// 16-B pad slot after every 16 cells.  Unpadded, cells 16 apart share a bank pair of the
+// 16-lane ds_read2_b64 groups and the segment-start lanes (3-5 cells apart) collide; the
+// pad shifts every 16-cell block by 2 banks and keeps the pair (2l, 2l+1) 16-B aligned.
+constexpr int kRow = kTile + 2 * (kTile / 16);
+__device__ __forceinline__ int lds_slot(int e) { return e + 2 * (e >> 4); }
+
 struct LdsEmit {
-  double *p;  // this wave's [kFusedFields][kTile] products
+  double *p;  // this wave's [kFusedFields][kRow] products
   double w0, w1;
-  int c;      // 2 * lane
+  int s;      // lds_slot(2 * lane)
   template <int C, class R>
   __device__ __forceinline__ void operator()(int k, const Vec<C, R> &x) const {
     const d2 q = {w0 * x.v[0], w1 * x.v[1]};  // one 16-B LDS store per field
-    *reinterpret_cast<d2 *>(p + k * kTile + c) = q;
+    *reinterpret_cast<d2 *>(p + k * kRow + s) = q;
   }
 };
 
@@ -370,7 +377,7 @@ template <int VAR, bool NT>
 __global__ __launch_bounds__(256) void cells_atmos_kernel(const Params *__restrict__ P,
                                                           const double *__restrict__ corr_m,
                                                           const AtmosFused af, int64_t lo, int64_t hi) {
-  __shared__ double s_p[4][kFusedFields * kTile];
+  __shared__ double s_p[4][kFusedFields * kRow];
   const int64_t n = P->n_max;
   const int64_t n_tiles = (hi + kTile - 1) / kTile;  // tiles [lo/kTile, n_tiles) of this launch
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -382,7 +389,7 @@ __global__ __launch_bounds__(256) void cells_atmos_kernel(const Params *__restri
   for (int64_t tile = lo / kTile + wave0; tile < n_tiles; tile += waves) {
     const int64_t t0 = tile * kTile;
     const int64_t j0 = t0 + 2 * lane;
-    LdsEmit emit{wp, 0.0, 0.0, 2 * lane};
+    LdsEmit emit{wp, 0.0, 0.0, lds_slot(2 * lane)};
     int32_t a0 = -1, a1 = -1;  // -1: past the grid end
     if (j0 + 2 <= n) {
       const int2 ii = *reinterpret_cast<const int2 *>(af.idx + j0);
@@ -420,8 +427,9 @@ __global__ __launch_bounds__(256) void cells_atmos_kernel(const Params *__restri
 #pragma unroll
       for (int k = 0; k < kFusedFields; ++k) acc[k] = 0.0;
       for (int e = c; e < end; ++e) {
+        const double *q = wp + lds_slot(e);
 #pragma unroll
-        for (int k = 0; k < kFusedFields; ++k) acc[k] = acc[k] + wp[k * kTile + e];
+        for (int k = 0; k < kFusedFields; ++k) acc[k] = acc[k] + q[k * kRow];
       }
       const bool cont = end == kTile && next_a == a;
 #pragma unroll
