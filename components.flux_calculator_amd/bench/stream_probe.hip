@@ -48,6 +48,12 @@ __global__ __launch_bounds__(256) void probe(Ptrs p, long n) {
         acc[0] += NT ? __builtin_nontemporal_load(p.in[r] + u) : p.in[r][u];
       }
     }
+    if constexpr (W == 0) {  // read-only: keep the loads alive without a real store stream
+      bool hit = false;
+#pragma unroll
+      for (int i = 0; i < C; ++i) hit = hit || acc[i] == 1234.5;
+      if (hit) p.out[0][u] = acc[0];
+    }
 #pragma unroll
     for (int w = 0; w < W; ++w) {
       if constexpr (C == 2) {
@@ -90,8 +96,11 @@ int run(const char *name, Ptrs &p, long n, int blocks) {
 }
 
 int main() {
-  const long n = 10'000'000;
-  Ptrs p;
+  // 10M cells x 8 B = 80 MB per array: a 17-array step (1.36 GB) is far beyond the 256 MB
+  // Infinity Cache.  The 1-in/1-out copy uses 100M-element arrays (1.6 GB per launch) for
+  // the same reason -- at 10M (160 MB) it would run from the Infinity Cache.
+  const long n = 10'000'000, n_copy = 100'000'000;
+  Ptrs p, pc;
   for (int i = 0; i < 16; ++i) {
     double *x;
     CHECK(hipMalloc(&x, n * sizeof(double)));
@@ -99,18 +108,31 @@ int main() {
     p.in[i] = x;
     CHECK(hipMalloc(&p.out[i], n * sizeof(double)));
   }
-  for (int blocks : {1024, 2048, 4096, 8192, 19532}) {
-    run<1, 1, 2, false>("copy", p, n, blocks);
-    run<10, 7, 2, false>("cclm-shape", p, n, blocks);
+  for (int i = 0; i < 16; ++i) pc.in[i] = nullptr, pc.out[i] = nullptr;
+  {
+    double *x, *y;
+    CHECK(hipMalloc(&x, n_copy * sizeof(double)));
+    CHECK(hipMemset(x, 0, n_copy * sizeof(double)));
+    CHECK(hipMalloc(&y, n_copy * sizeof(double)));
+    pc.in[0] = x;
+    pc.out[0] = y;
   }
-  run<1, 1, 4, false>("copy", p, n, 2048);
+  for (int blocks : {2048, 8192, 0}) {
+    run<1, 1, 2, false>("copy 1.6 GB", pc, n_copy, blocks ? blocks : (int)(n_copy / 2 / 256));
+    run<1, 1, 2, true>("copy 1.6 GB nt", pc, n_copy, blocks ? blocks : (int)(n_copy / 2 / 256));
+  }
+  for (int blocks : {1024, 2048, 4096, 8192, 19532}) run<10, 7, 2, false>("cclm-shape", p, n, blocks);
   run<10, 7, 1, false>("cclm-shape", p, n, 2048);
   run<10, 7, 4, false>("cclm-shape", p, n, 2048);
   run<10, 7, 2, true>("cclm-shape", p, n, 2048);
   run<10, 7, 4, true>("cclm-shape", p, n, 2048);
   run<11, 7, 2, false>("mom5-shape", p, n, 2048);
   run<5, 6, 2, false>("rco-shape", p, n, 2048);
-  run<17, 0, 2, false>("read-only 17", p, n, 2048);
+  run<16, 0, 2, false>("read-only 16", p, n, 2048);
+  run<16, 0, 2, true>("read-only 16 nt", p, n, 2048);
+  run<10, 7, 2, true>("cclm-shape nt", p, n, 8192);
+  run<11, 7, 2, true>("mom5-shape nt", p, n, 8192);
+  run<5, 6, 2, true>("rco-shape nt", p, n, 8192);
   run<1, 16, 2, false>("write-heavy 1/16", p, n, 2048);
   return 0;
 }
