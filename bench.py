@@ -46,6 +46,7 @@ def parse():
     p.add_argument("--bias", action="store_true", help="monthly evaporation bias corrections")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget")
     p.add_argument("--cpu-cells", type=int, default=1_000_000)
+    p.add_argument("--cpu-cells-mt", type=int, default=4_000_000, help="all-cores CPU sample")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--atmos", type=int, default=1,
                    help="exchange->atmosphere accumulation (+ one RCCL all-reduce when N>1)")
@@ -83,6 +84,38 @@ def cpu_baseline(args, variants):
         "sample": f"{reps} coupling steps x {len(variants)} variants ({'+'.join(variants)}) over "
                   f"{n} cells, T={args.types}, reference call order, {el:.1f} s on 1 thread",
     }
+
+
+def cpu_all_cores(args, variants):
+    """SURVEY.md 8d CPU timing (ii): every host core available to this process, OpenMP over
+    contiguous APPLE ranges (the reference's MPI range decomposition), the C port of the
+    path (oracle/fco.c, bit-matched to the reference flux_lib), same workload shape."""
+    import ctypes
+
+    import oracle_lib
+    from fcx.synthetic import build_case, inputs_for_bench
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    n = args.cpu_cells_mt
+    data = inputs_for_bench(n)
+    cases = [build_case(v, n=n, T=args.types, bias=args.bias, data=data if args.types == 1 else None)
+             for v in variants]
+    lib, _ = oracle_lib.load("c")
+    states = [oracle_lib.OracleState(c, 0) for c in cases]
+    for st in states:
+        lib.fco_step_threads(ctypes.byref(st.st), threads)
+    cells, t0, reps = 0, time.perf_counter(), 0
+    while True:
+        for st in states:
+            lib.fco_step_threads(ctypes.byref(st.st), threads)
+            cells += n
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= args.cpu_seconds / 2 and reps >= 2:
+            break
+    return {"value": cells / el / 1e6, "unit": "Mcells/s", "cores": threads, "kind": "port",
+            "sample": f"{reps} coupling steps x {len(variants)} variants over {n} cells, OpenMP "
+                      f"APPLE ranges on {threads} threads, {el:.1f} s"}
 
 
 def main():
@@ -170,8 +203,11 @@ def main():
             for e in engines:
                 e.atmos_finish()
 
+    # config 5 (--bias): hourly steps whose timed half crosses 1961-01-31 -> 02-01, so the
+    # bias month slice changes inside the timed region (init_date 19610101)
+    t_base = 31 * 86400 - 3600 * (args.steps // 2) if args.bias else 0
     for w in range(args.warmup):
-        step(w * 3600)
+        step(t_base + w * 3600)
     torch.cuda.synchronize()
 
     ev = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -181,7 +217,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        step(k * 3600, ev[k])
+        step(t_base + k * 3600, ev[k])
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -262,6 +298,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu:
         cb = cpu_baseline(args, variants)
         out["cpu_baseline"] = cb
+        out["cpu_baseline_all_cores"] = cpu_all_cores(args, variants)
     if rank == 0:
         print(json.dumps(out), flush=True)
     for e in engines:

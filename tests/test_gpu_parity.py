@@ -238,3 +238,32 @@ def test_golden_reference_outputs(stem):
            for k in spec["outputs"]}
     got = fused(case, t=tg.MANIFEST["step_time"], phases=(PHASE_EARLY, PHASE_NORMAL))
     assert_parity(got, ref, label=stem)
+
+
+@pytest.mark.parametrize("variant", ["CCLM", "MOM5", "RCO"])
+def test_fp64_tolerance_report_config5(variant):
+    """SURVEY.md 8d tolerance row: per field the mixed error (the gate), the plain elementwise
+    max relative error, the count of cells above 1e-10 and error percentiles, on config 5
+    (bias on, 32,768 cells, a step in February).  Written to gpurun_out/ for profiles/."""
+    import json
+    import os
+
+    n = 32_768
+    case = build_case(variant, n=n, T=1, bias=True)
+    ref = oracle_lib.run_case(case, "c", current_step_time=STEP_T)
+    got = fused(case)
+    worst = assert_parity(got, ref, label=case.name)
+    rep = {}
+    for key, r in ref.items():
+        g = np.asarray(got[key])
+        nz = np.abs(r) > 0
+        rel = np.zeros_like(r)
+        rel[nz] = np.abs(g[nz] - r[nz]) / np.abs(r[nz])
+        rep["%d:%d:%s" % key] = {"mixed": worst[key], "max_rel": float(rel.max()),
+                                 "cells_rel_gt_1e-10": int((rel > 1e-10).sum()),
+                                 "p50_rel": float(np.percentile(rel, 50)), "p99_rel": float(np.percentile(rel, 99)),
+                                 "bit_identical_cells": int((g == r).sum()), "cells": int(r.size)}
+    out = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out")
+    os.makedirs(out, exist_ok=True)
+    with open(os.path.join(out, f"fp64_error_{variant}.json"), "w") as f:
+        json.dump(rep, f, indent=1)
