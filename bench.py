@@ -50,6 +50,9 @@ def parse():
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--atmos", type=int, default=1,
                    help="exchange->atmosphere accumulation (+ one RCCL all-reduce when N>1)")
+    p.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL)")
+    p.add_argument("--same-device", action="store_true",
+                   help="rehearsal only: every rank on GPU 0 (with --backend gloo on a 1-GPU box)")
     p.add_argument("--precision", choices=("f64", "f32"), default="f64",
                    help="f32: the fp32 cell-pass variant (config 5; no atmosphere accumulation)")
     return p.parse_args()
@@ -128,10 +131,14 @@ def main():
     import torch
     import torch.distributed as dist
 
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    gpu = 0 if args.same_device else local_rank
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.backend)
 
     from fcx.basic import PHASE_ALL, PHASE_NORMAL
     from fcx.engine import Engine
@@ -178,7 +185,7 @@ def main():
             atmos = {"local": la, "fields": [(PHASE_NORMAL, 1, g, name, outs[name]) for name, g in atm_fields],
                      "shared": (shared[i * nb * stride:], stride) if nb else None}
         e = Engine(c.lf, c.num_surface_types, c.methods, corrections=c.corrections,
-                   averages=c.averages, device=local_rank, stream=stream.cuda_stream, atmos=atmos,
+                   averages=c.averages, device=gpu, stream=stream.cuda_stream, atmos=atmos,
                    # per-kernel times come from the bench's own events on the same stream;
                    # the engine's internal ones would add a second event pair per launch
                    # (measured +2.5 % per step, components.flux_calculator_amd/bench/event_probe.py)
@@ -276,7 +283,8 @@ def main():
             "surface_types": args.types,
             "bias_corrections": bool(args.bias),
             "grids": "u/v grids = t grid",
-            "parallelism": f"dp{world} (APPLE contiguous cell ranges)",
+            "parallelism": f"dp{world} (APPLE contiguous cell ranges)"
+                           + (f", REHEARSAL: all ranks on GPU 0 over {args.backend}" if args.same_device else ""),
             "atmos_accumulation": (f"6 fluxes -> {la.n_atmos} atmosphere cells per GPU (1 per ~4 "
                                    "exchange cells), one all-reduce of the shared boundary cells per step"
                                    if la is not None else "off"),
