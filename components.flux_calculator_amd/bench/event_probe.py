@@ -24,6 +24,11 @@ def main():
     ap.add_argument("--cells", type=int, default=10_000_000)
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--order", default="CCLM,MOM5,RCO", help="engine creation order")
+    ap.add_argument("--atmos", type=int, default=1)
+    ap.add_argument("--spacer-mb", type=int, default=0, help="allocation between inputs and engines")
+    ap.add_argument("--engines-reversed", action="store_true",
+                    help="allocate all cases first, then create the engines in reverse order")
     a = ap.parse_args()
     import torch
 
@@ -37,13 +42,21 @@ def main():
     stream = torch.cuda.current_stream(dev)
     data = {k: torch.as_tensor(v).to(dev) for k, v in inputs_for_bench(n).items()}
     la = PeriodicAtmosMap().local(0, n, 0, 1, n)
-    engines = []
-    for v in ("CCLM", "MOM5", "RCO"):
+    spacer = torch.empty(a.spacer_mb << 20, dtype=torch.uint8, device=dev) if a.spacer_mb else None  # noqa: F841
+    cases = []
+    for v in a.order.split(","):
         c = build_case(v, n=n, T=1, device=dev, data=data)
         outs = [torch.empty(la.n_atmos, dtype=torch.float64, device=dev) for _ in ATM]
         atmos = {"local": la, "fields": [(PHASE_NORMAL, 1, g, name, o) for (name, g), o in zip(ATM, outs)]}
-        engines.append((c, outs, Engine(c.lf, 1, c.methods, device=0, stream=stream.cuda_stream,
-                                        atmos=atmos, options={"atmos_in_run": 0})))
+        cases.append((c, outs, atmos if a.atmos else None))
+    made = {}
+    order = range(len(cases) - 1, -1, -1) if a.engines_reversed else range(len(cases))
+    for i in order:
+        c, outs, atmos = cases[i]
+        made[i] = (c, outs, Engine(c.lf, 1, c.methods, device=0, stream=stream.cuda_stream,
+                                   atmos=atmos, options={"atmos_in_run": 0}))
+        made[i][2].run(PHASE_ALL, 0)  # plan + Params allocated now, in creation order
+    engines = [made[i] for i in range(len(cases))]
 
     def run(mode):
         torch_events = mode in ("torch_events", "both")
@@ -65,6 +78,24 @@ def main():
         torch.cuda.synchronize()
         return (time.perf_counter() - t0) / a.steps * 1e3
 
+    # predecessor effect: kernel Y timed right after kernel X (one event pair around Y only)
+    pairs = {}
+    for _, _, e in engines:
+        e.set_option("timing", 0)
+    names = tuple(f"{v}#{i}" for i, v in enumerate(a.order.split(",")))
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for x in range(len(engines)):
+        for y in range(len(engines)):
+            ts = []
+            for r in range(15):
+                engines[x][2].run(PHASE_ALL, 0)
+                ev0.record(stream)
+                engines[y][2].run(PHASE_ALL, 0)
+                ev1.record(stream)
+                ev1.synchronize()
+                ts.append(ev0.elapsed_time(ev1))
+            pairs[f"{names[y]} after {names[x]}"] = round(float(np.median(ts)), 4)
+
     modes = ["none", "torch_events", "fcx_timing", "both"]
     res = {m: [] for m in modes}
     for r in range(a.rounds):
@@ -72,8 +103,9 @@ def main():
         np.random.default_rng(r).shuffle(order)
         for m in order:
             res[m].append(run(m))
-    out = {m: round(float(np.median(v)), 4) for m, v in res.items()}
-    print(json.dumps({"ms_per_step_median": out, "cells": n, "steps": a.steps, "rounds": a.rounds}))
+    out = {m: round(float(np.median(v)), 4) for m, v in res.items() if v}
+    print(json.dumps({"ms_per_step_median": out, "kernel_ms_after": pairs, "cells": n, "steps": a.steps,
+                      "rounds": a.rounds}))
 
 
 if __name__ == "__main__":

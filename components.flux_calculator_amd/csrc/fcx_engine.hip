@@ -273,8 +273,6 @@ static int gpu_init(fcx_engine *e) {
   }
   HIP_TRY(hipEventCreate(&e->ev0));
   HIP_TRY(hipEventCreate(&e->ev1));
-  HIP_TRY(hipStreamCreateWithFlags(&e->s_in, hipStreamNonBlocking));
-  HIP_TRY(hipStreamCreateWithFlags(&e->s_out, hipStreamNonBlocking));
   e->gpu_ready = true;
   return FCX_OK;
 }
@@ -1161,6 +1159,10 @@ static int step_pipelined(fcx_engine *e, int phase, int32_t t, Plan *pl) {
   const int64_t want = std::max<int64_t>((n + e->chunks - 1) / e->chunks, e->min_chunk);
   const int64_t per = (want + kChunkAlign - 1) / kChunkAlign * kChunkAlign;
   const int K = (int)((n + per - 1) / per);
+  // the copy streams exist only for engines that take this path: every stream is a
+  // hardware-queue claim (GPU_MAX_HW_QUEUES), and device-resident engines never need them
+  if (!e->s_in) HIP_TRY(hipStreamCreateWithFlags(&e->s_in, hipStreamNonBlocking));
+  if (!e->s_out) HIP_TRY(hipStreamCreateWithFlags(&e->s_out, hipStreamNonBlocking));
   while ((int)e->ev_in.size() < K) {
     hipEvent_t a, b;
     HIP_TRY(hipEventCreateWithFlags(&a, hipEventDisableTiming));
