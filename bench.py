@@ -182,7 +182,10 @@ def main():
             outs = {name: torch.empty(max(la.n_atmos, 1), dtype=torch.float64, device=dev)
                     for name, _ in atm_fields}
             atm_outs.append(outs)
-            atmos = {"local": la, "fields": [(PHASE_NORMAL, 1, g, name, outs[name]) for name, g in atm_fields],
+            # OASIS sends the type-0 fields ('S A xxxx 00'): with several surface types those
+            # are the averages over the types, with one type the type-1 fluxes themselves
+            s0 = 0 if args.types >= 2 else 1
+            atmos = {"local": la, "fields": [(PHASE_NORMAL, s0, g, name, outs[name]) for name, g in atm_fields],
                      "shared": (shared[i * nb * stride:], stride) if nb else None}
         e = Engine(c.lf, c.num_surface_types, c.methods, corrections=c.corrections,
                    averages=c.averages, device=gpu, stream=stream.cuda_stream, atmos=atmos,

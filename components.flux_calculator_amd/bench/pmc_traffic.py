@@ -24,10 +24,10 @@ VARIANTS = {"1": "CCLM", "2": "MOM5", "3": "RCO", "0": "generic"}
 
 def kernel_key(name):
     """(variant, atmos fused, dtype) of a cells kernel, or None for any other kernel."""
-    m = re.search(r"cells_kernel<(\d), (true|false), (\d), (true|false), (double|float)>", name)
+    m = re.search(r"cells_kernel<(\d), (true|false), (\d), (true|false), (double|float)", name)
     if m:
         return VARIANTS[m.group(3)], 0, "f64" if m.group(5) == "double" else "f32"
-    m = re.search(r"cells_atmos_kernel<(\d), (true|false)>", name)
+    m = re.search(r"cells_atmos_kernel<(\d), (true|false)", name)
     if m:
         return VARIANTS[m.group(1)], 1, "f64"
     return None

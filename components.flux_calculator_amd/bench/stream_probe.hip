@@ -20,8 +20,8 @@
 typedef double d2 __attribute__((ext_vector_type(2)));
 
 struct Ptrs {
-  const double *in[16];
-  double *out[16];
+  const double *in[32];
+  double *out[32];
 };
 
 template <int R, int W, int C, bool NT>
@@ -101,14 +101,14 @@ int main() {
   // the same reason -- at 10M (160 MB) it would run from the Infinity Cache.
   const long n = 10'000'000, n_copy = 100'000'000;
   Ptrs p, pc;
-  for (int i = 0; i < 16; ++i) {
+  for (int i = 0; i < 32; ++i) {
     double *x;
     CHECK(hipMalloc(&x, n * sizeof(double)));
     CHECK(hipMemset(x, 0, n * sizeof(double)));
     p.in[i] = x;
     CHECK(hipMalloc(&p.out[i], n * sizeof(double)));
   }
-  for (int i = 0; i < 16; ++i) pc.in[i] = nullptr, pc.out[i] = nullptr;
+  for (int i = 0; i < 32; ++i) pc.in[i] = nullptr, pc.out[i] = nullptr;
   {
     double *x, *y;
     CHECK(hipMalloc(&x, n_copy * sizeof(double)));
@@ -133,6 +133,10 @@ int main() {
   run<10, 7, 2, true>("cclm-shape nt", p, n, 8192);
   run<11, 7, 2, true>("mom5-shape nt", p, n, 8192);
   run<5, 6, 2, true>("rco-shape nt", p, n, 8192);
+  // several surface types: T=2 CCLM (8 shared + 3 per type in, 7 per type + 7 averages out)
+  // and T=6 with the accumulation-free shape, to see what many concurrent streams reach
+  run<14, 21, 2, true>("T2 cclm-shape nt", p, n, 8192);
+  run<26, 32, 2, true>("T4ish 26/32 nt", p, n, 8192);
   run<1, 16, 2, false>("write-heavy 1/16", p, n, 2048);
   return 0;
 }

@@ -519,10 +519,21 @@ static void plan_fused_atmos(fcx_engine *e, Plan &pl, uint32_t stages, int phase
   const TypeParams &tp = pl.host.type[0];
   AtmosFused af{};
   int nf = 0;
+  const bool multi = e->T >= 2;
+  if (multi && !pl.host.ravg_on) return;  // several types: only register averages are fused
   for (auto &f : e->atm_fields) {
     if (!(f.phase & phase)) continue;
     const int b = e->buf(f.s, f.g, f.var);
     int k = -1;
+    if (multi) {  // the type-0 averages OASIS sends, held in registers by the kernel
+      for (int slot = 0; slot < kFusedFields; ++slot)
+        if (f.s == 0 && pl.host.ravg.out[slot] && b >= 0 && e->bufs[b].dev == pl.host.ravg.out[slot]) k = slot;
+      if (k < 0 || af.out[k]) return;
+      af.out[k] = f.out_dev;
+      af.x[k] = e->bufs[b].dev;
+      ++nf;
+      continue;
+    }
     if (f.s == 1 && f.var == FCX_MEVA && (stages & S_MEVA) && b == e->buf(1, 1, FCX_MEVA)) k = 0;
     if (f.s == 1 && f.var == FCX_HLAT && (stages & S_HLAT) && b == e->buf(1, 1, FCX_HLAT) &&
         (tp.m_hlat == FCX_WATER || tp.m_hlat == FCX_ICE || tp.m_hlat == FCX_ZERO))
@@ -550,6 +561,46 @@ static void plan_fused_atmos(fcx_engine *e, Plan &pl, uint32_t stages, int phase
   pl.af = af;
   pl.atm_nf = nf;
   pl.atm_fused = true;
+}
+
+// Register slot (AvgSlot) of the type-0 average of (g, var), or -1 when it has to be done
+// by re-reading X_s: every surface type must produce X_s in registers in this launch (a
+// computing method and a bound output -- not 'none'/'copy'), and one FARE array per type
+// (the t grid's) must serve it.
+static int ravg_slot(const fcx_engine *e, const Params &P, uint32_t stages, int g, int var) {
+  if (e->T < 2) return -1;
+  int slot = -1;
+  if (g == 1 && var == FCX_MEVA) slot = A_MEVA;
+  if (g == 1 && var == FCX_HLAT) slot = A_HLAT;
+  if (g == 1 && var == FCX_HSEN) slot = A_HSEN;
+  if (g == 1 && var == FCX_RBBR) slot = A_RBBR;
+  if (g == 1 && var == FCX_TSUR) slot = A_TSUR;
+  if (P.merged_uv && g == 2 && var == FCX_UMOM) slot = A_UMOM;
+  if (P.merged_uv && g == 3 && var == FCX_VMOM) slot = A_VMOM;
+  if (slot < 0 || P.ravg.out[slot]) return -1;
+  for (int s = 1; s <= e->T; ++s) {
+    const TypeParams &tp = P.type[s - 1];
+    const int fare = e->buf(s, 1, FCX_FARE);
+    if (fare < 0 || e->buf(s, g, FCX_FARE) != fare) return -1;
+    bool ok = false;
+    switch (slot) {
+      case A_MEVA: ok = (stages & S_MEVA) && is_compute(tp.m_meva) && tp.t.meva; break;
+      case A_HLAT:
+        ok = (stages & S_HLAT) && tp.t.hlat &&
+             (tp.m_hlat == FCX_WATER || tp.m_hlat == FCX_ICE || tp.m_hlat == FCX_ZERO);
+        break;
+      case A_HSEN: ok = (stages & S_HSEN) && is_compute(tp.m_hsen) && tp.t.hsen; break;
+      case A_RBBR: ok = (stages & S_RBBR) && tp.t.rbbr && (tp.m_rbbr == FCX_STBO || tp.m_rbbr == FCX_ZERO); break;
+      case A_UMOM: ok = (stages & S_UMOM) && is_compute(tp.m_mom) && tp.uv[0].mom; break;
+      case A_VMOM: ok = (stages & S_VMOM) && is_compute(tp.m_mom) && tp.uv[1].mom; break;
+      case A_TSUR: ok = e->buf(s, 1, FCX_TSUR) >= 0; break;
+    }
+    if (!ok) return -1;
+    // the value averaged is the array's value as stored by this launch: the array of X_s
+    const int b = e->buf(s, g, var);
+    if (b < 0) return -1;
+  }
+  return slot;
 }
 
 static int build_plan(fcx_engine *e, uint32_t stages, int avg_phases, Plan &pl) {
@@ -707,6 +758,23 @@ static int build_plan(fcx_engine *e, uint32_t stages, int avg_phases, Plan &pl) 
     for (int s = 2; s <= e->T; ++s)
       if (e->method[FCX_FLUX_MASS_EVAP][s - 1] == FCX_COPY) P.type[0].bias_adds++;
 
+  // standard variant of every surface type: the method sets compiled into cells_kernel<.., VAR>
+  // (HLAT and RBBR methods stay per type at run time)
+  pl.variant = 0;
+  if (P.merged_uv) {
+    for (int v = 1; v <= 3; ++v) {
+      const int m = v == 1 ? FCX_CCLM : v == 2 ? FCX_MOM5 : FCX_RCO;
+      const int q = v == 3 ? FCX_NONE : FCX_CCLM;
+      bool all = true;
+      for (int s = 0; s < e->T; ++s) {
+        const TypeParams &tp = P.type[s];
+        all = all && tp.m_meva == m && tp.m_hsen == m && tp.m_mom == m && tp.m_qsur[0] == q &&
+              tp.m_qsur[1] == q && tp.m_qsur[2] == q;
+      }
+      if (all) pl.variant = v;
+    }
+  }
+
   // type-0 averages
   if (stages & S_AVG) {
     std::vector<std::pair<int, int>> list;
@@ -720,6 +788,17 @@ static int build_plan(fcx_engine *e, uint32_t stages, int avg_phases, Plan &pl) 
     }
     for (auto &a : list) {
       const int g = a.first, var = a.second;
+      const int slot = ravg_slot(e, P, stages, g, var);
+      if (slot >= 0) {  // accumulated in registers as the types are produced
+        P.ravg.out[slot] = out(0, g, var);
+        for (int s = 1; s <= e->T; ++s) {
+          P.ravg.fare[s - 1] = in(s, 1, FCX_FARE);
+          if (slot == A_TSUR) P.type[s - 1].t.tsur = in(s, 1, FCX_TSUR);
+        }
+        P.ravg_on = 1;
+        n_max = std::max(n_max, e->n[0]);
+        continue;
+      }
       if (P.num_avg >= kMaxAvg) return fail(FCX_E_UNSUPPORTED, "more than %d averaged outputs", kMaxAvg);
       AvgEntry &ae = P.avg[P.num_avg++];
       ae.grid = g - 1;
@@ -744,19 +823,6 @@ static int build_plan(fcx_engine *e, uint32_t stages, int avg_phases, Plan &pl) 
   for (int b : pl.reads)
     if (!writes.count(b)) pure.push_back(b);
   pl.reads.swap(pure);
-  // T=1 hot path of a standard variant: every method of the type matches one of the
-  // compile-time method sets of cells_kernel<.., VAR>
-  pl.variant = 0;
-  if (e->T == 1 && P.merged_uv) {
-    const TypeParams &tp = P.type[0];
-    for (int v = 1; v <= 3; ++v) {
-      const int m = v == 1 ? FCX_CCLM : v == 2 ? FCX_MOM5 : FCX_RCO;
-      const int q = v == 3 ? FCX_NONE : FCX_CCLM;
-      if (tp.m_meva == m && tp.m_hsen == m && tp.m_mom == m && tp.m_qsur[0] == q &&
-          tp.m_qsur[1] == q && tp.m_qsur[2] == q)
-        pl.variant = v;
-    }
-  }
   plan_fused_atmos(e, pl, stages, avg_phases);
   HIP_TRY(hipMalloc(&pl.dev, sizeof(Params)));
   HIP_TRY(hipMemcpy(pl.dev, &P, sizeof(Params), hipMemcpyHostToDevice));
@@ -990,6 +1056,7 @@ static int launch_plan(fcx_engine *e, Plan *pl, const double *corr_m, int64_t lo
   lc.merged = pl->host.merged_uv != 0;
   lc.variant = (e->specialize && lc.merged) ? pl->variant : 0;
   lc.f32 = e->f32;
+  lc.ravg = pl->host.ravg_on != 0;
   const bool fused = pl->atm_fused && lc.variant && lc.cells_per_thread == 2;
   if (fused) {  // the shared-slot pointers may have been set after the plan was built
     pl->af.shared = e->atm_shared;

@@ -53,6 +53,17 @@ struct AvgEntry {
   const double *x[kMaxTypes];
   const double *fare[kMaxTypes];
 };
+// Type-0 averages accumulated in registers while the surface types are processed (the
+// kernel produces X_s, adds X_s * FARE_s to an accumulator, in type order from 0.0: the
+// sum of calc:377-383 without re-reading X_s or FARE_s).  One slot per value the cells
+// kernel holds in registers; slots 0..5 are also the fused accumulation fields.
+enum AvgSlot : int { A_MEVA = 0, A_HLAT = 1, A_HSEN = 2, A_RBBR = 3, A_UMOM = 4, A_VMOM = 5, A_TSUR = 6 };
+constexpr int kAvgSlots = 7;
+struct AvgRegs {
+  double *out[kAvgSlots];          // type-0 array of the slot, nullptr = not averaged in registers
+  const double *fare[kMaxTypes];   // FARE(s) of the t grid (shared by every register slot)
+};
+
 struct Params {
   int64_t n[3];          // cells per grid
   int64_t n_max;         // max of the grids in this launch
@@ -62,7 +73,10 @@ struct Params {
   int32_t merged_uv;     // u/v grids are the t grid (same buffers, same sizes)
   int32_t num_avg;
   TypeParams type[kMaxTypes];
-  AvgEntry avg[kMaxAvg];
+  AvgEntry avg[kMaxAvg];  // averages done by re-reading X_s (the rest)
+  AvgRegs ravg;
+  int32_t ravg_on;        // any ravg.out set (selects the RAVG kernel instantiation)
+  int32_t pad2;
 };
 
 // launchers (fcx_kernels.hip); return hipError_t as int
@@ -74,6 +88,7 @@ struct LaunchConfig {
   bool merged = false;       // u/v grids are the t grid
   int variant = 0;           // 0 generic, 1 CCLM, 2 MOM5, 3 RCO (T=1 specialisations)
   bool f32 = false;          // fp32 fields (FCX_PRECISION_F32): 4 cells per lane
+  bool ravg = false;         // register averages in this plan (Params::ravg_on)
   int64_t lo = 0, hi = -1;   // cell range of this launch (lo a multiple of kChunkAlign;
                              // hi < 0: to n_max) -- the pipelined host-bound step
 };

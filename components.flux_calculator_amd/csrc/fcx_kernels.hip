@@ -98,12 +98,26 @@ struct NoEmit {
   __device__ __forceinline__ void operator()(int, const Vec<C, R> &) const {}
 };
 
-template <int C, bool NT, class R, class Emit = NoEmit>
+template <int C, bool NT, class R, class Emit>
 __device__ __forceinline__ void momentum(int8_t m, bool north, const UVGridPtrs &g,
                                          const Vec<C, R> &ts, const Vec<C, R> &ps, const Vec<C, R> &u,
                                          const Vec<C, R> &v, const Vec<C, R> &vel, const Vec<C, R> &qs,
-                                         const Vec<C, R> &a, int64_t j0, int64_t n,
-                                         const Emit &emit = Emit(), int slot = -1) {
+                                         const Vec<C, R> &a, int64_t j0, int64_t n, Emit &emit, int slot);
+
+template <int C, bool NT, class R>
+__device__ __forceinline__ void momentum(int8_t m, bool north, const UVGridPtrs &g,
+                                         const Vec<C, R> &ts, const Vec<C, R> &ps, const Vec<C, R> &u,
+                                         const Vec<C, R> &v, const Vec<C, R> &vel, const Vec<C, R> &qs,
+                                         const Vec<C, R> &a, int64_t j0, int64_t n) {
+  NoEmit none;
+  momentum<C, NT, R>(m, north, g, ts, ps, u, v, vel, qs, a, j0, n, none, -1);
+}
+
+template <int C, bool NT, class R, class Emit>
+__device__ __forceinline__ void momentum(int8_t m, bool north, const UVGridPtrs &g,
+                                         const Vec<C, R> &ts, const Vec<C, R> &ps, const Vec<C, R> &u,
+                                         const Vec<C, R> &v, const Vec<C, R> &vel, const Vec<C, R> &qs,
+                                         const Vec<C, R> &a, int64_t j0, int64_t n, Emit &emit, int slot) {
   if (!g.mom) return;
   Vec<C, R> out;
   if (m == FCX_ZERO) {
@@ -157,20 +171,92 @@ __device__ __forceinline__ void uv_grid(const TypeParams &tp, int k, uint32_t st
   }
 }
 
-// VAR: 0 = generic (any T, methods read from the parameter block); 1/2/3 = the T=1 hot
-// path of the CCLM / MOM5 / RCO variant with QSUR/MEVA/HSEN/momentum methods fixed at
-// compile time, so the other method paths vanish from the code and its register budget.
-template <int C, bool MERGED, int VAR, bool NT, class R = double, class Emit = NoEmit>
+// LDS accumulators of the register-average slots: each lane owns C contiguous values per
+// slot (16 B), slot k at base + k * stride.  Private to the lane, so no synchronisation;
+// they keep 7 x C values out of the VGPR budget of the multi-type kernels.
+template <int C, class R>
+struct AccLds {
+  R *base;
+  int stride;  // elements between slots
+  __device__ __forceinline__ Vec<C, R> get(int k) const {
+    Vec<C, R> r;
+#pragma unroll
+    for (int i = 0; i < C; ++i) r.v[i] = base[k * stride + i];
+    return r;
+  }
+  __device__ __forceinline__ void set(int k, const Vec<C, R> &x) const {
+#pragma unroll
+    for (int i = 0; i < C; ++i) base[k * stride + i] = x.v[i];
+  }
+};
+
+// Where a produced flux goes besides its own array.  RAVG: X_s * FARE_s is added to the
+// type-0 accumulator of its slot (type order, from 0.0 -- calc:377-383) and the averages
+// go to the emitter (the fused atmosphere accumulation) once all types are done; without
+// RAVG the value of the single surface type goes to the emitter.
+template <int C, class R, bool RAVG, class Emit>
+struct Sink {
+  const Emit &emit;
+  const AvgRegs &ra;
+  AccLds<C, R> acc;
+  Vec<C, R> fare;
+  __device__ __forceinline__ Sink(const Emit &e, const AvgRegs &r, AccLds<C, R> a) : emit(e), ra(r), acc(a) {
+    if constexpr (RAVG) {
+#pragma unroll
+      for (int k = 0; k < kAvgSlots; ++k)
+        if (ra.out[k]) acc.set(k, splat<C, R>(R(0)));
+    }
+  }
+  __device__ __forceinline__ void operator()(int k, const Vec<C, R> &x) {
+    if constexpr (RAVG) {
+      if (ra.out[k]) {
+        Vec<C, R> a = acc.get(k);
+#pragma unroll
+        for (int i = 0; i < C; ++i) a.v[i] = a.v[i] + x.v[i] * fare.v[i];
+        acc.set(k, a);
+      }
+    } else {
+      if (k < kFusedFields) emit(k, x);
+    }
+  }
+};
+
+// VAR: 0 = generic (methods read from the parameter block); 1/2/3 = the CCLM / MOM5 / RCO
+// variant with the QSUR/MEVA/HSEN/momentum methods of every surface type fixed at compile
+// time, so the other method paths vanish from the code and its register budget.  Any T.
+// Inputs shared by consecutive surface types (the atmosphere fields are aliased into every
+// type, basic:334-358) are loaded once: a type reloads an input only when its pointer
+// differs from the previous type's (wave-uniform scalar compare).  Inputs are never written
+// by the pass, so a held value is the array's value.
+// TM: 1 = one surface type, fixed at compile time (the held inputs and the type loop
+// vanish); 0 = T from the parameter block.  RAVG (register averages) needs TM = 0.
+template <int C, bool MERGED, int VAR, bool NT, class R = double, int TM = 1, bool RAVG = false,
+          class Emit = NoEmit>
 __device__ __forceinline__ void process(const Params *__restrict__ P, const double *__restrict__ corr_m,
-                                        int64_t j0, const Emit &emit = Emit()) {
+                                        int64_t j0, const Emit &emit = Emit(),
+                                        AccLds<C, R> acc_lds = AccLds<C, R>{nullptr, 0}) {
+  static_assert(!(RAVG && TM), "register averages need more than one surface type");
   const uint32_t stages = P->stages;
-  const int T = VAR ? 1 : P->num_types;
+  const int T = TM ? 1 : P->num_types;
   const int64_t nt = P->n[0];
   const bool do_t = j0 < nt;
   Vec<C, R> corr = {};
   if (do_t && corr_m && (stages & S_MEVA)) corr = LD(corr_m, j0, nt);
   Vec<C, R> rsdd = {};
   if (do_t && P->rsdd0 && (stages & S_RSDR)) rsdd = LD(P->rsdd0, j0, nt);
+  Sink<C, R, RAVG, Emit> sink(emit, P->ravg, acc_lds);
+
+  // inputs held across surface types, with the pointer they were loaded from
+  Vec<C, R> ts = {}, fi = {}, ps = {}, pa = {}, qa = {}, ta = {}, u = {}, v = {}, amoi = {}, cmoi = {},
+            chea = {}, amom = {}, cmom = {}, vel = {};
+  const double *h_ts = nullptr, *h_fi = nullptr, *h_ps = nullptr, *h_pa = nullptr, *h_qa = nullptr,
+               *h_ta = nullptr, *h_u = nullptr, *h_v = nullptr, *h_amoi = nullptr, *h_cmoi = nullptr,
+               *h_chea = nullptr, *h_amom = nullptr, *h_cmom = nullptr;
+#define HOLD(var, ptr)                    \
+  if ((ptr) && (ptr) != h_##var) {        \
+    var = LD(ptr, j0, nt);                \
+    h_##var = (ptr);                      \
+  }
 
   for (int s = 0; s < T; ++s) {
     const TypeParams &tp = P->type[s];
@@ -183,30 +269,32 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
     const int8_t m_hs = VAR ? kVarMethod : tp.m_hsen;
     const int8_t m_mo = VAR ? kVarMethod : tp.m_mom;
     if (do_t) {
-      // ---- load every t-grid input this type needs (before any store of this type)
-      Vec<C, R> ts = {}, fi = {}, ps = {}, pa = {}, qa = {}, ta = {}, u = {}, v = {}, amoi = {},
-             cmoi = {}, chea = {}, qs = {}, me = {};
-      if (g.tsur) ts = LD(g.tsur, j0, nt);
-      if (g.fice) fi = LD(g.fice, j0, nt);
-      if (g.psur) ps = LD(g.psur, j0, nt);
-      if (g.patm) pa = LD(g.patm, j0, nt);
-      if (g.qatm) qa = LD(g.qatm, j0, nt);
-      if (g.tatm) ta = LD(g.tatm, j0, nt);
-      if (g.uatm) u = LD(g.uatm, j0, nt);
-      if (g.vatm) v = LD(g.vatm, j0, nt);
-      if (g.amoi) amoi = LD(g.amoi, j0, nt);
-      if (g.cmoi) cmoi = LD(g.cmoi, j0, nt);
-      if (g.chea) chea = LD(g.chea, j0, nt);
-      if (g.qsur_in) qs = LD(g.qsur_in, j0, nt);
+      // ---- every t-grid input this type needs (before any store of this type)
+      Vec<C, R> qs = {}, me = {};
+      HOLD(ts, g.tsur)
+      HOLD(fi, g.fice)
+      HOLD(ps, g.psur)
+      HOLD(pa, g.patm)
+      HOLD(qa, g.qatm)
+      HOLD(ta, g.tatm)
+      const bool wind_new = (g.uatm && g.uatm != h_u) || (g.vatm && g.vatm != h_v);
+      HOLD(u, g.uatm)
+      HOLD(v, g.vatm)
+      HOLD(amoi, g.amoi)
+      HOLD(cmoi, g.cmoi)
+      HOLD(chea, g.chea)
+      if (g.qsur_in) qs = LD(g.qsur_in, j0, nt);  // may be written by this pass: never held
       if (g.meva_in) me = LD(g.meva_in, j0, nt);
-      Vec<C, R> amom = {}, cmom = {};
       if constexpr (MERGED) {
         const UVGridPtrs &gu = tp.uv[0];
-        if (gu.amom) amom = LD(gu.amom, j0, nt);
-        if (gu.cmom) cmom = LD(gu.cmom, j0, nt);
+        HOLD(amom, gu.amom)
+        HOLD(cmom, gu.cmom)
       }
-      Vec<C, R> vel;
-      FOR_C vel.v[i] = wind(u.v[i], v.v[i]);
+      if (wind_new) FOR_C vel.v[i] = wind(u.v[i], v.v[i]);
+      if constexpr (RAVG) {
+        if (P->ravg_on) sink.fare = LD(P->ravg.fare[s], j0, nt);
+        sink(A_TSUR, ts);
+      }
 
       // ---- calc_flux_radiation_blackbody (calc:331-343)
       if ((stages & S_RBBR) && g.rbbr) {
@@ -214,10 +302,10 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
         if (tp.m_rbbr == FCX_STBO) {
           FOR_C r.v[i] = rbbr_stbo(ts.v[i]);
           ST(g.rbbr, j0, nt, r);
-          emit(3, r);
+          sink(A_RBBR, r);
         } else if (tp.m_rbbr == FCX_ZERO) {
           ST(g.rbbr, j0, nt, splat<C, R>(R(0)));
-          emit(3, splat<C, R>(R(0)));
+          sink(A_RBBR, splat<C, R>(R(0)));
         }
       }
       // ---- calc_spec_vapor_surface(t) (calc:37-49)
@@ -244,7 +332,7 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
             FOR_C me.v[i] = me.v[i] + corr.v[i];
           }
           if (g.meva) ST(g.meva, j0, nt, me);
-          emit(0, me);
+          sink(A_MEVA, me);
         }
       }
       // ---- calc_flux_heat_latent (calc:135-152)
@@ -260,7 +348,7 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
           h = splat<C, R>(R(0));
           ST(g.hlat, j0, nt, h);
         }
-        if (tp.m_hlat == FCX_WATER || tp.m_hlat == FCX_ICE || tp.m_hlat == FCX_ZERO) emit(1, h);
+        if (tp.m_hlat == FCX_WATER || tp.m_hlat == FCX_ICE || tp.m_hlat == FCX_ZERO) sink(A_HLAT, h);
       }
       // ---- calc_flux_heat_sensible (calc:167-206), P3: QATM in the q_s slot
       if ((stages & S_HSEN) && g.hsen) {
@@ -277,7 +365,7 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
           h = splat<C, R>(R(0));
           ST(g.hsen, j0, nt, h);
         }
-        if (m == FCX_CCLM || m == FCX_MOM5 || m == FCX_RCO || m == FCX_ZERO) emit(2, h);
+        if (m == FCX_CCLM || m == FCX_MOM5 || m == FCX_RCO || m == FCX_ZERO) sink(A_HSEN, h);
       }
       if constexpr (MERGED) {
         // u and v grids ARE the t grid: QSUR(u/v) = QSUR(t) (same inputs, same method),
@@ -296,8 +384,8 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
         const bool do_v = (stages & S_VMOM) && tp.uv[1].mom;
         if (do_u || do_v) {
           const Vec<C, R> &a = (m_mo == FCX_MOM5) ? cmom : amom;
-          if (do_u) momentum<C, NT, R, Emit>(m_mo, false, tp.uv[0], ts, ps, u, v, vel, qs, a, j0, nt, emit, 4);
-          if (do_v) momentum<C, NT, R, Emit>(m_mo, true, tp.uv[1], ts, ps, u, v, vel, qs, a, j0, nt, emit, 5);
+          if (do_u) momentum<C, NT, R>(m_mo, false, tp.uv[0], ts, ps, u, v, vel, qs, a, j0, nt, sink, A_UMOM);
+          if (do_v) momentum<C, NT, R>(m_mo, true, tp.uv[1], ts, ps, u, v, vel, qs, a, j0, nt, sink, A_VMOM);
         }
       }
       // ---- distribute_shortwave_radiation_flux (calc:355-362): RSDR_s = RSDD_0
@@ -308,8 +396,20 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
       if (j0 < P->n[2]) uv_grid<C, NT, R>(tp, 1, stages, j0, P->n[2]);
     }
   }
+#undef HOLD
 
   // ---- average_across_surface_types (calc:376-383), summed in type order
+  if constexpr (RAVG) {
+    if (do_t) {
+#pragma unroll
+      for (int k = 0; k < kAvgSlots; ++k) {
+        if (!P->ravg.out[k]) continue;
+        const Vec<C, R> avg = sink.acc.get(k);
+        ST(P->ravg.out[k], j0, nt, avg);
+        if (k < kFusedFields) emit(k, avg);  // the type-0 field OASIS sends on
+      }
+    }
+  }
   if (stages & S_AVG) {
     for (int e = 0; e < P->num_avg; ++e) {
       const AvgEntry &ae = P->avg[e];
@@ -327,14 +427,17 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
 }
 
 // cells [lo, hi) of the plan (lo a multiple of C), grid-stride over C-cell units
-template <int C, bool MERGED, int VAR, bool NT, class R>
-__global__ __launch_bounds__(256) void cells_kernel(const Params *__restrict__ P,
+template <int C, bool MERGED, int VAR, bool NT, class R, int TM, bool RAVG>
+__global__ __launch_bounds__(256, RAVG ? 3 : 1) void cells_kernel(const Params *__restrict__ P,
                                                     const double *__restrict__ corr_m, int64_t lo,
                                                     int64_t hi) {
   const int64_t u_end = (hi + C - 1) / C;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  // register-average accumulators: [slot][thread][C] (16 B per lane and slot, conflict-free)
+  __shared__ R s_acc[RAVG ? kAvgSlots * 256 * C : 1];
+  const AccLds<C, R> acc{s_acc + threadIdx.x * C, 256 * C};
   for (int64_t u = lo / C + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u < u_end; u += stride)
-    process<C, MERGED, VAR, NT, R>(P, corr_m, u * C);
+    process<C, MERGED, VAR, NT, R, TM, RAVG>(P, corr_m, u * C, NoEmit(), acc);
 }
 
 // The T=1 hot path with the exchange -> atmosphere accumulation fused in (AtmosFused).
@@ -373,11 +476,14 @@ __device__ __forceinline__ void wave_sync() {
 // lowest set bit index of m, 64 if none
 __device__ __forceinline__ int first_bit(uint64_t m) { return m ? __builtin_ctzll(m) : 64; }
 
-template <int VAR, bool NT>
-__global__ __launch_bounds__(256) void cells_atmos_kernel(const Params *__restrict__ P,
+template <int VAR, bool NT, int TM, bool RAVG>
+__global__ __launch_bounds__(256, RAVG ? 3 : 1) void cells_atmos_kernel(const Params *__restrict__ P,
                                                           const double *__restrict__ corr_m,
                                                           const AtmosFused af, int64_t lo, int64_t hi) {
-  __shared__ double s_p[4][kFusedFields * kRow];
+  // product rows [kFusedFields][kRow]; with RAVG they first serve as the accumulators of
+  // the type-0 averages (slot k = row k, TSUR in an extra row), then hold w * average
+  constexpr int kRows = RAVG ? kAvgSlots : kFusedFields;
+  __shared__ double s_p[4][kRows * kRow];
   const int64_t n = P->n_max;
   const int64_t n_tiles = (hi + kTile - 1) / kTile;  // tiles [lo/kTile, n_tiles) of this launch
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -405,7 +511,8 @@ __global__ __launch_bounds__(256) void cells_atmos_kernel(const Params *__restri
     const int32_t prev_tile = t0 > 0 ? af.idx[t0 - 1] : -2;  // wave-uniform loads
     const int64_t tend = t0 + kTile;
     const int32_t next_a = (tend < n) ? af.idx[tend] : -3;
-    if (j0 < n) process<2, true, VAR, NT, double>(P, corr_m, j0, emit);
+    if (j0 < n)
+      process<2, true, VAR, NT, double, TM, RAVG>(P, corr_m, j0, emit, AccLds<2, double>{wp + emit.s, kRow});
     // segment starts: cell 2l+i begins a segment when its atmosphere cell differs from the
     // previous cell's (the first cell past the grid end also "starts", which ends the last
     // real segment)
@@ -564,43 +671,72 @@ static int grid_for(int64_t units, int max_blocks = 256 * 8) {
   return (int)blocks;
 }
 
-template <int C, bool MERGED, int VAR, bool NT, class R>
+template <int C, bool MERGED, int VAR, bool NT, class R, int TM, bool RAVG>
 static void launch_one(int blocks, hipStream_t s, const Params *dp, const double *corr_m, int64_t lo,
                        int64_t hi) {
-  hipLaunchKernelGGL((cells_kernel<C, MERGED, VAR, NT, R>), dim3(blocks), dim3(256), 0, s, dp, corr_m, lo, hi);
+  hipLaunchKernelGGL((cells_kernel<C, MERGED, VAR, NT, R, TM, RAVG>), dim3(blocks), dim3(256), 0, s, dp,
+                     corr_m, lo, hi);
 }
 
-template <int C, bool MERGED, int VAR, class R>
+template <int C, bool MERGED, int VAR, class R, int TM, bool RAVG>
 static void launch_nt(bool nt, int blocks, hipStream_t s, const Params *dp, const double *corr_m,
                       int64_t lo, int64_t hi) {
   if (nt)
-    launch_one<C, MERGED, VAR, true, R>(blocks, s, dp, corr_m, lo, hi);
+    launch_one<C, MERGED, VAR, true, R, TM, RAVG>(blocks, s, dp, corr_m, lo, hi);
   else
-    launch_one<C, MERGED, VAR, false, R>(blocks, s, dp, corr_m, lo, hi);
+    launch_one<C, MERGED, VAR, false, R, TM, RAVG>(blocks, s, dp, corr_m, lo, hi);
 }
 
-template <int C, class R>
+template <int C, class R, int TM, bool RAVG>
 static void launch_c(const LaunchConfig &lc, int blocks, hipStream_t s, const Params *dp,
                      const double *corr_m, int64_t lo, int64_t hi) {
   if (!lc.merged) {
-    launch_nt<C, false, 0, R>(lc.nontemporal, blocks, s, dp, corr_m, lo, hi);
+    launch_nt<C, false, 0, R, TM, RAVG>(lc.nontemporal, blocks, s, dp, corr_m, lo, hi);
     return;
   }
   switch (lc.variant) {
-    case 1: launch_nt<C, true, 1, R>(lc.nontemporal, blocks, s, dp, corr_m, lo, hi); break;
-    case 2: launch_nt<C, true, 2, R>(lc.nontemporal, blocks, s, dp, corr_m, lo, hi); break;
-    case 3: launch_nt<C, true, 3, R>(lc.nontemporal, blocks, s, dp, corr_m, lo, hi); break;
-    default: launch_nt<C, true, 0, R>(lc.nontemporal, blocks, s, dp, corr_m, lo, hi); break;
+    case 1: launch_nt<C, true, 1, R, TM, RAVG>(lc.nontemporal, blocks, s, dp, corr_m, lo, hi); break;
+    case 2: launch_nt<C, true, 2, R, TM, RAVG>(lc.nontemporal, blocks, s, dp, corr_m, lo, hi); break;
+    case 3: launch_nt<C, true, 3, R, TM, RAVG>(lc.nontemporal, blocks, s, dp, corr_m, lo, hi); break;
+    default: launch_nt<C, true, 0, R, TM, RAVG>(lc.nontemporal, blocks, s, dp, corr_m, lo, hi); break;
   }
 }
 
-template <int VAR>
+// type mode: one surface type (compile-time), several, several with register averages
+template <int C, class R>
+static void launch_r(const Params *hp, const LaunchConfig &lc, int blocks, hipStream_t s, const Params *dp,
+                     const double *corr_m, int64_t lo, int64_t hi) {
+  if (hp->num_types == 1)
+    launch_c<C, R, 1, false>(lc, blocks, s, dp, corr_m, lo, hi);
+  else if (lc.ravg)
+    launch_c<C, R, 0, true>(lc, blocks, s, dp, corr_m, lo, hi);
+  else
+    launch_c<C, R, 0, false>(lc, blocks, s, dp, corr_m, lo, hi);
+}
+
+template <int VAR, int TM, bool RAVG>
 static void launch_atm(bool nt, int blocks, hipStream_t s, const Params *dp, const double *corr_m,
                        const AtmosFused &af, int64_t lo, int64_t hi) {
   if (nt)
-    hipLaunchKernelGGL((cells_atmos_kernel<VAR, true>), dim3(blocks), dim3(256), 0, s, dp, corr_m, af, lo, hi);
+    hipLaunchKernelGGL((cells_atmos_kernel<VAR, true, TM, RAVG>), dim3(blocks), dim3(256), 0, s, dp, corr_m,
+                       af, lo, hi);
   else
-    hipLaunchKernelGGL((cells_atmos_kernel<VAR, false>), dim3(blocks), dim3(256), 0, s, dp, corr_m, af, lo, hi);
+    hipLaunchKernelGGL((cells_atmos_kernel<VAR, false, TM, RAVG>), dim3(blocks), dim3(256), 0, s, dp, corr_m,
+                       af, lo, hi);
+}
+
+// fused accumulation: one surface type (its fluxes), or several with the type-0 averages in
+// registers (what OASIS sends); several types without register averages are not fused
+template <int VAR>
+static int launch_atm_r(const Params *hp, const LaunchConfig &lc, int blocks, hipStream_t s, const Params *dp,
+                        const double *corr_m, const AtmosFused &af, int64_t lo, int64_t hi) {
+  if (hp->num_types == 1)
+    launch_atm<VAR, 1, false>(lc.nontemporal, blocks, s, dp, corr_m, af, lo, hi);
+  else if (lc.ravg)
+    launch_atm<VAR, 0, true>(lc.nontemporal, blocks, s, dp, corr_m, af, lo, hi);
+  else
+    return (int)hipErrorInvalidValue;
+  return 0;
 }
 
 int launch_cells(const Params *hp, const Params *dp, const double *corr_m, const LaunchConfig &lc,
@@ -612,12 +748,14 @@ int launch_cells(const Params *hp, const Params *dp, const double *corr_m, const
   if (atm) {  // fused accumulation: T=1 specialised merged kernel, 2 cells per lane
     const int64_t tiles = (hi - lo + kTile - 1) / kTile;
     const int blocks = (int)std::max<int64_t>(1, lc.max_blocks > 0 ? std::min<int64_t>(tiles, lc.max_blocks) : tiles);
+    int r = 0;
     switch (lc.variant) {
-      case 1: launch_atm<1>(lc.nontemporal, blocks, s, dp, corr_m, *atm, lo, hi); break;
-      case 2: launch_atm<2>(lc.nontemporal, blocks, s, dp, corr_m, *atm, lo, hi); break;
-      case 3: launch_atm<3>(lc.nontemporal, blocks, s, dp, corr_m, *atm, lo, hi); break;
+      case 1: r = launch_atm_r<1>(hp, lc, blocks, s, dp, corr_m, *atm, lo, hi); break;
+      case 2: r = launch_atm_r<2>(hp, lc, blocks, s, dp, corr_m, *atm, lo, hi); break;
+      case 3: r = launch_atm_r<3>(hp, lc, blocks, s, dp, corr_m, *atm, lo, hi); break;
       default: return (int)hipErrorInvalidValue;
     }
+    if (r) return r;
     return (int)hipGetLastError();
   }
   // vector width: 16 B per lane and array (2 fp64 or 4 fp32 cells), or 1 cell when the
@@ -627,13 +765,13 @@ int launch_cells(const Params *hp, const Params *dp, const double *corr_m, const
   const int blocks = grid_for(units, lc.max_blocks);
   if (lc.f32) {
     if (c == 4)
-      launch_c<4, float>(lc, blocks, s, dp, corr_m, lo, hi);
+      launch_r<4, float>(hp, lc, blocks, s, dp, corr_m, lo, hi);
     else
-      launch_c<1, float>(lc, blocks, s, dp, corr_m, lo, hi);
+      launch_r<1, float>(hp, lc, blocks, s, dp, corr_m, lo, hi);
   } else if (c == 2) {
-    launch_c<2, double>(lc, blocks, s, dp, corr_m, lo, hi);
+    launch_r<2, double>(hp, lc, blocks, s, dp, corr_m, lo, hi);
   } else {
-    launch_c<1, double>(lc, blocks, s, dp, corr_m, lo, hi);
+    launch_r<1, double>(hp, lc, blocks, s, dp, corr_m, lo, hi);
   }
   return (int)hipGetLastError();
 }

@@ -8,6 +8,10 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.normpath(os.path.join(_HERE, "..", "..", "lib", "libfcx.so"))
+# development A/B of two builds of the same library (e.g. launch-bound experiments); the
+# override must still be a libfcx build -- there is no other implementation to fall back to
+if os.environ.get("FCX_LIBRARY"):
+    LIB_PATH = os.path.abspath(os.environ["FCX_LIBRARY"])
 
 FCX_OK = 0
 FCX_MEM_HOST = 0x0
