@@ -134,7 +134,10 @@ struct fcx_engine {
   bool pin_host = true;
   int chunks = 8;                                   // fcx_step pipeline depth (1 = off)
   int64_t min_chunk = 256 * 1024;                   // cells per chunk at least (~2 MB/array)
-  int zero_copy = 2;  // kernels use the host arrays in place: 0 off, 1 on, 2 auto (small grids)
+  // kernels use the host arrays in place: 0 off (default), 1 on, 2 auto (small grids).  Off
+  // by default: it is the one mode in which kernels touch host memory directly; an
+  // unexplained, timing-dependent illegal-access report followed a test using it
+  int zero_copy = 0;
   bool zc_active = false;
   bool timing = true;  // ev0/ev1 around every run (fcx_last_kernel_ms)
   std::vector<std::pair<char *, size_t>> pinned;    // hipHostRegister'ed page ranges

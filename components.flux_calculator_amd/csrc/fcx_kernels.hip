@@ -296,6 +296,7 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
         sink(A_TSUR, ts);
       }
 
+
       // ---- calc_flux_radiation_blackbody (calc:331-343)
       if ((stages & S_RBBR) && g.rbbr) {
         Vec<C, R> r;

@@ -52,8 +52,8 @@ def test_fused_t1(variant, bias, n):
 @pytest.mark.parametrize("variant", ["CCLM", "MOM5", "RCO"])
 @pytest.mark.parametrize("zero_copy", [0, 1])
 def test_fused_t1_host_modes(variant, zero_copy):
-    """Host-bound fields through device mirrors (copies) and through zero-copy mapping (the
-    default for grids this small, FCX_OPT_ZERO_COPY=2): same oracle parity either way."""
+    """Host-bound fields through device mirrors (copies, the default) and through zero-copy
+    mapping (FCX_OPT_ZERO_COPY=1): same oracle parity either way."""
     case = build_case(variant, n=10_007, T=1, bias=True)
     ref = oracle_lib.run_case(case, "c", current_step_time=STEP_T)
     eng = engine_for(case, options={"zero_copy": zero_copy})

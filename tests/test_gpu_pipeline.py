@@ -85,8 +85,8 @@ def test_pinned_small_arrays_sharing_pages():
 
 
 def test_default_min_chunk_keeps_small_grids_sequential():
-    """Below 2 x 256K cells the default engine maps the host arrays (zero-copy auto) instead of
-    pipelining copies; same bits as the mirrored sequential step."""
+    """Below 2 x 256K cells the default step is the sequential mirrored one (same bits as an
+    explicitly sequential engine)."""
     case = build_case("RCO", n=70_000, T=1)
     for k in case.outputs:
         case.lf.field[k][:] = np.nan
