@@ -178,3 +178,33 @@ def test_two_processes_share_one_gpu_gloo():
         for name, vals in outs.items():
             got[name][a0: a0 + len(vals)] = vals
     assert_parity(got, ref, label="2 processes")
+
+
+@pytest.mark.parametrize("fused", [True, False])
+@pytest.mark.parametrize("variant,T", [("CCLM", 2), ("MOM5", 3), ("RCO", 2)])
+def test_atmos_accumulation_of_type0_averages(variant, T, fused):
+    """Several surface types: OASIS sends the type-0 averages (S A xxxx 00).  The averages
+    are accumulated in LDS as the types are produced (register slots) and, fused, handed to
+    the accumulation without being re-read; both paths give the sequential SCRIP sum of the
+    GPU's own averages bit for bit, and the averages match the oracle."""
+    import torch
+    from fcx.engine import Engine
+
+    n = 40_003
+    case = build_case(variant, n=n, T=T, bias=True, seed=913)
+    ref = oracle_lib.run_case(case, "c", current_step_time=7200)
+    amap = synthetic_atmos_map(n)
+    la = local_atmos(amap, 0, 1)
+    outs = {name: torch.full((la.n_atmos,), float("nan"), dtype=torch.float64, device="cuda:0")
+            for name, _ in FIELDS}
+    atmos = {"local": la, "fields": [(2, 0, g, name, outs[name]) for name, g in FIELDS]}
+    eng = Engine(case.lf, T, case.methods, corrections=case.corrections, averages=case.averages, atmos=atmos,
+                 options=None if fused else {"specialize": 0})
+    eng.step(PHASE_ALL, 7200)
+    for name, g in FIELDS:
+        avg = np.asarray(case.lf.field[(0, g, name)])
+        want = oracle_lib.atmos_accumulate(amap.atmos_index, amap.weight, avg, amap.n_atmos)
+        np.testing.assert_array_equal(outs[name].cpu().numpy(), want, err_msg=name)
+    assert_parity({k: np.asarray(case.lf.field[k]) for k in case.outputs},
+                  {k: ref[k] for k in case.outputs}, label=f"{variant} T{T}")
+    eng.close()

@@ -170,3 +170,33 @@ def test_zero_copy_per_call_dropin():
     got = {k: np.array(case.lf.field[k], copy=True) for k in case.outputs}
     eng.close()
     assert_parity(got, ref, label="zero-copy per call")
+
+
+def test_pipeline_multi_type_register_averages_and_fused_accumulation():
+    """T=3: type-0 averages in the LDS slots, their accumulation fused, chunked host step."""
+    n = 60_001
+    case = build_case("CCLM", n=n, T=3, bias=True)
+    amap = synthetic_atmos_map(n)
+    outs = {name: np.full(amap.n_atmos, np.nan) for name in ("MEVA", "HSEN", "UMOM")}
+    atmos = {"local": local_atmos(amap, 0, 1),
+             "fields": [(2, 0, 1, "MEVA", outs["MEVA"]), (2, 0, 1, "HSEN", outs["HSEN"]),
+                        (2, 0, 2, "UMOM", outs["UMOM"])]}
+    res = []
+    for chunks in (1, 6):
+        for k in case.outputs:
+            case.lf.field[k][:] = np.nan
+        for v in outs.values():
+            v[:] = np.nan
+        eng = Engine(case.lf, 3, case.methods, corrections=case.corrections, averages=case.averages,
+                     atmos=atmos, options={"pipeline_min_chunk": 1024, "pipeline_chunks": chunks})
+        eng.step(PHASE_ALL, STEP_T)
+        eng.close()
+        res.append({**{k: np.array(case.lf.field[k], copy=True) for k in case.outputs},
+                    **{("atm", k): v.copy() for k, v in outs.items()}})
+    same_bits(res[0], res[1])
+    ref = oracle_lib.run_case(case, "c", current_step_time=STEP_T)
+    assert_parity({k: res[0][k] for k in case.outputs}, ref, label="T3 chunked")
+    for name in outs:
+        g = 2 if name == "UMOM" else 1
+        want = oracle_lib.atmos_accumulate(amap.atmos_index, amap.weight, res[0][(0, g, name)], amap.n_atmos)
+        np.testing.assert_array_equal(res[0][("atm", name)], want, err_msg=name)
