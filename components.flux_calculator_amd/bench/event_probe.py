@@ -96,6 +96,28 @@ def main():
                 ts.append(ev0.elapsed_time(ev1))
             pairs[f"{names[y]} after {names[x]}"] = round(float(np.median(ts)), 4)
 
+    # dirty-cache hypothesis: a 512 MB read (torch sum) between X and Y -- if X leaves dirty
+    # Infinity-Cache lines, the flush absorbs the write-back and Y runs at its clean speed
+    flush_buf = torch.ones(64 << 20, dtype=torch.float64, device=dev)  # 512 MB
+    ev2 = torch.cuda.Event(enable_timing=True)
+    flushed = {}
+    for x in range(len(engines)):
+        y = 0
+        tf, ty = [], []
+        for r in range(15):
+            engines[x][2].run(PHASE_ALL, 0)
+            ev0.record(stream)
+            flush_buf.sum()
+            ev2.record(stream)
+            engines[y][2].run(PHASE_ALL, 0)
+            ev1.record(stream)
+            ev1.synchronize()
+            tf.append(ev0.elapsed_time(ev2))
+            ty.append(ev2.elapsed_time(ev1))
+        flushed[f"{names[y]} after {names[x]} + 512 MB read"] = {"flush_ms": round(float(np.median(tf)), 4),
+                                                                 "kernel_ms": round(float(np.median(ty)), 4)}
+    del flush_buf
+
     modes = ["none", "torch_events", "fcx_timing", "both"]
     res = {m: [] for m in modes}
     for r in range(a.rounds):
@@ -104,8 +126,8 @@ def main():
         for m in order:
             res[m].append(run(m))
     out = {m: round(float(np.median(v)), 4) for m, v in res.items() if v}
-    print(json.dumps({"ms_per_step_median": out, "kernel_ms_after": pairs, "cells": n, "steps": a.steps,
-                      "rounds": a.rounds}))
+    print(json.dumps({"ms_per_step_median": out, "kernel_ms_after": pairs, "flushed": flushed, "cells": n,
+                      "steps": a.steps, "rounds": a.rounds}))
 
 
 if __name__ == "__main__":
