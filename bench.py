@@ -40,7 +40,10 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--cells", type=int, default=10_000_000, help="exchange-grid cells per GPU")
+    p.add_argument("--cells", type=int, default=10_000_000, help="exchange-grid cells per GPU (weak scaling)")
+    p.add_argument("--global-cells", type=int, default=0,
+                   help="fixed global grid sharded over the ranks by APPLE ranges (strong scaling, "
+                        "config 4: 40000000); overrides --cells")
     p.add_argument("--variants", default=",".join(VARIANTS))
     p.add_argument("--types", type=int, default=1, help="surface types")
     p.add_argument("--bias", action="store_true", help="monthly evaporation bias corrections")
@@ -87,6 +90,19 @@ def cpu_baseline(args, variants):
         "sample": f"{reps} coupling steps x {len(variants)} variants ({'+'.join(variants)}) over "
                   f"{n} cells, T={args.types}, reference call order, {el:.1f} s on 1 thread",
     }
+
+
+def host_cpu():
+    """lscpu-style model name and the CPUs this process may use (SURVEY.md 8d CPU timing)."""
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"model": model, "nproc": len(os.sched_getaffinity(0)), "machine_cpus": os.cpu_count()}
 
 
 def cpu_all_cores(args, variants):
@@ -153,10 +169,14 @@ def main():
 
     # this rank's APPLE range of the global grid (decomp_def.F90:23-31): weak scaling,
     # every rank owns args.cells cells; the seed follows the global offset
-    n = args.cells
-    n_global = n * world
-    offset, size = apple_range(n_global, rank, world)
-    assert size == n
+    if args.global_cells:  # config 4: one fixed grid, decomp_def.F90 ranges
+        n_global = args.global_cells
+        offset, n = apple_range(n_global, rank, world)
+    else:  # weak scaling: every rank owns args.cells cells of a grid of world * cells
+        n = args.cells
+        n_global = n * world
+        offset, size = apple_range(n_global, rank, world)
+        assert size == n
     host = inputs_for_bench(n, seed=BASE_SEED + offset)
     data = {k: torch.as_tensor(v).to(dev) for k, v in host.items()}
     if f32:  # inputs rounded once; every variant's case shares them
@@ -240,7 +260,7 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         t_max = float(tt.item())
     ms_per_step = t_max / args.steps * 1e3
-    cells_per_step = n * len(variants) * world
+    cells_per_step = n_global * len(variants)
     value = cells_per_step * args.steps / t_max / 1e6
 
     mean_ms = kern_ms.mean(axis=0)
@@ -271,7 +291,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.global_cells else "weak",
         "vs_baseline": None,
         "dtype": args.precision,
         "data": "synthetic (SURVEY.md 8d distributions, seeded PCG64)",
@@ -281,6 +301,7 @@ def main():
                          + (" + exchange->atmosphere accumulation" if la is not None else "")
                          + (", fp32 variant (config 5)" if f32 else "") + ", inputs HBM-resident"),
             "cells_per_gpu": n,
+            "cells_global": n_global,
             "cells_per_step": cells_per_step,
             "variants": list(variants),
             "surface_types": args.types,
@@ -310,6 +331,7 @@ def main():
         cb = cpu_baseline(args, variants)
         out["cpu_baseline"] = cb
         out["cpu_baseline_all_cores"] = cpu_all_cores(args, variants)
+        out["host_cpu"] = host_cpu()
     if rank == 0:
         print(json.dumps(out), flush=True)
     for e in engines:
