@@ -267,3 +267,26 @@ def test_fp64_tolerance_report_config5(variant):
     os.makedirs(out, exist_ok=True)
     with open(os.path.join(out, f"fp64_error_{variant}.json"), "w") as f:
         json.dump(rep, f, indent=1)
+
+
+@pytest.mark.parametrize("quirk", [False, True])
+def test_bias_window_of_rank_range(quirk):
+    """Corrections of rank 1 of 2 cut from a global field by fcx.bias.window (intended, or the
+    reference's one-cell-early read, P5), passed month-major [12][n]: same as the oracle fed
+    with the same window."""
+    from fcx.bias import window
+    from fcx.parallel import apple_range
+
+    n_global = 10_000
+    off, n = apple_range(n_global, 1, 2)
+    g = np.random.default_rng(5).normal(0.0, 1e-5, (12, n_global))
+    w = window(g, off, n, reference_offset_quirk=quirk)
+    np.testing.assert_array_equal(w, g[:, off - 1: off - 1 + n] if quirk else g[:, off: off + n])
+    case = build_case("CCLM", n=n, T=1, bias=True)
+    case.corrections = (case.corrections[0], np.ascontiguousarray(w.T))  # oracle: cell-major
+    ref = oracle_lib.run_case(case, "c", current_step_time=STEP_T)
+    eng = Engine(case.lf, 1, case.methods, corrections=(case.corrections[0], w))  # month-major
+    eng.step(PHASE_ALL, STEP_T)
+    got = outputs(case)
+    eng.close()
+    assert_parity(got, ref, label=f"bias window quirk={quirk}")
