@@ -290,3 +290,40 @@ def test_bias_window_of_rank_range(quirk):
     got = outputs(case)
     eng.close()
     assert_parity(got, ref, label=f"bias window quirk={quirk}")
+
+
+def test_regridding_matrices_read_from_files(tmp_path):
+    """The staged regrid path with links read back by fcx.io.read_regridding_matrix from
+    NetCDF-3 files (io:109-198), t->u and t->v, against the oracle on the same links."""
+    from scipy.io import netcdf_file
+
+    from fcx.io import read_regridding_matrix
+
+    rng = np.random.default_rng(11)
+    case = build_case("MOM5", n=700, T=2, bias=True, sep_grids=(640, 610))
+    nt, nu, nv = case.grid_size
+    mats = {}
+    for which, (ns, nd, fname) in {2: (nt, nu, "t_to_u"), 3: (nt, nv, "t_to_v")}.items():
+        nnz = 4 * nd
+        src = rng.integers(1, ns + 1, nnz)
+        dst = np.repeat(np.arange(1, nd + 1), 4)[rng.permutation(nnz)]
+        w = rng.uniform(0.0, 1.0, nnz)
+        path = str(tmp_path / f"regrid_{fname}.nc")
+        with netcdf_file(path, "w") as f:
+            f.createDimension("num_links", nnz)
+            f.createDimension("num_wgts", 1)
+            for name, vals, typ in (("src_address", src, "i"), ("dst_address", dst, "i")):
+                v = f.createVariable(name, typ, ("num_links",))
+                v[:] = vals.astype(np.int32)
+            m = f.createVariable("remap_matrix", "d", ("num_links", "num_wgts"))
+            m[:] = w[:, None]
+        mats[which] = read_regridding_matrix(path, ns, 0, nd, 0)
+    case.regrid = {"matrices": mats}
+    for s in (1, 2):
+        case.methods["which_spec_vapor_surface_u"][s - 1] = "none"
+        case.lf.put_to[(s, 1, "QSUR")] = 2
+        case.lf.put_to[(s, 1, "HSEN")] = 4
+        case.lf.allocate_localvar("HSEN", s, 3, value=np.nan)
+        case.outputs.append((s, 3, "HSEN"))
+    ref = oracle_lib.run_case(case, "c", current_step_time=STEP_T, regrid=True)
+    assert_parity(fused(case, phases=(PHASE_EARLY, PHASE_NORMAL)), ref, label="regrid from files")
