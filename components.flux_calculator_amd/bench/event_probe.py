@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--order", default="CCLM,MOM5,RCO", help="engine creation order")
     ap.add_argument("--atmos", type=int, default=1)
     ap.add_argument("--spacer-mb", type=int, default=0, help="allocation between inputs and engines")
+    ap.add_argument("--pool", action="store_true",
+                    help="repack every case's device arrays into one allocation before the engines")
     ap.add_argument("--engines-reversed", action="store_true",
                     help="allocate all cases first, then create the engines in reverse order")
     a = ap.parse_args()
@@ -49,6 +51,23 @@ def main():
         outs = [torch.empty(la.n_atmos, dtype=torch.float64, device=dev) for _ in ATM]
         atmos = {"local": la, "fields": [(PHASE_NORMAL, 1, g, name, o) for (name, g), o in zip(ATM, outs)]}
         cases.append((c, outs, atmos if a.atmos else None))
+    if a.pool:  # one allocation for all fields of all cases (aliases kept)
+        uniq = {}
+        for c, _, _ in cases:
+            for t in c.lf.field.values():
+                uniq.setdefault(t.data_ptr(), t)
+        total = sum(t.numel() for t in uniq.values())
+        pool = torch.empty(total + 32 * len(uniq), dtype=torch.float64, device=dev)
+        view, off = {}, 0
+        for ptr, t in uniq.items():
+            v = pool[off: off + t.numel()]
+            v.copy_(t)
+            view[ptr] = v
+            off += (t.numel() + 31) // 32 * 32  # 256-B aligned sub-buffers
+        for c, _, _ in cases:
+            for k, t in list(c.lf.field.items()):
+                c.lf.field[k] = view[t.data_ptr()]
+        del uniq
     made = {}
     order = range(len(cases) - 1, -1, -1) if a.engines_reversed else range(len(cases))
     for i in order:
