@@ -14,9 +14,12 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <mutex>
 #include <set>
 #include <string>
 #include <vector>
+
+#include <unistd.h>
 
 #include "fcx_internal.h"
 
@@ -77,6 +80,8 @@ int var0(int var) { return var - 1; }
 
 }  // namespace
 
+static void unpin_host_arrays(fcx_engine *e);
+
 struct fcx_engine {
   int device = 0;
   int T = 0;
@@ -130,6 +135,23 @@ struct fcx_engine {
   void *atm_pool = nullptr;
   bool atmos_in_run = true;
   bool atm_done_fused = false;  // the last fcx_run already accumulated the atmosphere fields
+  // exchange -> model remaps (SCRIP links, CSR by destination in link order)
+  struct RemapField {
+    int phase, s, g, var;
+    double *out_host = nullptr, *out_dev = nullptr;
+    bool external = false;
+  };
+  struct Remap {
+    int64_t n_dst = 0, n_links = 0;
+    int32_t max_src = -1;
+    std::vector<int32_t> row, col;
+    std::vector<double> w;
+    int32_t *d_row = nullptr, *d_col = nullptr;
+    double *d_w = nullptr;
+    std::vector<RemapField> fields;
+    void *pool = nullptr;
+  };
+  std::vector<Remap> remaps;
   // host-bound steps: page-locked caller arrays and the H2D / compute / D2H pipeline
   bool pin_host = true;
   int chunks = 8;                                   // fcx_step pipeline depth (1 = off)
@@ -241,6 +263,12 @@ extern "C" int fcx_destroy(fcx_engine *e) {
   (void)hipFree(e->d_atm_col);
   (void)hipFree(e->d_atm_w);
   (void)hipFree(e->atm_pool);
+  for (auto &r : e->remaps) {
+    (void)hipFree(r.d_row);
+    (void)hipFree(r.d_col);
+    (void)hipFree(r.d_w);
+    (void)hipFree(r.pool);
+  }
   (void)hipFree(e->pool);
   if (e->ev0) (void)hipEventDestroy(e->ev0);
   if (e->ev1) (void)hipEventDestroy(e->ev1);
@@ -248,7 +276,7 @@ extern "C" int fcx_destroy(fcx_engine *e) {
   for (hipEvent_t ev : e->ev_comp) (void)hipEventDestroy(ev);
   if (e->s_in) (void)hipStreamDestroy(e->s_in);
   if (e->s_out) (void)hipStreamDestroy(e->s_out);
-  for (auto &r : e->pinned) (void)hipHostUnregister(r.first);
+  unpin_host_arrays(e);
   if (e->own_stream && e->stream) (void)hipStreamDestroy(e->stream);
   delete e;
   return FCX_OK;
@@ -844,12 +872,76 @@ static int get_plan(fcx_engine *e, uint32_t stages, int avg_phases, Plan **pl) {
   return FCX_OK;
 }
 
-// Page-lock the caller's host arrays once (hipHostRegister of their exact byte ranges,
-// merged where arrays overlap): the per-step H2D/D2H then run as DMA at the link rate and
-// overlap with compute.  The ranges are not rounded out to pages: a registered range that
-// swallowed the head of some other allocation would make the runtime treat that memory as
-// part of ours and reject copies running past our end.  A range the runtime refuses stays
-// pageable (its copies are still correct, only staged).
+// Process-wide page-lock registry.  The runtime locks whole pages, so two registrations
+// that touch one page -- two arrays of one engine, or arrays of two live engines, sharing a
+// page -- would tear down each other's lock when either is unregistered (the runtime aborts
+// in hipHostUnregister / hipFree).  Every registration made here therefore owns its pages
+// exclusively: ranges of one engine that share a page are merged, the same exact range
+// asked for again (another engine over the same arrays) is shared by reference count, and
+// a range whose pages meet a different live registration stays pageable.
+namespace {
+
+struct PinEntry {
+  uintptr_t a, b;  // registered bytes [a, b)
+  unsigned flags;
+  int refs;
+};
+std::mutex g_pin_mu;
+std::map<uintptr_t, PinEntry> g_pins;  // keyed by first page number; page spans disjoint
+
+uintptr_t page_shift() {
+  static const uintptr_t s = [] {
+    long ps = sysconf(_SC_PAGESIZE);
+    uintptr_t k = 12;
+    while (ps > 0 && ((uintptr_t)1 << k) < (uintptr_t)ps) ++k;
+    return k;
+  }();
+  return s;
+}
+
+// true: [a, b) is page-locked for the caller (new or shared registration)
+bool pin_range(uintptr_t a, uintptr_t b, unsigned flags) {
+  const uintptr_t sh = page_shift(), pa = a >> sh, pb = (b - 1) >> sh;
+  std::lock_guard<std::mutex> lk(g_pin_mu);
+  auto it = g_pins.upper_bound(pb);
+  if (it != g_pins.begin()) {
+    --it;  // the registration with the largest first page <= pb
+    PinEntry &x = it->second;
+    if (((x.b - 1) >> sh) >= pa) {
+      if (x.a == a && x.b == b && x.flags == flags) {
+        ++x.refs;
+        return true;
+      }
+      return false;  // pages shared with another registration: stay pageable
+    }
+  }
+  if (hipHostRegister(reinterpret_cast<void *>(a), b - a, flags) != hipSuccess) {
+    (void)hipGetLastError();  // e.g. registered by the caller already: leave it
+    return false;
+  }
+  g_pins.emplace(pa, PinEntry{a, b, flags, 1});
+  return true;
+}
+
+void unpin_range(uintptr_t a) {
+  std::lock_guard<std::mutex> lk(g_pin_mu);
+  auto it = g_pins.find(a >> page_shift());
+  if (it == g_pins.end() || it->second.a != a) return;
+  if (--it->second.refs == 0) {
+    (void)hipHostUnregister(reinterpret_cast<void *>(a));
+    g_pins.erase(it);
+  }
+}
+
+}  // namespace
+
+// Page-lock the caller's host arrays once: the per-step H2D/D2H then run as DMA at the link
+// rate and overlap with compute.  The registered ranges are the arrays' own bytes (merged
+// where two arrays share a page, which only spans bytes inside pages already touched); they
+// are not rounded out to pages: a registered range that swallowed the head of some other
+// allocation would make the runtime treat that memory as part of ours and reject copies
+// running past our end.  A range that cannot be registered exclusively stays pageable (its
+// copies are still correct, only staged).
 static void pin_host_arrays(fcx_engine *e) {
   std::vector<std::pair<uintptr_t, uintptr_t>> r;
   auto add = [&](const void *p, size_t bytes) {
@@ -861,22 +953,27 @@ static void pin_host_arrays(fcx_engine *e) {
     if (!bf.external) add(bf.host, (size_t)bf.n * e->esize);
   for (auto &f : e->atm_fields)
     if (!f.external) add(f.out_host, (size_t)std::max<int64_t>(e->n_atmos, 0) * sizeof(double));
+  for (auto &rm : e->remaps)
+    for (auto &f : rm.fields)
+      if (!f.external) add(f.out_host, (size_t)rm.n_dst * sizeof(double));
   std::sort(r.begin(), r.end());
+  const uintptr_t sh = page_shift();
   std::vector<std::pair<uintptr_t, uintptr_t>> m;
   for (auto &x : r) {
-    if (!m.empty() && x.first < m.back().second)
-      m.back().second = std::max(m.back().second, x.second);
+    if (!m.empty() && (x.first >> sh) <= ((m.back().second - 1) >> sh))
+      m.back().second = std::max(m.back().second, x.second);  // overlap or shared page
     else
       m.push_back(x);
   }
   const unsigned flags = e->zc_active ? hipHostRegisterMapped : hipHostRegisterDefault;
-  for (auto &x : m) {
-    char *p = reinterpret_cast<char *>(x.first);
-    if (hipHostRegister(p, x.second - x.first, flags) == hipSuccess)
-      e->pinned.push_back({p, x.second - x.first});
-    else
-      (void)hipGetLastError();  // e.g. already registered by the caller: leave it
-  }
+  for (auto &x : m)
+    if (pin_range(x.first, x.second, flags))
+      e->pinned.push_back({reinterpret_cast<char *>(x.first), x.second - x.first});
+}
+
+static void unpin_host_arrays(fcx_engine *e) {
+  for (auto &r : e->pinned) unpin_range(reinterpret_cast<uintptr_t>(r.first));
+  e->pinned.clear();
 }
 
 // Zero-copy (FCX_OPT_ZERO_COPY): a host array inside a page-locked range is used by the
@@ -915,6 +1012,14 @@ static void map_host_arrays(fcx_engine *e) {
       f.external = true;
     }
   }
+  for (auto &rm : e->remaps)
+    for (auto &f : rm.fields) {
+      if (f.external || !f.out_host) continue;
+      if (void *d = mapped(f.out_host)) {
+        f.out_dev = reinterpret_cast<double *>(d);
+        f.external = true;
+      }
+    }
 }
 
 extern "C" int fcx_set_precision(fcx_engine *e, int precision) {
@@ -1013,6 +1118,32 @@ extern "C" int fcx_commit(fcx_engine *e) {
         }
     }
   }
+  for (auto &rm : e->remaps) {
+    for (auto &f : rm.fields)
+      if (rm.max_src >= e->n[f.g - 1])
+        return fail(FCX_E_ARG, "remap link source %d outside the %lld cells of grid %d", rm.max_src,
+                    (long long)e->n[f.g - 1], f.g);
+    HIP_TRY(hipMalloc(&rm.d_row, rm.row.size() * sizeof(int32_t)));
+    HIP_TRY(hipMemcpy(rm.d_row, rm.row.data(), rm.row.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    HIP_TRY(hipMalloc(&rm.d_col, std::max<size_t>(rm.col.size(), 1) * sizeof(int32_t)));
+    HIP_TRY(hipMalloc(&rm.d_w, std::max<size_t>(rm.w.size(), 1) * sizeof(double)));
+    if (!rm.col.empty()) {
+      HIP_TRY(hipMemcpy(rm.d_col, rm.col.data(), rm.col.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+      HIP_TRY(hipMemcpy(rm.d_w, rm.w.data(), rm.w.size() * sizeof(double), hipMemcpyHostToDevice));
+    }
+    const size_t one = ((size_t)std::max<int64_t>(rm.n_dst, 1) * sizeof(double) + 255) / 256 * 256;
+    size_t need = 0;
+    for (auto &f : rm.fields) need += f.external ? 0 : one;
+    if (need) {
+      HIP_TRY(hipMalloc(&rm.pool, need));
+      size_t off = 0;
+      for (auto &f : rm.fields)
+        if (!f.external) {
+          f.out_dev = reinterpret_cast<double *>((char *)rm.pool + off);
+          off += one;
+        }
+    }
+  }
   e->committed = true;
   return FCX_OK;
 }
@@ -1078,6 +1209,8 @@ static int launch_plan(fcx_engine *e, Plan *pl, const double *corr_m, int64_t lo
 }
 
 static int regrid_var(fcx_engine *e, int var, int surface_type);
+static int run_remaps(fcx_engine *e, int phase);
+static int download_remaps(fcx_engine *e, int phase, hipStream_t s);
 
 // the reference step order with do_regridding after each calc (flux_calculator.F90:972-991)
 static int staged_sequence(int phase, std::vector<std::pair<uint32_t, int>> &seq) {
@@ -1119,6 +1252,7 @@ extern "C" int fcx_download(fcx_engine *e, int phase) {
     if ((f.phase & phase) && !f.external && e->n_atmos > 0)
       HIP_TRY(hipMemcpyAsync(f.out_host, f.out_dev, e->n_atmos * sizeof(double), hipMemcpyDeviceToHost,
                              e->stream));
+  if (int r = download_remaps(e, phase, e->stream)) return r;
   if (e->any_regrid) {  // device-side regrid destinations of the fields this phase computes
     std::vector<int> extra;
     std::vector<int> vars;
@@ -1167,6 +1301,45 @@ static int run_atmos(fcx_engine *e, int phase) {
   return FCX_OK;
 }
 
+// out[d] = sum over the links of d (link order, from 0.0) of w * field[src]: the SCRIP
+// weight application OASIS performs on 'S' fields sent to a model; atmos_kernel with the
+// target's CSR (columns = exchange cells), up to kMaxAtmosFields fields per launch
+static int run_remaps(fcx_engine *e, int phase) {
+  for (auto &rm : e->remaps) {
+    AtmosArgs a{};
+    a.row_ptr = rm.d_row;
+    a.col = rm.d_col;
+    a.w = rm.d_w;
+    a.n_atmos = rm.n_dst;
+    a.left = a.right = -1;
+    auto flush = [&]() -> int {
+      if (!a.nf) return FCX_OK;
+      const int r = launch_atmos(a, e->stream);
+      if (r) return fail(FCX_E_HIP, "remap launch: %s", hipGetErrorString((hipError_t)r));
+      a.nf = 0;
+      return FCX_OK;
+    };
+    for (auto &f : rm.fields) {
+      if (!(f.phase & phase)) continue;
+      a.x[a.nf] = e->dptr(f.s, f.g, f.var);
+      a.out[a.nf] = f.out_dev;
+      if (!a.x[a.nf]) return fail(FCX_E_MISSING, "remap field %s(%d) is not bound", kVarNames[var0(f.var)], f.s);
+      if (++a.nf == kMaxAtmosFields)
+        if (int r = flush()) return r;
+    }
+    if (int r = flush()) return r;
+  }
+  return FCX_OK;
+}
+
+static int download_remaps(fcx_engine *e, int phase, hipStream_t s) {
+  for (auto &rm : e->remaps)
+    for (auto &f : rm.fields)
+      if ((f.phase & phase) && !f.external && rm.n_dst > 0)
+        HIP_TRY(hipMemcpyAsync(f.out_host, f.out_dev, rm.n_dst * sizeof(double), hipMemcpyDeviceToHost, s));
+  return FCX_OK;
+}
+
 extern "C" int fcx_run(fcx_engine *e, int phase, int32_t t) {
   if (int r = check(e)) return r;
   if (phase < 1 || phase > 3) return fail(FCX_E_ARG, "phase %d unknown", phase);
@@ -1195,6 +1368,7 @@ extern "C" int fcx_run(fcx_engine *e, int phase, int32_t t) {
   }
   if (e->atmos_in_run && !e->atm_done_fused)
     if (int r = run_atmos(e, phase)) return r;
+  if (int r = run_remaps(e, phase)) return r;
   if (e->timing) HIP_TRY(hipEventRecord(e->ev1, e->stream));
   e->timed = e->timing;
   return FCX_OK;
@@ -1257,6 +1431,7 @@ static int step_pipelined(fcx_engine *e, int phase, int32_t t, Plan *pl) {
   }
   if (e->atmos_in_run && !e->atm_done_fused)
     if (int r = run_atmos(e, phase)) return r;
+  if (int r = run_remaps(e, phase)) return r;
   HIP_TRY(hipEventRecord(e->ev_comp[K - 1], e->stream));
   HIP_TRY(hipStreamWaitEvent(e->s_out, e->ev_comp[K - 1], 0));
   if (e->atmos_in_run || e->atm_done_fused)
@@ -1264,6 +1439,7 @@ static int step_pipelined(fcx_engine *e, int phase, int32_t t, Plan *pl) {
       if ((f.phase & phase) && !f.external && e->n_atmos > 0)
         HIP_TRY(hipMemcpyAsync(f.out_host, f.out_dev, e->n_atmos * sizeof(double), hipMemcpyDeviceToHost,
                                e->s_out));
+  if (int r = download_remaps(e, phase, e->s_out)) return r;
   if (e->timing) HIP_TRY(hipEventRecord(e->ev1, e->s_out));
   e->timed = e->timing;
   HIP_TRY(hipStreamSynchronize(e->s_out));
@@ -1605,4 +1781,58 @@ extern "C" int fcx_run_atmos(fcx_engine *e, int phase) {
   if (phase < 1 || phase > 3) return fail(FCX_E_ARG, "phase %d unknown", phase);
   if (e->atm_done_fused) return FCX_OK;  // done inside the last fcx_run
   return run_atmos(e, phase);
+}
+
+// ------------------------------------------------------------------ exchange -> model remaps
+
+extern "C" int fcx_add_remap(fcx_engine *e, int64_t n_dst, int64_t n_links, const int32_t *src,
+                             const int32_t *dst, const double *w, int32_t *remap_id) {
+  if (!e || !remap_id) return fail(FCX_E_ARG, "NULL argument");
+  if (e->committed) return fail(FCX_E_STATE, "engine already committed");
+  if (n_dst < 0 || n_links < 0 || (n_links > 0 && (!src || !dst || !w))) return fail(FCX_E_ARG, "bad remap");
+  fcx_engine::Remap rm;
+  rm.n_dst = n_dst;
+  rm.n_links = n_links;
+  rm.row.assign((size_t)n_dst + 1, 0);
+  for (int64_t k = 0; k < n_links; ++k) {
+    if (dst[k] < 0 || dst[k] >= n_dst || src[k] < 0)
+      return fail(FCX_E_ARG, "remap link %lld (%d -> %d) outside the grids", (long long)k, src[k], dst[k]);
+    rm.row[(size_t)dst[k] + 1]++;
+    rm.max_src = std::max(rm.max_src, src[k]);
+  }
+  for (int64_t d = 0; d < n_dst; ++d) rm.row[(size_t)d + 1] += rm.row[(size_t)d];
+  rm.col.assign((size_t)n_links, 0);
+  rm.w.assign((size_t)n_links, 0.0);
+  std::vector<int32_t> fill(rm.row.begin(), rm.row.end() - 1);
+  for (int64_t k = 0; k < n_links; ++k) {  // stable: each destination keeps its link order
+    const int32_t at = fill[(size_t)dst[k]]++;
+    rm.col[(size_t)at] = src[k];
+    rm.w[(size_t)at] = w[k];
+  }
+  *remap_id = (int32_t)e->remaps.size();
+  e->remaps.push_back(std::move(rm));
+  return FCX_OK;
+}
+
+extern "C" int fcx_add_remap_field(fcx_engine *e, int32_t remap_id, int phase, int s, int g, int var, double *out,
+                                   int flags) {
+  if (!e) return fail(FCX_E_ARG, "NULL engine");
+  if (e->committed) return fail(FCX_E_STATE, "engine already committed");
+  if (e->f32) return fail(FCX_E_UNSUPPORTED, "fp32 engine: remaps run in fp64 only");
+  if (remap_id < 0 || remap_id >= (int32_t)e->remaps.size()) return fail(FCX_E_ARG, "remap %d unknown", remap_id);
+  if (phase < 1 || phase > 3 || s < 0 || s > kMaxTypes || g < 1 || g > 3 || var < 1 || var > kNumVars || !out)
+    return fail(FCX_E_ARG, "bad remap field arguments");
+  fcx_engine::RemapField f;
+  f.phase = phase;
+  f.s = s;
+  f.g = g;
+  f.var = var;
+  if (flags & FCX_MEM_DEVICE) {
+    f.out_dev = out;
+    f.external = true;
+  } else {
+    f.out_host = out;
+  }
+  e->remaps[(size_t)remap_id].fields.push_back(f);
+  return FCX_OK;
 }

@@ -64,6 +64,8 @@ SIGNATURES = [
     ("fcx_last_kernel_ms", _I, [_P, _c.POINTER(_c.c_float)]),
     ("fcx_pinned_bytes", _I, [_P, _P]),
     ("fcx_algorithmic_bytes", _I, [_P, _I, _c.POINTER(_I64)]),
+    ("fcx_add_remap", _I, [_P, _I64, _I64, _P, _P, _P, _P]),
+    ("fcx_add_remap_field", _I, [_P, _I32, _I, _I, _I, _I, _P, _I]),
     ("fcx_set_option", _I, [_P, _I, _I64]),
     ("fcx_set_atmos_map", _I, [_P, _I64, _P, _P]),
     ("fcx_add_atmos_field", _I, [_P, _I, _I, _I, _I, _P, _I]),

@@ -18,11 +18,13 @@ class Engine:
     """
 
     def __init__(self, lf: LocalFields, num_surface_types, methods, corrections=None,
-                 averages=(), regrid=None, device=0, stream=None, atmos=None, options=None):
+                 averages=(), regrid=None, device=0, stream=None, atmos=None, options=None, remaps=None):
         """atmos: exchange -> atmosphere accumulation, dict with
              local   : fcx.parallel.LocalAtmos of this rank
              fields  : [(phase, surface_type, grid, name, out_array[n_atmos])]
              shared  : optional (device_buffer[n_boundaries * stride], stride)
+        remaps: exchange -> model remaps, each {"n_dst", "src", "dst", "w" (0-based links),
+                 "fields": [(phase, surface_type, grid, name, out_array[n_dst])]}
         options: {name: value} for fcx_set_option."""
         self.lib = _lib.load()
         self.lf = lf
@@ -89,6 +91,20 @@ class Engine:
                     self._keep.append(buf)
                     _lib.check(self.lib.fcx_set_atmos_shared(h, ctypes.c_void_p(data_ptr(buf)), la.n_boundaries,
                                                              stride, la.left, la.right))
+            for rm in remaps or ():
+                src = np.ascontiguousarray(rm["src"], dtype=np.int32)
+                dst = np.ascontiguousarray(rm["dst"], dtype=np.int32)
+                w = np.ascontiguousarray(rm["w"], dtype=np.float64)
+                self._keep += [src, dst, w]
+                rid = ctypes.c_int32()
+                _lib.check(self.lib.fcx_add_remap(h, int(rm["n_dst"]), src.shape[0], ctypes.c_void_p(src.ctypes.data),
+                                                  ctypes.c_void_p(dst.ctypes.data), ctypes.c_void_p(w.ctypes.data),
+                                                  ctypes.byref(rid)))
+                for phase, s, g, name, out in rm["fields"]:
+                    flags = _lib.FCX_MEM_DEVICE if is_device(out) else _lib.FCX_MEM_HOST
+                    self._keep.append(out)
+                    _lib.check(self.lib.fcx_add_remap_field(h, rid.value, phase, s, g, IDX[name],
+                                                            ctypes.c_void_p(data_ptr(out)), flags))
             for name, value in (options or {}).items():
                 _lib.check(self.lib.fcx_set_option(h, self.OPTIONS[name], int(value)))
             _lib.check(self.lib.fcx_commit(h))

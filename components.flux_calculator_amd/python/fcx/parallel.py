@@ -167,3 +167,48 @@ class PeriodicAtmosMap:
         idx = self.index(x)
         return AtmosMap(np.ascontiguousarray(idx, dtype=np.int32), self.weight(x, n_global),
                         int(idx[-1]) + 1 if n_global else 0)
+
+
+@dataclass
+class ModelMap:
+    """Exchange -> model (e.g. ocean) remap links, SCRIP style: 0-based src (exchange cell),
+    dst (model cell) and weight, in file order."""
+    src: np.ndarray
+    dst: np.ndarray
+    weight: np.ndarray
+    n_model: int
+
+
+def synthetic_model_map(n_exchange, n_model, links_per_cell=1, seed=20231016):
+    """Every exchange cell lies in one model cell (conservative weights area_x / area_model).
+    The exchange grid follows the atmosphere rows, so a model cell is met in several short
+    runs scattered along it: runs of 1..8 exchange cells, each in a random model cell.
+    links_per_cell=2 adds a second, distance-weighted link per exchange cell (the two weights
+    summing to the conservative one), as a non-conservative remap has; links in a shuffled
+    file order."""
+    rng = np.random.Generator(np.random.PCG64([seed, 7]))
+    lengths = rng.integers(1, 9, n_exchange // 4 + 2)
+    lengths = lengths[: int(np.searchsorted(np.cumsum(lengths), n_exchange)) + 1]
+    owner = np.repeat(rng.integers(0, n_model, lengths.size), lengths)[:n_exchange]
+    area = rng.uniform(0.5, 1.5, n_exchange)
+    tot = np.bincount(owner, weights=area, minlength=n_model)
+    w = area / tot[owner]
+    src = np.arange(n_exchange, dtype=np.int64)
+    if links_per_cell == 1:
+        return ModelMap(src.astype(np.int32), owner.astype(np.int32), w, n_model)
+    other = (owner + rng.integers(1, n_model, n_exchange)) % n_model
+    f = rng.uniform(0.6, 0.9, n_exchange)
+    s2 = np.stack([src, src], 1).reshape(-1)
+    d2 = np.stack([owner, other], 1).reshape(-1)
+    w2 = np.stack([w * f, w * (1 - f)], 1).reshape(-1)
+    perm = rng.permutation(s2.size)
+    return ModelMap(s2[perm].astype(np.int32), d2[perm].astype(np.int32), w2[perm], n_model)
+
+
+def local_links(mmap: ModelMap, offset, size):
+    """The links whose exchange cell is in this rank's range, src made local (0-based); dst
+    stays global: every rank writes partial sums of the whole model grid and one all-reduce
+    of the outputs completes them."""
+    keep = (mmap.src >= offset) & (mmap.src < offset + size)
+    return (np.ascontiguousarray(mmap.src[keep] - offset, dtype=np.int32),
+            np.ascontiguousarray(mmap.dst[keep], dtype=np.int32), np.ascontiguousarray(mmap.weight[keep]))

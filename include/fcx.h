@@ -176,6 +176,19 @@ int fcx_atmos_finish(fcx_engine *e);
 /* the accumulation of `phase` on its own (fcx_run runs it unless FCX_OPT_ATMOS_IN_RUN=0) */
 int fcx_run_atmos(fcx_engine *e, int phase);
 
+/* ---- exchange-grid -> model remaps ----
+ * The SCRIP weight application OASIS3-MCT performs on the 'S' fields sent to a model
+ * (remap files mappings/remap_<grid>_exchangegrid_to_<model>.nc): out[d] = sum over the
+ * links k with dst[k] == d, in link order from 0.0, of w[k] * field[src[k]].  src: 0-based
+ * cell of the field's grid on this rank; dst: 0-based cell of the target grid (n_dst cells,
+ * e.g. the whole ocean grid).  With several ranks, every rank writes its partial sums of
+ * all n_dst cells (0 where it has no link); an all-reduce (sum) of the output arrays over
+ * the ranks completes them.  Run by fcx_run / fcx_step after the fluxes. */
+int fcx_add_remap(fcx_engine *e, int64_t n_dst, int64_t n_links, const int32_t *src_cell,
+                  const int32_t *dst_cell, const double *weight, int32_t *remap_id);
+int fcx_add_remap_field(fcx_engine *e, int32_t remap_id, int phase, int surface_type, int grid,
+                        int var, double *out, int flags);
+
 /* launch tuning of the fused cells kernel (defaults are the measured best on MI355X) */
 enum fcx_option {
   FCX_OPT_CELLS_PER_THREAD = 1, /* 1 or 2 cells per lane (2: 16-B loads; default 2)       */

@@ -337,6 +337,12 @@ int fco_step_threads(fco_state *st, int nthreads) {
 #endif
 }
 
+void fco_remap_apply(int64_t n_links, const int32_t *src, const int32_t *dst, const double *w,
+                     const double *x, int64_t n_dst, double *out) {
+  for (int64_t d = 0; d < n_dst; ++d) out[d] = 0.0;
+  for (int64_t k = 0; k < n_links; ++k) out[dst[k]] = out[dst[k]] + w[k] * x[src[k]];
+}
+
 void fco_atmos_accumulate(int64_t n_cells, const int32_t *atmos_index, const double *weight,
                           const double *x_field, int64_t n_atmos, double *out) {
   for (int64_t a = 0; a < n_atmos; ++a) out[a] = 0.0;

@@ -89,6 +89,11 @@ int  fco_current_month(int32_t init_date, int64_t seconds);
  * weight application out[a] = sum_x w[x] * x_field[x] over the exchange cells x of atmosphere
  * cell a.  Not in the reference repository (OASIS is a sibling component): restated from the
  * published SCRIP remap, PARITY UNPINNED.  Cells are summed in increasing x, from 0.0. */
+/* OASIS-style SCRIP weight application of a remapping file to a target (model) grid:
+ * out[d] = 0 for all d, then out[dst[k]] += w[k] * x[src[k]] for k in link order
+ * (0-based indices).  OASIS3-MCT itself is not in the reference: parity unpinned. */
+void fco_remap_apply(int64_t n_links, const int32_t *src, const int32_t *dst, const double *w,
+                     const double *x, int64_t n_dst, double *out);
 void fco_atmos_accumulate(int64_t n_cells, const int32_t *atmos_index, const double *weight,
                           const double *x_field, int64_t n_atmos, double *out);
 /* one full coupling step in reference order (flux_calculator.F90:902-991), no regridding */

@@ -64,6 +64,8 @@ def load(kind="c"):
             lib.fco_current_month.restype = ctypes.c_int
             lib.fco_step_threads.argtypes = [ctypes.POINTER(FcoState), ctypes.c_int]
             lib.fco_step.argtypes = [ctypes.POINTER(FcoState)]
+            lib.fco_remap_apply.argtypes = [ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                            ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
             lib.fco_atmos_accumulate.argtypes = [ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
                                                  ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
         _libs[kind] = (lib, p)
@@ -185,4 +187,17 @@ def atmos_accumulate(atmos_index, weight, x_field, n_atmos):
     out = np.empty(int(n_atmos))
     lib.fco_atmos_accumulate(idx.shape[0], idx.ctypes.data, w.ctypes.data, x.ctypes.data,
                              int(n_atmos), out.ctypes.data)
+    return out
+
+
+def remap_apply(src, dst, w, x_field, n_dst):
+    """fco_remap_apply: sequential SCRIP weight application in link order (parity unpinned)."""
+    lib, _ = load("c")
+    src = np.ascontiguousarray(src, dtype=np.int32)
+    dst = np.ascontiguousarray(dst, dtype=np.int32)
+    w = np.ascontiguousarray(w, dtype=np.float64)
+    x = np.ascontiguousarray(x_field, dtype=np.float64)
+    out = np.empty(int(n_dst))
+    lib.fco_remap_apply(src.shape[0], src.ctypes.data, dst.ctypes.data, w.ctypes.data, x.ctypes.data,
+                        int(n_dst), out.ctypes.data)
     return out

@@ -84,6 +84,43 @@ def test_pinned_small_arrays_sharing_pages():
     same_bits(a, b)
 
 
+def test_page_lock_registry_shared_and_conflicting_engines():
+    """Page-locked ranges are process-wide and page-exclusive: a second live engine over the
+    same arrays shares the registration (reference count), one whose small arrays sit on the
+    same heap pages stays pageable, and closing engines in either order leaves the others
+    correct and unregisters the pages exactly once."""
+    a = build_case("CCLM", n=2_001, T=2, bias=True)
+    b = build_case("CCLM", n=2_001, T=2, bias=True)  # allocated right after: shares pages
+    ref_a = run(a, {"pin_host": 0})
+    ref_b = run(b, {"pin_host": 0})
+
+    def engine(case):
+        return Engine(case.lf, 2, case.methods, corrections=case.corrections,
+                      averages=case.averages, options={"pin_host": 1})
+
+    def step(eng, case):
+        for k in case.outputs:
+            case.lf.field[k][:] = np.nan
+        eng.step(PHASE_ALL, STEP_T)
+        return {k: np.array(case.lf.field[k], copy=True) for k in case.outputs}
+
+    for close_first in (0, 1, 2):
+        e = [engine(a), engine(a), engine(b)]
+        assert e[0].pinned_bytes() > 0
+        assert e[1].pinned_bytes() == e[0].pinned_bytes()  # the same ranges, shared
+        e[close_first].close()
+        for i, (eng, case, ref) in enumerate(((e[0], a, ref_a), (e[1], a, ref_a), (e[2], b, ref_b))):
+            if i != close_first:
+                same_bits(step(eng, case), ref)
+        for i in range(3):
+            if i != close_first:
+                e[i].close()
+    e = engine(a)  # everything unregistered: pinning works again from scratch
+    assert e.pinned_bytes() > 0
+    same_bits(step(e, a), ref_a)
+    e.close()
+
+
 def test_default_min_chunk_keeps_small_grids_sequential():
     """Below 2 x 256K cells the default step is the sequential mirrored one (same bits as an
     explicitly sequential engine)."""

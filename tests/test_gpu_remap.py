@@ -1,0 +1,98 @@
+"""Exchange -> model remaps on the GPU (fcx_add_remap): the SCRIP weight
+application OASIS performs on the fields sent to a bottom model, CSR by destination in link
+order, checked bit for bit against the sequential application (oracle/fco.c:fco_remap_apply)
+on the GPU's own fluxes; the fluxes themselves against the oracle (tests/parity.py)."""
+import numpy as np
+import pytest
+
+import oracle_lib
+from parity import assert_parity, mixed_error
+
+pytestmark = pytest.mark.gpu
+
+from fcx.basic import PHASE_ALL  # noqa: E402
+from fcx.engine import Engine  # noqa: E402
+from fcx.parallel import apple_range, local_links, synthetic_model_map  # noqa: E402
+from fcx.synthetic import build_case  # noqa: E402
+
+STEP_T = 3600 * 24 * 40
+FIELDS = (("MEVA", 1), ("HSEN", 1), ("UMOM", 2), ("VMOM", 3))
+
+
+def remap_spec(mmap, outs, s=1, src=None, dst=None, w=None):
+    return {"n_dst": mmap.n_model, "src": mmap.src if src is None else src, "dst": mmap.dst if dst is None else dst,
+            "w": mmap.weight if w is None else w,
+            "fields": [(2, s, g, name, outs[name]) for name, g in FIELDS]}
+
+
+@pytest.mark.parametrize("links", [1, 2])
+@pytest.mark.parametrize("device_out", [False, True])
+def test_remap_bit_exact(links, device_out):
+    torch = pytest.importorskip("torch")
+    n = 30_011
+    case = build_case("CCLM", n=n, T=1, bias=True)
+    mmap = synthetic_model_map(n, 2_000, links_per_cell=links)
+    if device_out:
+        outs = {k: torch.full((mmap.n_model,), float("nan"), dtype=torch.float64, device="cuda:0") for k, _ in FIELDS}
+    else:
+        outs = {k: np.full(mmap.n_model, np.nan) for k, _ in FIELDS}
+    eng = Engine(case.lf, 1, case.methods, corrections=case.corrections, remaps=[remap_spec(mmap, outs)])
+    eng.step(PHASE_ALL, STEP_T)
+    eng.close()
+    for name, g in FIELDS:
+        want = oracle_lib.remap_apply(mmap.src, mmap.dst, mmap.weight, np.asarray(case.lf.field[(1, g, name)]),
+                                      mmap.n_model)
+        got = outs[name].cpu().numpy() if device_out else outs[name]
+        np.testing.assert_array_equal(got, want, err_msg=name)
+    ref = oracle_lib.run_case(case, "c", current_step_time=STEP_T)
+    assert_parity({k: np.asarray(case.lf.field[k]) for k in case.outputs}, ref, label="remap fluxes")
+
+
+def test_remap_of_type0_averages_in_a_pipelined_step():
+    """T=3: the model receives the type-0 averages; chunked host step; two remap targets."""
+    n = 40_003
+    case = build_case("MOM5", n=n, T=3, bias=True)
+    m1 = synthetic_model_map(n, 1_500, links_per_cell=2, seed=1)
+    m2 = synthetic_model_map(n, 900, links_per_cell=1, seed=2)
+    o1 = {k: np.full(m1.n_model, np.nan) for k, _ in FIELDS}
+    o2 = {k: np.full(m2.n_model, np.nan) for k, _ in FIELDS}
+    eng = Engine(case.lf, 3, case.methods, corrections=case.corrections, averages=case.averages,
+                 remaps=[remap_spec(m1, o1, s=0), remap_spec(m2, o2, s=0)],
+                 options={"pipeline_min_chunk": 1024, "pipeline_chunks": 5})
+    eng.step(PHASE_ALL, STEP_T)
+    eng.close()
+    for mm, oo in ((m1, o1), (m2, o2)):
+        for name, g in FIELDS:
+            want = oracle_lib.remap_apply(mm.src, mm.dst, mm.weight, np.asarray(case.lf.field[(0, g, name)]),
+                                          mm.n_model)
+            np.testing.assert_array_equal(oo[name], want, err_msg=name)
+
+
+def test_sharded_remap_partial_sums_complete_by_summation():
+    """Three engines on APPLE shards write partial sums of the whole model grid; their sum
+    (the all-reduce) equals the single-engine remap up to association."""
+    n, world = 24_007, 3
+    full = build_case("RCO", n=n, T=1, bias=False, seed=17)
+    mmap = synthetic_model_map(n, 1_000, links_per_cell=2)
+    total = {k: np.zeros(mmap.n_model) for k, _ in FIELDS}
+    for r in range(world):
+        off, size = apple_range(n, r, world)
+        case = build_case("RCO", n=size, T=1, bias=False, seed=17)
+        remap_arrays = {}
+        for key, a in full.lf.field.items():
+            if id(a) not in remap_arrays:
+                remap_arrays[id(a)] = np.ascontiguousarray(np.asarray(a)[off: off + size])
+            case.lf.field[key] = remap_arrays[id(a)]
+        src, dst, w = local_links(mmap, off, size)
+        outs = {k: np.full(mmap.n_model, np.nan) for k, _ in FIELDS}
+        eng = Engine(case.lf, 1, case.methods, remaps=[remap_spec(mmap, outs, src=src, dst=dst, w=w)])
+        eng.step(PHASE_ALL, 0)
+        eng.close()
+        for k in total:
+            total[k] += outs[k]
+        for key in case.outputs:  # the shard's fluxes back into the global arrays
+            np.asarray(full.lf.field[key])[off: off + size] = case.lf.field[key]
+    for name, g in FIELDS:
+        want = oracle_lib.remap_apply(mmap.src, mmap.dst, mmap.weight, np.asarray(full.lf.field[(1, g, name)]),
+                                      mmap.n_model)
+        assert mixed_error(total[name], want) <= 1e-12, name

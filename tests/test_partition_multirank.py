@@ -140,3 +140,49 @@ def test_sharded_step_with_one_allreduce_matches_single_process(world):
         # cells owned by one rank are bit-identical; shared cells differ by association only
         assert mixed_error(got[name], ref[name]) <= 1e-12, name
     assert_parity({k: got[k] for k in ATMOS_FIELDS}, ref, label=f"world={world}")
+
+
+def _remap_rank(rank, world, port, n, q):
+    import torch
+    import torch.distributed as dist
+
+    from fcx.parallel import local_links, synthetic_model_map
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        mmap = synthetic_model_map(n, 300, links_per_cell=2)
+        x = np.random.default_rng(3).normal(size=n)
+        off, size = apple_range(n, rank, world)
+        src, dst, w = local_links(mmap, off, size)
+        part = torch.from_numpy(oracle_lib.remap_apply(src, dst, w, x[off: off + size], mmap.n_model))
+        dist.all_reduce(part)  # the one collective: partial sums of the whole model grid
+        q.put((rank, part.numpy().tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_model_remap_one_allreduce():
+    """Exchange -> model remap on APPLE shards: each rank applies its own links to the whole
+    model grid, one all-reduce completes it; equal to the single-process remap up to the
+    association of the shared model cells."""
+    import torch.multiprocessing as mp
+
+    from fcx.parallel import synthetic_model_map
+
+    n, world = 20_003, 2
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    port = _free_port()
+    procs = [ctx.Process(target=_remap_rank, args=(r, world, port, n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get() for _ in range(world)]
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    mmap = synthetic_model_map(n, 300, links_per_cell=2)
+    x = np.random.default_rng(3).normal(size=n)
+    ref = oracle_lib.remap_apply(mmap.src, mmap.dst, mmap.weight, x, mmap.n_model)
+    for _, vals in res:
+        assert mixed_error(np.array(vals), ref) <= 1e-12
+    np.testing.assert_array_equal(np.array(res[0][1]), np.array(res[1][1]))  # every rank gets it
