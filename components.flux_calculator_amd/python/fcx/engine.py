@@ -126,6 +126,10 @@ class Engine:
     def step(self, phase=PHASE_ALL, current_step_time=0):
         _lib.check(self.lib.fcx_step(self.h, phase, int(current_step_time)))
 
+    def do_regridding(self, name, surface_type=0):
+        """do_regridding (basic:463-522) of one variable, host arrays in and out."""
+        _lib.check(self.lib.fcx_do_regridding(self.h, IDX[name], int(surface_type)))
+
     def synchronize(self):
         _lib.check(self.lib.fcx_synchronize(self.h))
 

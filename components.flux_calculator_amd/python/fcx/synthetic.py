@@ -266,3 +266,62 @@ def inputs_for_bench(n, seed=BASE_SEED):
     d = bottom_fields(n, 1, seed)
     d.update(atmos_fields(n, seed, tsur=d["TSUR"]))
     return d
+
+
+class SyntheticCoupler:
+    """A stand-in for OASIS3-MCT in fcx.driver: get() fills a received field with the
+    seeded synthetic values of its variable (SURVEY.md 8d distributions) for the field's
+    grid, surface type and time; put() records a copy of every sent field.
+
+    Names are the reference's R/S + letter + VAR + NN (basic:150, 267)."""
+
+    def __init__(self, grid_size, num_surface_types, seed=BASE_SEED):
+        self.grid_size = list(grid_size)
+        self.T = max(int(num_surface_types), 1)
+        self.seed = seed
+        self.sent = {}  # (name, time) -> ndarray
+        self.grid_of = {}  # received name -> which_grid
+        self._cache = {}
+
+    def _values(self, g, time):
+        key = (g, time)
+        if key not in self._cache:
+            n = self.grid_size[g - 1]
+            s = self.seed + 7919 * g + (time // 60)
+            bottom = [bottom_fields(n, st, s) for st in range(1, self.T + 1)]
+            atm = atmos_fields(n, s, tsur=bottom[0]["TSUR"])
+            fa = fare(n, self.T, s)
+            for st in range(self.T):
+                bottom[st]["FARE"] = fa[st]
+            self._cache[key] = (atm, bottom)
+        return self._cache[key]
+
+    def get(self, name, time, out, which_grid=None):
+        var, st = name[2:6], int(name[6:8])
+        g = which_grid or self.grid_of.get(name, 1)
+        atm, bottom = self._values(g, time)
+        src = atm if st == 0 else bottom[min(st, self.T) - 1]
+        if var in src:
+            vals = src[var]
+        elif var in atm:
+            vals = atm[var]
+        else:
+            vals = bottom[min(max(st, 1), self.T) - 1].get(var)
+        if vals is None:
+            raise KeyError(f"synthetic coupler has no values for {name}")
+        if hasattr(out, "copy_"):
+            import torch
+
+            out.copy_(torch.as_tensor(vals, dtype=out.dtype))
+        else:
+            out[:] = vals
+
+    def put(self, name, time, array):
+        a = array if isinstance(array, np.ndarray) else array.detach().cpu().numpy()
+        self.sent[(name, time)] = np.array(a, copy=True)
+
+    @classmethod
+    def for_setup(cls, setup, seed=BASE_SEED):
+        c = cls(setup.grid_size, setup.num_surface_types, seed)
+        c.grid_of = {f.name: f.which_grid for f in setup.input_field}
+        return c

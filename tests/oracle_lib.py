@@ -91,11 +91,18 @@ IDX0 = {n: i for i, n in enumerate(VARNAMES)}
 class OracleState:
     """A private copy of a case's LocalFields (aliasing preserved) wired into FcoState."""
 
-    def __init__(self, case, current_step_time=0):
+    def __init__(self, case, current_step_time=0, copy=True):
+        """copy=False: work in place on the case's own float64 host arrays (the way the
+        Fortran works on local_field), for OracleEngine."""
         self.case = case
         self.arrays = {}
         copies = {}
         for key, a in case.lf.field.items():
+            if not copy:
+                if not (isinstance(a, np.ndarray) and a.dtype == np.float64 and a.flags.c_contiguous):
+                    raise TypeError(f"{key}: in-place oracle needs contiguous float64 host arrays")
+                self.arrays[key] = a
+                continue
             a = np.asarray(a) if isinstance(a, np.ndarray) else a.detach().cpu().numpy()
             if id(a) not in copies:
                 copies[id(a)] = np.array(a, dtype=np.float64, copy=True)
@@ -141,6 +148,28 @@ def run_case(case, kind="c", current_step_time=0, phases=(1, 2), regrid=False):
     o = OracleState(case, current_step_time)
     run_state(o, kind, phases, regrid)
     return o.outputs()
+
+
+class OracleEngine:
+    """The fcx.driver engine interface (step / do_regridding) on the C oracle, in place on
+    a set-up's LocalFields: the reference time loop with the oracle doing the arithmetic."""
+
+    def __init__(self, setup, corrections=None, regrid=None):
+        from fcx.synthetic import Case
+
+        self.case = Case(name="setup", lf=setup.local_field, num_surface_types=setup.num_surface_types,
+                         methods=setup.methods, corrections=corrections, averages=setup.averages(),
+                         regrid=regrid)
+        self.o = OracleState(self.case, 0, copy=False)
+        self.lib, _ = load("c")
+
+    def do_regridding(self, name, surface_type=0):
+        self.lib.fco_do_regridding(ctypes.byref(self.o.st), IDX0[name], int(surface_type))
+
+    def step(self, phase, current_step_time=0):
+        if self.case.corrections is not None:
+            self.o.st.current_month = current_month(self.case.corrections[0], current_step_time)
+        run_state(self.o, "c", (1, 2) if phase == 3 else (phase,), regrid=True)
 
 
 def run_state(o, kind="c", phases=(1, 2), regrid=False):
