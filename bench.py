@@ -38,8 +38,8 @@ VARIANTS = ("CCLM", "MOM5", "RCO")
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=50)
-    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--warmup", type=int, default=200)
     p.add_argument("--cells", type=int, default=10_000_000, help="exchange-grid cells per GPU (weak scaling)")
     p.add_argument("--global-cells", type=int, default=0,
                    help="fixed global grid sharded over the ranks by APPLE ranges (strong scaling, "

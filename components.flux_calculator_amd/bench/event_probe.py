@@ -29,6 +29,8 @@ def main():
     ap.add_argument("--spacer-mb", type=int, default=0, help="allocation between inputs and engines")
     ap.add_argument("--pool", action="store_true",
                     help="repack every case's device arrays into one allocation before the engines")
+    ap.add_argument("--pool-reverse", action="store_true",
+                    help="with --pool: pack the cases in reverse order (case 0's arrays last)")
     ap.add_argument("--engines-reversed", action="store_true",
                     help="allocate all cases first, then create the engines in reverse order")
     a = ap.parse_args()
@@ -53,7 +55,7 @@ def main():
         cases.append((c, outs, atmos if a.atmos else None))
     if a.pool:  # one allocation for all fields of all cases (aliases kept)
         uniq = {}
-        for c, _, _ in cases:
+        for c, _, _ in (cases[::-1] if a.pool_reverse else cases):
             for t in c.lf.field.values():
                 uniq.setdefault(t.data_ptr(), t)
         total = sum(t.numel() for t in uniq.values())
@@ -120,21 +122,24 @@ def main():
     flush_buf = torch.ones(64 << 20, dtype=torch.float64, device=dev)  # 512 MB
     ev2 = torch.cuda.Event(enable_timing=True)
     flushed = {}
-    for x in range(len(engines)):
-        y = 0
-        tf, ty = [], []
-        for r in range(15):
-            engines[x][2].run(PHASE_ALL, 0)
-            ev0.record(stream)
-            flush_buf.sum()
-            ev2.record(stream)
-            engines[y][2].run(PHASE_ALL, 0)
-            ev1.record(stream)
-            ev1.synchronize()
-            tf.append(ev0.elapsed_time(ev2))
-            ty.append(ev2.elapsed_time(ev1))
-        flushed[f"{names[y]} after {names[x]} + 512 MB read"] = {"flush_ms": round(float(np.median(tf)), 4),
-                                                                 "kernel_ms": round(float(np.median(ty)), 4)}
+    # a 512 MB read (sum) or write (fill) between X and Y: a write has to evict dirty
+    # memory-side cache lines X left behind, a read need not
+    for kind, op in (("read", lambda: flush_buf.sum()), ("write", lambda: flush_buf.fill_(1.0))):
+        for x in range(len(engines)):
+            y = 0
+            tf, ty = [], []
+            for r in range(15):
+                engines[x][2].run(PHASE_ALL, 0)
+                ev0.record(stream)
+                op()
+                ev2.record(stream)
+                engines[y][2].run(PHASE_ALL, 0)
+                ev1.record(stream)
+                ev1.synchronize()
+                tf.append(ev0.elapsed_time(ev2))
+                ty.append(ev2.elapsed_time(ev1))
+            flushed[f"{names[y]} after {names[x]} + 512 MB {kind}"] = {
+                "flush_ms": round(float(np.median(tf)), 4), "kernel_ms": round(float(np.median(ty)), 4)}
     del flush_buf
 
     modes = ["none", "torch_events", "fcx_timing", "both"]
