@@ -95,6 +95,56 @@ int run(const char *name, Ptrs &p, long n, int blocks) {
   return 0;
 }
 
+// The bench's step shape: CCLM (10 in / 7 out), MOM5 (11 / 7) and RCO (5 / 6) back to back on
+// SHARED inputs, each writing its OWN outputs (as the three engines of bench.py do).  A kernel
+// repeated on the same outputs can coalesce its writes with the previous launch's dirty lines
+// in the memory-side Infinity Cache; in this sequence every launch writes fresh addresses.
+int interleaved(const Ptrs &base, long n, int blocks) {
+  Ptrs pc = base, pm = base, pr = base, pc2 = base;
+  for (int w = 0; w < 7; ++w) pc.out[w] = base.out[w], pm.out[w] = base.out[7 + w], pc2.out[w] = base.out[7 + w];
+  for (int w = 0; w < 6; ++w) pr.out[w] = base.out[14 + w];
+  hipEvent_t ev[4];
+  for (auto &h : ev) CHECK(hipEventCreate(&h));
+  const int reps = 50;
+  float t[3] = {0, 0, 0};
+  for (int r = -5; r < reps; ++r) {
+    CHECK(hipEventRecord(ev[0]));
+    hipLaunchKernelGGL((probe<10, 7, 2, true>), dim3(blocks), dim3(256), 0, 0, pc, n);
+    CHECK(hipEventRecord(ev[1]));
+    hipLaunchKernelGGL((probe<11, 7, 2, true>), dim3(blocks), dim3(256), 0, 0, pm, n);
+    CHECK(hipEventRecord(ev[2]));
+    hipLaunchKernelGGL((probe<5, 6, 2, true>), dim3(blocks), dim3(256), 0, 0, pr, n);
+    CHECK(hipEventRecord(ev[3]));
+    CHECK(hipEventSynchronize(ev[3]));
+    if (r < 0) continue;
+    for (int k = 0; k < 3; ++k) {
+      float ms;
+      CHECK(hipEventElapsedTime(&ms, ev[k], ev[k + 1]));
+      t[k] += ms / reps;
+    }
+  }
+  const int rw[3][2] = {{10, 7}, {11, 7}, {5, 6}};
+  const char *nm[3] = {"interleaved cclm-shape nt", "interleaved mom5-shape nt", "interleaved rco-shape nt"};
+  for (int k = 0; k < 3; ++k)
+    printf("%-28s R=%2d W=%2d C=2 nt=1 blocks=%6d  %8.3f ms  %7.1f GB/s\n", nm[k], rw[k][0], rw[k][1], blocks, t[k],
+           (rw[k][0] + rw[k][1]) * n * 8.0 / (t[k] * 1e-3) / 1e9);
+  // one shape alternating between two output sets: fresh addresses every launch
+  float alt = 0;
+  for (int r = -4; r < 2 * reps; ++r) {
+    CHECK(hipEventRecord(ev[0]));
+    hipLaunchKernelGGL((probe<10, 7, 2, true>), dim3(blocks), dim3(256), 0, 0, (r & 1) ? pc2 : pc, n);
+    CHECK(hipEventRecord(ev[1]));
+    CHECK(hipEventSynchronize(ev[1]));
+    float ms;
+    CHECK(hipEventElapsedTime(&ms, ev[0], ev[1]));
+    if (r >= 0) alt += ms / (2 * reps);
+  }
+  printf("%-28s R=%2d W=%2d C=2 nt=1 blocks=%6d  %8.3f ms  %7.1f GB/s\n", "cclm-shape nt, 2 out sets", 10, 7, blocks,
+         alt, 17 * n * 8.0 / (alt * 1e-3) / 1e9);
+  for (auto &h : ev) CHECK(hipEventDestroy(h));
+  return 0;
+}
+
 int main() {
   // 10M cells x 8 B = 80 MB per array: a 17-array step (1.36 GB) is far beyond the 256 MB
   // Infinity Cache.  The 1-in/1-out copy uses 100M-element arrays (1.6 GB per launch) for
@@ -138,5 +188,6 @@ int main() {
   run<14, 21, 2, true>("T2 cclm-shape nt", p, n, 8192);
   run<26, 32, 2, true>("T4ish 26/32 nt", p, n, 8192);
   run<1, 16, 2, false>("write-heavy 1/16", p, n, 2048);
+  if (interleaved(p, n, 8192)) return 1;
   return 0;
 }
