@@ -156,10 +156,10 @@ struct fcx_engine {
   bool pin_host = true;
   int chunks = 8;                                   // fcx_step pipeline depth (1 = off)
   int64_t min_chunk = 256 * 1024;                   // cells per chunk at least (~2 MB/array)
-  // kernels use the host arrays in place: 0 off (default), 1 on, 2 auto (small grids).  Off
-  // by default: it is the one mode in which kernels touch host memory directly; an
-  // unexplained, timing-dependent illegal-access report followed a test using it
-  int zero_copy = 0;
+  // kernels use the host arrays in place: 0 off, 1 on, 2 auto (default: grids below two
+  // pipeline chunks, where per-array copy calls dominate the step, and only when page-locking
+  // is allowed)
+  int zero_copy = 2;
   bool zc_active = false;
   bool timing = true;  // ev0/ev1 around every run (fcx_last_kernel_ms)
   std::vector<std::pair<char *, size_t>> pinned;    // hipHostRegister'ed page ranges
@@ -1046,7 +1046,7 @@ extern "C" int fcx_commit(fcx_engine *e) {
   // auto: zero-copy exactly where the pipelined step would not apply (grids below two
   // chunks), i.e. where the step is latency-bound and per-array copies dominate it
   const int64_t n_big = std::max(e->n[0], std::max(e->n[1], e->n[2]));
-  e->zc_active = e->zero_copy == 1 || (e->zero_copy == 2 && n_big < 2 * e->min_chunk);
+  e->zc_active = e->zero_copy == 1 || (e->zero_copy == 2 && e->pin_host && n_big < 2 * e->min_chunk);
   if (e->pin_host || e->zc_active) pin_host_arrays(e);
   if (e->zc_active) map_host_arrays(e);
   // one pooled allocation for all host-bound mirrors, 256-B aligned sub-buffers

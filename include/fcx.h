@@ -203,8 +203,9 @@ enum fcx_option {
                                    default 262144: smaller grids take the sequential step) */
   FCX_OPT_ZERO_COPY = 9,        /* host-bound fields read/written by the kernels in place
                                    through the host link (page-locked, mapped): no mirrors,
-                                   no copy calls.  0 off (default), 1 on, 2 auto: on when
-                                   every grid is below 2 x PIPELINE_MIN_CHUNK cells */
+                                   no copy calls.  0 off, 1 on, 2 auto (default): on when
+                                   every grid is below 2 x PIPELINE_MIN_CHUNK cells and
+                                   PIN_HOST is on */
   FCX_OPT_TIMING = 10           /* record the events behind fcx_last_kernel_ms (default 1) */
 };
 int fcx_set_option(fcx_engine *e, int option, int64_t value);
