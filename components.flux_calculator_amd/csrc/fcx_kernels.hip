@@ -252,13 +252,26 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
   const double *h_ts = nullptr, *h_fi = nullptr, *h_ps = nullptr, *h_pa = nullptr, *h_qa = nullptr,
                *h_ta = nullptr, *h_u = nullptr, *h_v = nullptr, *h_amoi = nullptr, *h_cmoi = nullptr,
                *h_chea = nullptr, *h_amom = nullptr, *h_cmom = nullptr;
-#define HOLD(var, ptr)                    \
-  if ((ptr) && (ptr) != h_##var) {        \
-    var = LD(ptr, j0, nt);                \
-    h_##var = (ptr);                      \
+  // With T from the parameter block (TM = 0) the inputs are reloaded for every type instead
+  // of held: holding kept 14 two-cell vectors (~56 VGPRs) live across the type loop and the
+  // kernels at 3 waves per SIMD; the shared atmosphere fields come back from L2 / the
+  // Infinity Cache.  FCX_HOLD_ACROSS_TYPES=1 restores the holding (A/B builds).
+#ifndef FCX_HOLD_ACROSS_TYPES
+#define FCX_HOLD_ACROSS_TYPES 0
+#endif
+  constexpr bool kReload = TM == 0 && !FCX_HOLD_ACROSS_TYPES;
+#define HOLD(var, ptr)                          \
+  if constexpr (kReload) {                      \
+    if (ptr) var = LD(ptr, j0, nt);             \
+  } else if ((ptr) && (ptr) != h_##var) {       \
+    var = LD(ptr, j0, nt);                      \
+    h_##var = (ptr);                            \
   }
 
   for (int s = 0; s < T; ++s) {
+    if constexpr (kReload) {  // nothing of the previous type stays live
+      ts = fi = ps = pa = qa = ta = u = v = amoi = cmoi = chea = amom = cmom = vel = Vec<C, R>{};
+    }
     const TypeParams &tp = P->type[s];
     const TGridPtrs &g = tp.t;
     constexpr int8_t kVarMethod = VAR == 1 ? FCX_CCLM : VAR == 2 ? FCX_MOM5 : FCX_RCO;
@@ -277,7 +290,7 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
       HOLD(pa, g.patm)
       HOLD(qa, g.qatm)
       HOLD(ta, g.tatm)
-      const bool wind_new = (g.uatm && g.uatm != h_u) || (g.vatm && g.vatm != h_v);
+      const bool wind_new = kReload ? (g.uatm || g.vatm) : ((g.uatm && g.uatm != h_u) || (g.vatm && g.vatm != h_v));
       HOLD(u, g.uatm)
       HOLD(v, g.vatm)
       HOLD(amoi, g.amoi)
@@ -477,8 +490,12 @@ __device__ __forceinline__ void wave_sync() {
 // lowest set bit index of m, 64 if none
 __device__ __forceinline__ int first_bit(uint64_t m) { return m ? __builtin_ctzll(m) : 64; }
 
+// blocks per CU the multi-type (RAVG) fused kernel is compiled for: 4 -> <= 128 VGPRs
+#ifndef FCX_RAVG_ATMOS_BLOCKS
+#define FCX_RAVG_ATMOS_BLOCKS 4
+#endif
 template <int VAR, bool NT, int TM, bool RAVG>
-__global__ __launch_bounds__(256, RAVG ? 3 : 1) void cells_atmos_kernel(const Params *__restrict__ P,
+__global__ __launch_bounds__(256, RAVG ? FCX_RAVG_ATMOS_BLOCKS : 1) void cells_atmos_kernel(const Params *__restrict__ P,
                                                           const double *__restrict__ corr_m,
                                                           const AtmosFused af, int64_t lo, int64_t hi) {
   // product rows [kFusedFields][kRow]; with RAVG they first serve as the accumulators of
