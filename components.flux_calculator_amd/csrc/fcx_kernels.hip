@@ -259,13 +259,30 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
 #ifndef FCX_HOLD_ACROSS_TYPES
 #define FCX_HOLD_ACROSS_TYPES 0
 #endif
+// FCX_TEMPORAL_SHARED=1: load an input the next type binds too with a temporal load, so the
+// reload hits L2.  Measured (T=2/T=6 benches, 3 interleaved runs each): L2-miss reads fall to
+// the algorithmic bytes (CCLM T=2 186 -> 132 B/cell), but the step is 1.7 % / 0.6 % slower --
+// the non-temporal reloads were already served by the Infinity Cache.  Off by default.
+#ifndef FCX_TEMPORAL_SHARED
+#define FCX_TEMPORAL_SHARED 0
+#endif
   constexpr bool kReload = TM == 0 && !FCX_HOLD_ACROSS_TYPES;
-#define HOLD(var, ptr)                          \
-  if constexpr (kReload) {                      \
-    if (ptr) var = LD(ptr, j0, nt);             \
-  } else if ((ptr) && (ptr) != h_##var) {       \
-    var = LD(ptr, j0, nt);                      \
-    h_##var = (ptr);                            \
+  // grp.member names the pointer in TypeParams (the next type's is compared when
+  // FCX_TEMPORAL_SHARED is on).
+#define HOLD(var, grp, member)                                                         \
+  {                                                                                    \
+    const double *ptr_ = tp.grp.member;                                                \
+    if constexpr (kReload) {                                                           \
+      if (ptr_) {                                                                      \
+        if (FCX_TEMPORAL_SHARED && s + 1 < T && P->type[s + 1].grp.member == ptr_)     \
+          var = ld<C, false, R>(reinterpret_cast<const R *>(ptr_), j0, nt);            \
+        else                                                                           \
+          var = LD(ptr_, j0, nt);                                                      \
+      }                                                                                \
+    } else if (ptr_ && ptr_ != h_##var) {                                              \
+      var = LD(ptr_, j0, nt);                                                          \
+      h_##var = ptr_;                                                                  \
+    }                                                                                  \
   }
 
   for (int s = 0; s < T; ++s) {
@@ -284,24 +301,23 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
     if (do_t) {
       // ---- every t-grid input this type needs (before any store of this type)
       Vec<C, R> qs = {}, me = {};
-      HOLD(ts, g.tsur)
-      HOLD(fi, g.fice)
-      HOLD(ps, g.psur)
-      HOLD(pa, g.patm)
-      HOLD(qa, g.qatm)
-      HOLD(ta, g.tatm)
+      HOLD(ts, t, tsur)
+      HOLD(fi, t, fice)
+      HOLD(ps, t, psur)
+      HOLD(pa, t, patm)
+      HOLD(qa, t, qatm)
+      HOLD(ta, t, tatm)
       const bool wind_new = kReload ? (g.uatm || g.vatm) : ((g.uatm && g.uatm != h_u) || (g.vatm && g.vatm != h_v));
-      HOLD(u, g.uatm)
-      HOLD(v, g.vatm)
-      HOLD(amoi, g.amoi)
-      HOLD(cmoi, g.cmoi)
-      HOLD(chea, g.chea)
+      HOLD(u, t, uatm)
+      HOLD(v, t, vatm)
+      HOLD(amoi, t, amoi)
+      HOLD(cmoi, t, cmoi)
+      HOLD(chea, t, chea)
       if (g.qsur_in) qs = LD(g.qsur_in, j0, nt);  // may be written by this pass: never held
       if (g.meva_in) me = LD(g.meva_in, j0, nt);
       if constexpr (MERGED) {
-        const UVGridPtrs &gu = tp.uv[0];
-        HOLD(amom, gu.amom)
-        HOLD(cmom, gu.cmom)
+        HOLD(amom, uv[0], amom)
+        HOLD(cmom, uv[0], cmom)
       }
       if (wind_new) FOR_C vel.v[i] = wind(u.v[i], v.v[i]);
       if constexpr (RAVG) {
