@@ -79,7 +79,7 @@ def child(a):
         print(json.dumps(link_ceiling(N_IN[a.variants] * 8 * n, N_OUT[a.variants] * 8 * n)))
         return
     case = build_case(a.variants, n=n, T=1, data=inputs_for_bench(n))
-    opts = dict(SWEEP)[a.only]
+    opts = {**dict(SWEEP)[a.only], "timing": 1}  # device_timeline_ms / kernel_ms below
     eng = Engine(case.lf, 1, case.methods, options=opts)
     pinned = eng.pinned_bytes()
     eng.step(PHASE_ALL, 0)  # warm-up (first touch, plan, code objects)

@@ -50,7 +50,8 @@ def main():
     engines = []
     for v in VARIANTS:
         c = build_case(v, n=n, T=1, bias=bool(a.bias), device="cuda:0", data=data)
-        engines.append(Engine(c.lf, 1, c.methods, corrections=c.corrections, stream=stream.cuda_stream))
+        engines.append(Engine(c.lf, 1, c.methods, corrections=c.corrections, stream=stream.cuda_stream,
+                              options={"timing": 1}))
     for k in range(50):
         for e in engines:
             e.run(PHASE_ALL, k * 3600)
@@ -68,10 +69,43 @@ def main():
             e.run(PHASE_ALL, k * 3600)
             ts.append(e.last_kernel_ms() * 1e3)
         kern[v] = round(float(np.median(ts)), 2)
-    for e in engines:
-        e.close()
     out["device"] = {"us_per_step_3_variants": round(wall, 2), "kernel_us_median": kern,
                      "Mcells_per_s": round(3 * n / wall, 1)}
+
+    # ---- same step without the engines' timing events, and captured into one HIP graph
+    # (the engines launch on the capture stream; the replay reuses the captured month's
+    # bias slice, fine for timing)
+    for e in engines:
+        e.set_option("timing", 0)
+
+    def timed(fn, steps):
+        for k in range(50):
+            fn(k)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for k in range(steps):
+            fn(k)
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / steps * 1e6
+
+    def plain(k):
+        for e in engines:
+            e.run(PHASE_ALL, 0)
+    wall_ne = timed(plain, a.steps)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        cap = torch.cuda.current_stream().cuda_stream
+        for e in engines:
+            e.set_stream(cap)
+        for e in engines:
+            e.run(PHASE_ALL, 0)
+    for e in engines:
+        e.set_stream(stream.cuda_stream)
+    wall_g = timed(lambda k: g.replay(), a.steps)
+    out["device"]["us_per_step_no_events"] = round(wall_ne, 2)
+    out["device"]["us_per_step_one_graph"] = round(wall_g, 2)
+    for e in engines:
+        e.close()
 
     # ---- host-bound: fcx_step per variant (upload, run, download, synchronise)
     for mode, opts in (("host_mirrors", {"zero_copy": 0}), ("host_zero_copy", {"zero_copy": 1})):
@@ -79,6 +113,7 @@ def main():
         for v in VARIANTS:
             c = build_case(v, n=n, T=1, bias=bool(a.bias), data=host)
             e = Engine(c.lf, 1, c.methods, corrections=c.corrections, options=opts)
+            e.set_option("timing", 0)
             for k in range(50):
                 e.step(PHASE_ALL, k * 3600)
             ts = []
@@ -86,6 +121,7 @@ def main():
                 t0 = time.perf_counter()
                 e.step(PHASE_ALL, k * 3600)
                 ts.append(time.perf_counter() - t0)
+            e.set_option("timing", 1)
             e.run(PHASE_ALL, 0)
             e.synchronize()
             kms = e.last_kernel_ms()

@@ -126,6 +126,11 @@ class Engine:
     def step(self, phase=PHASE_ALL, current_step_time=0):
         _lib.check(self.lib.fcx_step(self.h, phase, int(current_step_time)))
 
+    def set_stream(self, stream):
+        """fcx_set_stream: launch on this HIP stream (a raw hipStream_t, e.g. a torch
+        stream's .cuda_stream) from now on, e.g. a capturing stream for a HIP graph."""
+        _lib.check(self.lib.fcx_set_stream(self.h, ctypes.c_void_p(stream)))
+
     def do_regridding(self, name, surface_type=0):
         """do_regridding (basic:463-522) of one variable, host arrays in and out."""
         _lib.check(self.lib.fcx_do_regridding(self.h, IDX[name], int(surface_type)))

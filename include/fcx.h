@@ -146,7 +146,8 @@ int fcx_do_regridding(fcx_engine *e, int var, int surface_type);           /* ba
 /* ---- device-resident use and measurement ---- */
 /* device buffer behind a slot (NULL if unbound) */
 int fcx_device_ptr(fcx_engine *e, int surface_type, int grid, int var, double **dptr);
-/* device time (hipEvents on the engine stream) of the kernels of the last fcx_run */
+/* device time (hipEvents on the engine stream) of the kernels of the last fcx_run;
+   needs FCX_OPT_TIMING = 1 */
 int fcx_last_kernel_ms(fcx_engine *e, float *ms);
 /* bytes of caller host memory page-locked by this engine (FCX_OPT_PIN_HOST) */
 int fcx_pinned_bytes(fcx_engine *e, int64_t *bytes);
@@ -206,7 +207,8 @@ enum fcx_option {
                                    no copy calls.  0 off, 1 on, 2 auto (default): on when
                                    every grid is below 2 x PIPELINE_MIN_CHUNK cells and
                                    PIN_HOST is on */
-  FCX_OPT_TIMING = 10           /* record the events behind fcx_last_kernel_ms (default 1) */
+  FCX_OPT_TIMING = 10           /* record the events behind fcx_last_kernel_ms (default 0:
+                                   two event records per run cost ~8 us on small grids) */
 };
 int fcx_set_option(fcx_engine *e, int option, int64_t value);
 
