@@ -22,7 +22,7 @@ ATM = (("MEVA", 1), ("HLAT", 1), ("HSEN", 1), ("RBBR", 1), ("UMOM", 2), ("VMOM",
 
 def grids(units_per_block_round, waves_units):
     """Caps giving k units per thread/wave exactly, for k = 1..4, plus the round numbers."""
-    out = {2048, 4096, 8192, 16384, 0}
+    out = {1024, 2048, 4096, 8192, 16384, 0}
     for k in (1, 2, 3, 4, 6):
         out.add(int(np.ceil(waves_units / (units_per_block_round * k))))
     return sorted(out)
@@ -35,6 +35,8 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--families", default="fused,f64,f32")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--types", type=int, default=1,
+                    help="surface types (>= 2: the type-0 averages are accumulated, as in bench.py)")
     a = ap.parse_args()
     import torch
 
@@ -51,14 +53,16 @@ def main():
     engines = {}
     for fam in a.families.split(","):
         for v in ("CCLM", "MOM5", "RCO"):
-            c = build_case(v, n=n, T=1, device=dev, data=data)
+            c = build_case(v, n=n, T=a.types, device=dev, data=data if a.types == 1 else None)
             atmos = None
             if fam == "fused":
                 outs = [torch.empty(la.n_atmos, dtype=torch.float64, device=dev) for _ in ATM]
-                atmos = {"local": la, "fields": [(PHASE_NORMAL, 1, g, name, o) for (name, g), o in zip(ATM, outs)]}
+                s0 = 0 if a.types >= 2 else 1
+                atmos = {"local": la, "fields": [(PHASE_NORMAL, s0, g, name, o) for (name, g), o in zip(ATM, outs)]}
             if fam == "f32":
                 c = as_dtype(c, "float32")
-            e = Engine(c.lf, 1, c.methods, device=0, stream=stream.cuda_stream, atmos=atmos)
+            e = Engine(c.lf, c.num_surface_types, c.methods, averages=c.averages, device=0,
+                       stream=stream.cuda_stream, atmos=atmos)
             if fam == "fused":
                 units, per_block = (n + 127) // 128, 4  # wave tiles, 4 waves per block
             else:
