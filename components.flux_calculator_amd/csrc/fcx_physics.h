@@ -61,11 +61,28 @@ __device__ __forceinline__ R meva_rco(R qa, R ts, R vel) {
   return rho_a * c_aw * vel * (q_w - qa);
 }
 
+// x**y for the Exner ratio ps/pa (within a few percent of 1) and y = Rd/cp: exp(y * log x).
+// With |y log x| < 0.01 the argument's error is ~1e-19 relative, so the result is as close
+// to x**y as a library pow (last-ulp differences only, like the reference's own pow against
+// ROCm's), at a fraction of ROCm's fp64 pow, which carries extra-precision log/exp for any
+// base.  Special values agree with pow for y > 0 (0 -> 0, inf -> inf, x < 0 or NaN -> NaN).
+#ifndef FCX_POW_EXPLOG
+#define FCX_POW_EXPLOG 1
+#endif
+template <class R>
+__device__ __forceinline__ R pow_exner(R x, R y) {
+#if FCX_POW_EXPLOG
+  return exp(y * log(x));
+#else
+  return pow(x, y);
+#endif
+}
+
 // flux_lib/heat/flux_heat_sensible.F90:74-94 (flux_heat_sensible_cclm; _mom5 = with CHEA)
 template <class R>
 __device__ __forceinline__ R hsen_cclm(R a, R pa, R ps, R qs, R ta, R ts, R vel) {
   const R fa = a * fmax(vel, R(kUmin)) * ps / (R(kRd) * t_tilde(ts, qs));
-  const R ef = pow(ps / pa, R(kRd / kCp));
+  const R ef = pow_exner(ps / pa, R(kRd / kCp));
   return fa * R(kCp) * (ts - ta * ef);
 }
 
