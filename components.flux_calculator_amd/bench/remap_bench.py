@@ -1,0 +1,81 @@
+#!/usr/bin/env python3
+"""Row f3 measurement: the exchange -> model remap (fcx_add_remap, atmos_kernel on the model
+grid's CSR) on config-3 sizes.  10M exchange cells (CCLM, T=1, fields HBM-resident), a
+2.5M-cell model grid (synthetic_model_map: runs of 1..8 exchange cells per model cell,
+scattered; 1 or 2 links per exchange cell), the 6 fluxes OASIS would send to the bottom
+model.  The remap time is the step with the remap minus the step without it (HIP events,
+medians of interleaved rounds); the kernel alone is in the rocprof summary of the same run.
+
+Algorithmic bytes of one remap launch: per link 4 (column) + 8 (weight) + 8 per field (the
+gathered value); per model cell 4 (row pointer) + 8 per field (the written sum).
+
+  python components.flux_calculator_amd/bench/remap_bench.py [--cells N] [--model M]
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.join(ROOT, "components.flux_calculator_amd", "python"))
+FIELDS = (("MEVA", 1), ("HLAT", 1), ("HSEN", 1), ("RBBR", 1), ("UMOM", 2), ("VMOM", 3))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--cells", type=int, default=10_000_000)
+    ap.add_argument("--model", type=int, default=2_500_000)
+    ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--reps", type=int, default=10)
+    a = ap.parse_args()
+    import torch
+
+    from fcx.basic import PHASE_ALL
+    from fcx.engine import Engine
+    from fcx.parallel import synthetic_model_map
+    from fcx.synthetic import build_case, inputs_for_bench
+
+    n, m = a.cells, a.model
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.current_stream(dev)
+    data = {k: torch.as_tensor(v).to(dev) for k, v in inputs_for_bench(n).items()}
+    case = build_case("CCLM", n=n, T=1, device=dev, data=data)
+    engines = {"none": Engine(case.lf, 1, case.methods, device=0, stream=stream.cuda_stream)}
+    alg = {}
+    for links in (1, 2):
+        mm = synthetic_model_map(n, m, links_per_cell=links)
+        outs = {k: torch.empty(m, dtype=torch.float64, device=dev) for k, _ in FIELDS}
+        rm = {"n_dst": m, "src": mm.src, "dst": mm.dst, "w": mm.weight,
+              "fields": [(2, 1, g, k, outs[k]) for k, g in FIELDS]}
+        engines[f"{links} link(s)/cell"] = Engine(case.lf, 1, case.methods, device=0,
+                                                  stream=stream.cuda_stream, remaps=[rm])
+        nl, nf = mm.src.size, len(FIELDS)
+        alg[f"{links} link(s)/cell"] = {"links": int(nl), "bytes": int(nl * (4 + 8 + 8 * nf) + m * (4 + 8 * nf))}
+    times = {k: [] for k in engines}
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for r in range(a.rounds):
+        order = list(engines)
+        np.random.default_rng(r).shuffle(order)
+        for k in order:
+            eng = engines[k]
+            eng.run(PHASE_ALL, 0)
+            e0.record(stream)
+            for _ in range(a.reps):
+                eng.run(PHASE_ALL, 0)
+            e1.record(stream)
+            e1.synchronize()
+            times[k].append(e0.elapsed_time(e1) / a.reps)
+    base = float(np.median(times["none"]))
+    out = {"cells": n, "model_cells": m, "fields": len(FIELDS), "step_ms_without_remap": round(base, 4)}
+    for k, v in alg.items():
+        ms = float(np.median(times[k])) - base
+        out[k] = {**v, "remap_ms": round(ms, 4), "GBps_algorithmic": round(v["bytes"] / (ms * 1e-3) / 1e9, 1)}
+    for e in engines.values():
+        e.close()
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
