@@ -37,7 +37,8 @@ VARIANTS = ("CCLM", "MOM5", "RCO")
 
 def parse():
     p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--gpus", type=int, default=1,
+                   help="ranks (one per GPU); without a launcher bench.py starts torch.distributed.run itself")
     p.add_argument("--steps", type=int, default=200)
     p.add_argument("--warmup", type=int, default=200)
     p.add_argument("--cells", type=int, default=10_000_000, help="exchange-grid cells per GPU (weak scaling)")
@@ -137,8 +138,25 @@ def cpu_all_cores(args, variants):
                       f"APPLE ranges on {threads} threads, {el:.1f} s"}
 
 
+def relaunch(n):
+    """`python bench.py --gpus N` outside a launcher: run this same command under
+    torch.distributed.run (one rank per GPU, rendezvous on 127.0.0.1) as a child process,
+    before anything touches the GPU, and return its exit code."""
+    import socket
+    import subprocess
+
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(relaunch(args.gpus))
     variants = tuple(v for v in args.variants.split(",") if v)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
