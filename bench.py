@@ -57,6 +57,8 @@ def parse():
     p.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL)")
     p.add_argument("--same-device", action="store_true",
                    help="rehearsal only: every rank on GPU 0 (with --backend gloo on a 1-GPU box)")
+    p.add_argument("--max-blocks", type=int, default=None,
+                   help="A/B only: FCX_OPT_MAX_BLOCKS of every engine (default: the engine's)")
     p.add_argument("--precision", choices=("f64", "f32"), default="f64",
                    help="f32: the fp32 cell-pass variant (config 5; no atmosphere accumulation)")
     return p.parse_args()
@@ -230,7 +232,8 @@ def main():
                    # per-kernel times come from the bench's own events on the same stream;
                    # the engine's internal ones would add a second event pair per launch
                    # (measured +2.5 % per step, components.flux_calculator_amd/bench/event_probe.py)
-                   options={"atmos_in_run": 0, "timing": 0})
+                   options={"atmos_in_run": 0, "timing": 0,
+                            **({"max_blocks": args.max_blocks} if args.max_blocks is not None else {})})
         cases.append(c)
         engines.append(e)
     # algorithmic bytes of one fcx_run: every distinct field array read once / written once,

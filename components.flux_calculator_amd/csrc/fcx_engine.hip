@@ -1650,7 +1650,7 @@ extern "C" int fcx_set_option(fcx_engine *e, int option, int64_t value) {
       e->launch.cells_per_thread = (int)value;
       return FCX_OK;
     case FCX_OPT_MAX_BLOCKS:
-      if (value < 0 || value > (1 << 30)) return fail(FCX_E_ARG, "max blocks %lld", (long long)value);
+      if (value < -1 || value > (1 << 30)) return fail(FCX_E_ARG, "max blocks %lld", (long long)value);
       e->launch.max_blocks = (int)value;
       return FCX_OK;
     case FCX_OPT_NONTEMPORAL:

@@ -83,7 +83,8 @@ struct Params {
 // how one cells_kernel launch is instantiated
 struct LaunchConfig {
   int cells_per_thread = 2;  // 1 or 2 (2 needs 16-B aligned arrays)
-  int max_blocks = 8192;     // grid-stride cap; 0 = one unit per thread (8192: tuned)
+  int max_blocks = -1;       // grid-stride cap; 0 = one unit per thread; -1 = per-kernel
+                             // default (cells_kernel: 8192, fused accumulation: one trip)
   bool nontemporal = true;   // non-temporal hint on the streamed loads/stores
   bool merged = false;       // u/v grids are the t grid
   int variant = 0;           // 0 generic, 1 CCLM, 2 MOM5, 3 RCO (T=1 specialisations)

@@ -510,8 +510,12 @@ __device__ __forceinline__ int first_bit(uint64_t m) { return m ? __builtin_ctzl
 #ifndef FCX_RAVG_ATMOS_BLOCKS
 #define FCX_RAVG_ATMOS_BLOCKS 4
 #endif
+// blocks per CU the T=1 fused kernels are compiled for (1: no register cap)
+#ifndef FCX_T1_ATMOS_BLOCKS
+#define FCX_T1_ATMOS_BLOCKS 1
+#endif
 template <int VAR, bool NT, int TM, bool RAVG>
-__global__ __launch_bounds__(256, RAVG ? FCX_RAVG_ATMOS_BLOCKS : 1) void cells_atmos_kernel(const Params *__restrict__ P,
+__global__ __launch_bounds__(256, RAVG ? FCX_RAVG_ATMOS_BLOCKS : FCX_T1_ATMOS_BLOCKS) void cells_atmos_kernel(const Params *__restrict__ P,
                                                           const double *__restrict__ corr_m,
                                                           const AtmosFused af, int64_t lo, int64_t hi) {
   // product rows [kFusedFields][kRow]; with RAVG they first serve as the accumulators of
@@ -780,8 +784,11 @@ int launch_cells(const Params *hp, const Params *dp, const double *corr_m, const
   if (lo % kChunkAlign || lo < 0) return (int)hipErrorInvalidValue;
   if (hi <= lo) return 0;
   if (atm) {  // fused accumulation: T=1 specialised merged kernel, 2 cells per lane
+    // four waves per block, one 128-cell tile per wave and trip.  Default: one trip (full
+    // grid) -- +2 % per T=1 step over the 8192-block cap, equal at T=2 (profiles/r01/grid_ab)
     const int64_t tiles = (hi - lo + kTile - 1) / kTile;
-    const int blocks = (int)std::max<int64_t>(1, lc.max_blocks > 0 ? std::min<int64_t>(tiles, lc.max_blocks) : tiles);
+    const int64_t full = (tiles + 3) / 4;
+    const int blocks = (int)std::max<int64_t>(1, lc.max_blocks > 0 ? std::min<int64_t>(full, lc.max_blocks) : full);
     int r = 0;
     switch (lc.variant) {
       case 1: r = launch_atm_r<1>(hp, lc, blocks, s, dp, corr_m, *atm, lo, hi); break;
@@ -796,7 +803,7 @@ int launch_cells(const Params *hp, const Params *dp, const double *corr_m, const
   // caller's arrays are not 16-B aligned
   const int c = lc.cells_per_thread == 1 ? 1 : lc.f32 ? 4 : 2;
   const int64_t units = (hi - lo + c - 1) / c;
-  const int blocks = grid_for(units, lc.max_blocks);
+  const int blocks = grid_for(units, lc.max_blocks < 0 ? 8192 : lc.max_blocks);
   if (lc.f32) {
     if (c == 4)
       launch_r<4, float>(hp, lc, blocks, s, dp, corr_m, lo, hi);

@@ -12,7 +12,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 SRC = os.path.join(HERE, "..", "csrc", "fcx_kernels.hip")
 cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
        "-I" + os.path.join(HERE, "..", "csrc"), "-I" + os.path.join(HERE, "..", "..", "include"), "-c", SRC,
-       "-o", "/tmp/fcx_kernels_res.o", "-Rpass-analysis=kernel-resource-usage"]
+       "-o", "/tmp/fcx_kernels_res.o", "-Rpass-analysis=kernel-resource-usage"] + sys.argv[2:]
 out = subprocess.run(cmd, capture_output=True, text=True).stderr
 cur, rows = None, []
 for line in out.splitlines():

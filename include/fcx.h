@@ -193,7 +193,9 @@ int fcx_add_remap_field(fcx_engine *e, int32_t remap_id, int phase, int surface_
 /* launch tuning of the fused cells kernel (defaults are the measured best on MI355X) */
 enum fcx_option {
   FCX_OPT_CELLS_PER_THREAD = 1, /* 1 or 2 cells per lane (2: 16-B loads; default 2)       */
-  FCX_OPT_MAX_BLOCKS = 2,       /* grid-stride cap in 256-thread blocks; 0 = no cap       */
+  FCX_OPT_MAX_BLOCKS = 2,       /* grid-stride cap in 256-thread blocks; 0 = no cap;
+                                   -1 (default) = per kernel: 8192 for the flux pass, no
+                                   cap for the T=1 pass with the fused accumulation       */
   FCX_OPT_NONTEMPORAL = 3,      /* non-temporal hint on streamed loads/stores (default 1) */
   FCX_OPT_SPECIALIZE = 4,       /* T=1 CCLM/MOM5/RCO specialised kernels (default 1)      */
   FCX_OPT_ATMOS_IN_RUN = 5,     /* fcx_run also runs the atmosphere accumulation (def. 1) */
