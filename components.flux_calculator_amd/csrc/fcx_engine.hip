@@ -128,6 +128,9 @@ struct fcx_engine {
   std::vector<int32_t> atm_idx;
   int32_t atm_maxseg = 0;
   double *d_atm_carry = nullptr;
+  uint32_t *d_atm_flag = nullptr;  // [tiles] hand-off flags (epoch tags)
+  uint32_t *h_atm_err = nullptr;   // mapped host word: a hand-off wait gave up
+  uint32_t atm_epoch = 0;          // tag of the current run's hand-offs
   double *d_atm_w = nullptr;
   std::vector<AtmosField> atm_fields;
   double *atm_shared = nullptr;
@@ -262,6 +265,8 @@ extern "C" int fcx_destroy(fcx_engine *e) {
   (void)hipFree(e->d_atm_row);
   (void)hipFree(e->d_atm_idx);
   (void)hipFree(e->d_atm_carry);
+  (void)hipFree(e->d_atm_flag);
+  if (e->h_atm_err) (void)hipHostFree(e->h_atm_err);
   (void)hipFree(e->d_atm_col);
   (void)hipFree(e->d_atm_w);
   (void)hipFree(e->atm_pool);
@@ -586,6 +591,8 @@ static void plan_fused_atmos(fcx_engine *e, Plan &pl, uint32_t stages, int phase
   af.idx = e->d_atm_idx;
   af.w = e->d_atm_w;
   af.carry = e->d_atm_carry;
+  af.flag = e->d_atm_flag;
+  if (e->h_atm_err && hipHostGetDevicePointer((void **)&af.err, e->h_atm_err, 0) != hipSuccess) af.err = nullptr;
   af.n_atmos = e->n_atmos;
   af.shared = e->atm_shared;
   af.stride = e->atm_stride;
@@ -1100,6 +1107,12 @@ extern "C" int fcx_commit(fcx_engine *e) {
                         hipMemcpyHostToDevice));
       const int64_t tiles = (e->n[0] + kTile - 1) / kTile;
       HIP_TRY(hipMalloc(&e->d_atm_carry, (size_t)std::max<int64_t>(tiles, 1) * kFusedFields * sizeof(double)));
+      HIP_TRY(hipMalloc(&e->d_atm_flag, (size_t)std::max<int64_t>(tiles, 1) * sizeof(uint32_t)));
+      HIP_TRY(hipMemset(e->d_atm_flag, 0, (size_t)std::max<int64_t>(tiles, 1) * sizeof(uint32_t)));
+      if (!e->h_atm_err) {
+        HIP_TRY(hipHostMalloc((void **)&e->h_atm_err, sizeof(uint32_t), hipHostMallocMapped));
+        *e->h_atm_err = 0;
+      }
     }
     if (!e->atm_contiguous) {
       HIP_TRY(hipMalloc(&e->d_atm_col, std::max<size_t>(e->atm_col.size(), 1) * sizeof(int32_t)));
@@ -1182,6 +1195,8 @@ static int copy_bufs(fcx_engine *e, const std::vector<int> &ids, bool h2d) {
   return FCX_OK;
 }
 
+static int check_handoff(fcx_engine *e);
+
 static int launch_plan(fcx_engine *e, Plan *pl, const double *corr_m, int64_t lo = 0, int64_t hi = -1,
                        bool fixup = true) {
   if (pl->host.n_max <= 0) return FCX_OK;
@@ -1199,10 +1214,16 @@ static int launch_plan(fcx_engine *e, Plan *pl, const double *corr_m, int64_t lo
     pl->af.stride = e->atm_stride;
     pl->af.left = e->atm_left;
     pl->af.right = e->atm_right;
+    // carries handed to the next tile's wave inside the launch: only when every wave makes
+    // one trip (no grid-stride cap), so a wave only ever waits on an earlier-dispatched one;
+    // a run's chunk launches share its epoch (lo == 0 starts a run)
+    pl->af.handoff = lc.max_blocks <= 0 && pl->af.err != nullptr;
+    if (lo == 0 && ++e->atm_epoch == 0) e->atm_epoch = 1;
+    pl->af.epoch = e->atm_epoch;
   }
   const int r = launch_cells(&pl->host, pl->dev, corr_m, lc, e->stream, fused ? &pl->af : nullptr);
   if (r) return fail(FCX_E_HIP, "cells_kernel launch: %s", hipGetErrorString((hipError_t)r));
-  if (fused && fixup) {
+  if (fused && fixup && !pl->af.handoff) {
     const int r2 = launch_atmos_fixup(pl->af, pl->host.n_max, e->stream);
     if (r2) return fail(FCX_E_HIP, "atmos_fixup launch: %s", hipGetErrorString((hipError_t)r2));
   }
@@ -1446,7 +1467,7 @@ static int step_pipelined(fcx_engine *e, int phase, int32_t t, Plan *pl) {
   e->timed = e->timing;
   HIP_TRY(hipStreamSynchronize(e->s_out));
   HIP_TRY(hipStreamSynchronize(e->stream));
-  return FCX_OK;
+  return check_handoff(e);
 }
 
 static bool host_bound(const fcx_engine *e, const Plan *pl) {
@@ -1471,10 +1492,20 @@ extern "C" int fcx_step(fcx_engine *e, int phase, int32_t t) {
   return fcx_synchronize(e);
 }
 
+// a fused accumulation whose carry hand-off gave up (a flag that never came) has wrong
+// atmosphere values: report it at the next synchronisation
+static int check_handoff(fcx_engine *e) {
+  if (e->h_atm_err && __atomic_load_n(e->h_atm_err, __ATOMIC_ACQUIRE)) {
+    *e->h_atm_err = 0;
+    return fail(FCX_E_HIP, "fused atmosphere accumulation: a carry hand-off timed out");
+  }
+  return FCX_OK;
+}
+
 extern "C" int fcx_synchronize(fcx_engine *e) {
   if (!e) return fail(FCX_E_ARG, "NULL engine");
   HIP_TRY(hipStreamSynchronize(e->stream));
-  return FCX_OK;
+  return check_handoff(e);
 }
 
 // one reference subroutine: upload what it reads, run, download what it writes

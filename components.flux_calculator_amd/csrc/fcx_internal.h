@@ -117,8 +117,10 @@ int launch_atmos(const AtmosArgs &a, void *stream);
 // Exchange -> atmosphere accumulation fused into the T=1 cells kernel.  The six fluxes it
 // can take from registers, in this order: MEVA HLAT HSEN RBBR UMOM VMOM (out[k] nullptr =
 // not accumulated).  Every 128-cell wave tile sums the segments that start in it;
-// a segment running past the tile end leaves its prefix sum in carry[tile][k] and
-// atmos_fixup_kernel continues it over the next tile's cells in link order.
+// a segment running past the tile end leaves its prefix sum in carry[tile][k], continued
+// over the next tile's cells in link order either by the wave of that tile (hand-off in the
+// launch: the carry is published with write-through stores and flag[tile] = epoch) or by
+// atmos_fixup_kernel after the launch (launches with a grid-stride cap).
 constexpr int kFusedFields = 6;
 constexpr int kTile = 128;  // cells per wave iteration (64 lanes x 2)
 struct AtmosFused {
@@ -127,6 +129,10 @@ struct AtmosFused {
   double *out[kFusedFields];
   const double *x[kFusedFields];  // the stored outputs (read by the fix-up only)
   double *carry;       // [n_tiles][kFusedFields]
+  uint32_t *flag;      // [n_tiles]: epoch of the run whose carry[tile] is published
+  uint32_t *err;       // set when a hand-off wait gave up (never in a correct run)
+  uint32_t epoch;      // this run's tag (never 0); the flags start at 0
+  int32_t handoff;     // 1: carries handed to the next tile's wave inside the launch
   int64_t n_atmos;
   double *shared;
   int32_t stride, left, right;

@@ -506,6 +506,58 @@ __device__ __forceinline__ void wave_sync() {
 // lowest set bit index of m, 64 if none
 __device__ __forceinline__ int first_bit(uint64_t m) { return m ? __builtin_ctzll(m) : 64; }
 
+// Where a finished segment sum goes: a segment that continues into the next tile leaves its
+// prefix as the carry of this tile -- published for the next tile's wave (hand-off:
+// write-through agent-scope stores, then once they have completed flag[tile] = epoch) or
+// left for atmos_fixup_kernel; a complete one is the atmosphere value (and the boundary
+// slot of a first/last atmosphere cell shared with a neighbour rank).
+__device__ __forceinline__ void segment_done(const AtmosFused &af, int64_t tile, int32_t a, const double *acc,
+                                             bool cont) {
+  if (cont) {
+#pragma unroll
+    for (int k = 0; k < kFusedFields; ++k) {
+      if (!af.out[k]) continue;
+      if (af.handoff)
+        __hip_atomic_store(af.carry + tile * kFusedFields + k, acc[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else
+        af.carry[tile * kFusedFields + k] = acc[k];
+    }
+    if (af.handoff) {
+      __builtin_amdgcn_s_waitcnt(0);  // the carry stores have completed before the flag is set
+      __hip_atomic_store(af.flag + tile, af.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return;
+  }
+#pragma unroll
+  for (int k = 0; k < kFusedFields; ++k) {
+    if (!af.out[k]) continue;
+    af.out[k][a] = acc[k];
+    if (a == 0 && af.left >= 0) af.shared[(int64_t)af.left * af.stride + k] = acc[k];
+    if (a == af.n_atmos - 1 && af.right >= 0) af.shared[(int64_t)af.right * af.stride + k] = acc[k];
+  }
+}
+
+// The carry of `tile` published with this run's epoch.  Every wait ends: the producer is an
+// earlier tile, so it was dispatched first (one trip per wave: it is resident or done);
+// should a flag never come, the wait gives up after ~2^16 polls and raises af.err.
+__device__ __forceinline__ void take_carry(const AtmosFused &af, int64_t tile, double *acc) {
+  bool ok = false;
+  for (int it = 0; it < (1 << 16); ++it) {
+    if (__hip_atomic_load(af.flag + tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == af.epoch) {
+      ok = true;
+      break;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+  if (!ok) __hip_atomic_store(af.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);  // the carry loads stay behind the flag poll
+#pragma unroll
+  for (int k = 0; k < kFusedFields; ++k)
+    acc[k] = af.out[k] ? __hip_atomic_load(af.carry + tile * kFusedFields + k, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT)
+                       : 0.0;
+}
+
 // blocks per CU the multi-type (RAVG) fused kernel is compiled for: 4 -> <= 128 VGPRs
 #ifndef FCX_RAVG_ATMOS_BLOCKS
 #define FCX_RAVG_ATMOS_BLOCKS 4
@@ -576,18 +628,20 @@ __global__ __launch_bounds__(256, RAVG ? FCX_RAVG_ATMOS_BLOCKS : FCX_T1_ATMOS_BL
 #pragma unroll
         for (int k = 0; k < kFusedFields; ++k) acc[k] = acc[k] + q[k * kRow];
       }
-      const bool cont = end == kTile && next_a == a;
+      segment_done(af, tile, a, acc, end == kTile && next_a == a);
+    }
+    // hand-off: the segment the previous tile carried into this one is continued here, from
+    // its carry over this tile's products of the segment's cells, in link order
+    if (af.handoff && lane == 0 && a0 >= 0 && a0 == prev_tile) {
+      const int end = min(min(2 * first_bit(m0), 2 * first_bit(m1) + 1), kTile);
+      double acc[kFusedFields];
+      take_carry(af, tile - 1, acc);
+      for (int e = 0; e < end; ++e) {
+        const double *q = wp + lds_slot(e);
 #pragma unroll
-      for (int k = 0; k < kFusedFields; ++k) {
-        if (!af.out[k]) continue;
-        if (cont) {
-          af.carry[tile * kFusedFields + k] = acc[k];
-        } else {
-          af.out[k][a] = acc[k];
-          if (a == 0 && af.left >= 0) af.shared[(int64_t)af.left * af.stride + k] = acc[k];
-          if (a == af.n_atmos - 1 && af.right >= 0) af.shared[(int64_t)af.right * af.stride + k] = acc[k];
-        }
+        for (int k = 0; k < kFusedFields; ++k) acc[k] = acc[k] + q[k * kRow];
       }
+      segment_done(af, tile, a0, acc, end == kTile && next_a == a0);
     }
     wave_sync();  // every lane is done reading before the next tile overwrites the region
   }

@@ -46,7 +46,7 @@ def shard_case(full, lo, hi, variant, seed=911):
     return case
 
 
-def make_engine(case, la, shared, stride, device="cuda:0", fused=True):
+def make_engine(case, la, shared, stride, device="cuda:0", fused=True, options=None):
     import torch
     from fcx.engine import Engine
 
@@ -55,9 +55,61 @@ def make_engine(case, la, shared, stride, device="cuda:0", fused=True):
     atmos = {"local": la, "fields": [(2, 1, g, name, outs[name]) for name, g in FIELDS],
              "shared": (shared, stride) if shared is not None else None}
     # specialize=0 turns the T=1 kernels (and with them the fused accumulation) off
-    eng = Engine(case.lf, 1, case.methods, corrections=case.corrections, atmos=atmos,
-                 options=None if fused else {"specialize": 0})
+    opts = dict(options or {})
+    if not fused:
+        opts["specialize"] = 0
+    eng = Engine(case.lf, 1, case.methods, corrections=case.corrections, atmos=atmos, options=opts or None)
     return eng, outs
+
+
+def random_run_map(n, lengths, seed):
+    """An atmosphere map with the given run-length range (exchange cells per atmosphere
+    cell), ordered by atmosphere cell, normalised weights."""
+    from fcx.parallel import AtmosMap
+
+    rng = np.random.default_rng(seed)
+    runs = rng.integers(lengths[0], lengths[1] + 1, n)
+    ends = np.cumsum(runs)
+    n_atmos = int(np.searchsorted(ends, n, side="left")) + 1
+    idx = np.repeat(np.arange(n_atmos, dtype=np.int32), runs[:n_atmos])[:n]
+    area = rng.uniform(0.5, 1.5, n)
+    w = area / np.bincount(idx, weights=area, minlength=n_atmos)[idx]
+    return AtmosMap(np.ascontiguousarray(idx, dtype=np.int32), np.ascontiguousarray(w), n_atmos)
+
+
+# run lengths: within a tile, every boundary crossed (130..140 > one 128-cell tile: carries
+# handed across several tiles in a chain), mixed 1..400
+@pytest.mark.parametrize("lengths", [(1, 7), (130, 140), (1, 400)])
+@pytest.mark.parametrize("mode", ["handoff", "capped", "pipelined"])
+def test_fused_accumulation_long_segments(lengths, mode):
+    """The fused accumulation with segments crossing one or several 128-cell wave tiles:
+    carries handed to the next tile's wave inside the launch (default one-trip grid), left
+    to the fix-up kernel (a grid-stride cap), and across the chunk launches of the pipelined
+    host step.  Bit-identical to the sequential sum of the GPU's own fluxes."""
+    import torch
+    from fcx.engine import Engine
+    from fcx.parallel import local_atmos
+
+    n = 300_001 if mode == "pipelined" else 70_001
+    case = build_case("CCLM", n=n, T=1, bias=True, seed=17)
+    amap = random_run_map(n, lengths, seed=lengths[1])
+    la = local_atmos(amap, 0, 1)
+    outs = {name: torch.full((la.n_atmos,), float("nan"), dtype=torch.float64, device="cuda:0")
+            for name, _ in FIELDS}
+    atmos = {"local": la, "fields": [(2, 1, g, name, outs[name]) for name, g in FIELDS]}
+    opts = {"handoff": {}, "capped": {"max_blocks": 64},
+            "pipelined": {"pipeline_chunks": 4, "pipeline_min_chunk": 65536, "zero_copy": 0}}[mode]
+    eng = Engine(case.lf, 1, case.methods, corrections=case.corrections, atmos=atmos, options=opts)
+    for step in range(3):  # the epochs of later runs must not see stale flags
+        for o in outs.values():
+            o.fill_(float("nan"))
+        eng.step(PHASE_ALL, 3600 * step)
+        torch.cuda.synchronize()
+        for name, g in FIELDS:
+            gpu_flux = np.asarray(case.lf.field[(1, g, name)])
+            want = oracle_lib.atmos_accumulate(amap.atmos_index, amap.weight, gpu_flux, amap.n_atmos)
+            np.testing.assert_array_equal(outs[name].cpu().numpy(), want, err_msg=f"{name} step {step}")
+    eng.close()
 
 
 @pytest.mark.parametrize("fused", [True, False])
