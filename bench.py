@@ -336,7 +336,7 @@ def main():
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": (f"cells_atmos_kernel[{variants[dom]}]+atmos_fixup" if la is not None
+            "kernel": (f"cells_atmos_kernel[{variants[dom]}]" if la is not None
                        else f"cells_kernel[{variants[dom]}]"),
             "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBS,

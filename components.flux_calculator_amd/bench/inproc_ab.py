@@ -1,0 +1,120 @@
+#!/usr/bin/env python3
+"""A/B of libfcx builds in ONE process over the SAME device arrays (measurement tool).
+
+Physical placement of the field arrays moves the HBM rate of a many-stream kernel by up to
+~10 % from one allocation to the next (profiles/r01/alloc_probe.txt), which swamps small
+kernel differences between separate bench runs.  Here every build's engines are bound to
+the same LocalFields (inputs, outputs, atmosphere map and outputs), and the builds take
+turns, step by step, so they see the same placement and the same clock state.
+
+  FCX_LIBRARY is the reference build (load()); the others come from --lib NAME=PATH.
+  python inproc_ab.py --lib ho=ab/ho/libfcx.so --lib triv=ab/triv/libfcx.so [--types 1]
+
+Output: one JSON object, per build the mean step time and per-variant kernel times and
+GB/s (algorithmic bytes, bench.py's definition).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.join(ROOT, "components.flux_calculator_amd", "python"))
+
+VARIANTS = ("CCLM", "MOM5", "RCO")
+FIELDS = (("MEVA", 1), ("HLAT", 1), ("HSEN", 1), ("RBBR", 1), ("UMOM", 2), ("VMOM", 3))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--lib", action="append", default=[], help="NAME=PATH of another build")
+    ap.add_argument("--cells", type=int, default=10_000_000)
+    ap.add_argument("--types", type=int, default=1)
+    ap.add_argument("--rounds", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=40, help="steps per build and round")
+    ap.add_argument("--warmup", type=int, default=100)
+    ap.add_argument("--variants", default=",".join(VARIANTS))
+    a = ap.parse_args()
+
+    import torch
+    from fcx import _lib
+    from fcx.basic import PHASE_ALL, PHASE_NORMAL
+    from fcx.engine import Engine
+    from fcx.parallel import PeriodicAtmosMap
+    from fcx.synthetic import build_case, inputs_for_bench
+
+    libs = {"ref": None}
+    for spec in a.lib:
+        name, path = spec.split("=", 1)
+        libs[name] = _lib.load_path(path)
+    variants = [v for v in a.variants.split(",") if v]
+    n = a.cells
+    dev = torch.device("cuda", 0)
+    host = inputs_for_bench(n)
+    data = {k: torch.as_tensor(v).to(dev) for k, v in host.items()}
+    del host
+    stream = torch.cuda.current_stream(dev)
+    la = PeriodicAtmosMap().local(0, n, 0, 1, n)
+    cases, outs = [], []
+    for v in variants:
+        cases.append(build_case(v, n=n, T=a.types, device=dev, data=data if a.types == 1 else None))
+        outs.append({name: torch.empty(max(la.n_atmos, 1), dtype=torch.float64, device=dev)
+                     for name, _ in FIELDS})
+    s0 = 0 if a.types >= 2 else 1
+    engines = {}
+    for lname, lib in libs.items():
+        engines[lname] = [
+            Engine(c.lf, c.num_surface_types, c.methods, corrections=c.corrections, averages=c.averages,
+                   device=0, stream=stream.cuda_stream,
+                   atmos={"local": la, "fields": [(PHASE_NORMAL, s0, g, name, o[name]) for name, g in FIELDS]},
+                   options={"atmos_in_run": 0, "timing": 0}, lib=lib)
+            for c, o in zip(cases, outs)]
+    alg = [engines["ref"][i].algorithmic_bytes(PHASE_ALL) for i in range(len(variants))]
+
+    def step(es, t, ev=None):
+        for i, e in enumerate(es):
+            if ev is not None:
+                ev[i][0].record(stream)
+            e.run(PHASE_ALL, t)
+            if ev is not None:
+                ev[i][1].record(stream)
+
+    names = list(libs)
+    for w in range(a.warmup):
+        for lname in names:
+            step(engines[lname], w * 3600)
+    torch.cuda.synchronize()
+    kern = {k: [] for k in names}
+    wall = {k: [] for k in names}
+    for r in range(a.rounds):
+        order = names[r % len(names):] + names[: r % len(names)]  # rotate who goes first
+        for lname in order:
+            ev = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                   for _ in variants] for _ in range(a.steps)]
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for k in range(a.steps):
+                step(engines[lname], k * 3600, ev[k])
+            torch.cuda.synchronize()
+            wall[lname].append((time.perf_counter() - t0) / a.steps * 1e3)
+            kern[lname].append([[x.elapsed_time(y) for x, y in row] for row in ev])
+    out = {"cells": n, "types": a.types, "rounds": a.rounds, "steps": a.steps, "builds": {}}
+    for lname in names:
+        km = np.array(kern[lname]).reshape(-1, len(variants)).mean(axis=0)
+        out["builds"][lname] = {
+            "ms_per_step": round(float(np.mean(wall[lname])), 4),
+            "ms_per_step_rounds": [round(x, 4) for x in wall[lname]],
+            "kernels": {v: {"ms": round(float(km[i]), 4), "GBps": round(alg[i] / (km[i] * 1e-3) / 1e9, 1)}
+                        for i, v in enumerate(variants)},
+        }
+    for es in engines.values():
+        for e in es:
+            e.close()
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()

@@ -8,6 +8,9 @@
 
 #include <cstdio>
 #include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <initializer_list>
 
 #define CHECK(x)                                                                           \
   do {                                                                                     \
@@ -95,33 +98,55 @@ int measure(const char *label, double *const *arr, long n) {
   return 0;
 }
 
-int main() {
+int main(int argc, char **argv) {
   const long n = 10'000'000;
   const size_t bytes = n * sizeof(double);
   const size_t two_mb = 2u << 20;
   const int A = 31;
+  const int rounds = argc > 1 ? atoi(argv[1]) : 1;
+  if (argc > 2 && !strcmp(argv[2], "alloc")) {  // fresh sets of separate allocations
+    for (int set = 0; set < rounds; ++set) {
+      double *arr[A];
+      void *pad = nullptr;
+      if (set % 2) CHECK(hipMalloc(&pad, (size_t)(set * 37 + 1) << 20));  // shift the next VAs
+      for (int i = 0; i < A; ++i) {
+        CHECK(hipMalloc(&arr[i], bytes));
+        CHECK(hipMemset(arr[i], 0, bytes));
+      }
+      printf("set %d: VA of array 0 %p, deltas (MiB):", set, (void *)arr[0]);
+      for (int i = 1; i < 6; ++i) printf(" %.2f", ((char *)arr[i] - (char *)arr[i - 1]) / 1048576.0);
+      printf("\n");
+      char label[64];
+      snprintf(label, sizeof label, "separate, set %d", set);
+      if (measure(label, arr, n)) return 1;
+      for (int i = 0; i < A; ++i) CHECK(hipFree(arr[i]));
+      if (pad) CHECK(hipFree(pad));
+    }
+    return 0;
+  }
   double *sep[A];
   for (int i = 0; i < A; ++i) {
     CHECK(hipMalloc(&sep[i], bytes));
     CHECK(hipMemset(sep[i], 0, bytes));
   }
-  if (measure("separate hipMalloc", sep, n)) return 1;
-  for (int i = 0; i < A; ++i) CHECK(hipFree(sep[i]));
-
   const size_t rounded = (bytes + two_mb - 1) / two_mb * two_mb;
-  const size_t staggers[] = {0, 256, 1024, 4096, 8192, 65536, 2u << 20, 4352, 3u << 20};
   char *pool;
   const size_t pool_bytes = A * (rounded + (4u << 20)) + (8u << 20);
   CHECK(hipMalloc(&pool, pool_bytes));
   CHECK(hipMemset(pool, 0, pool_bytes));
-  for (size_t s : staggers) {
-    double *arr[A];
-    for (int i = 0; i < A; ++i) arr[i] = reinterpret_cast<double *>(pool + i * rounded + i * s);
-    char label[64];
-    snprintf(label, sizeof label, "pool, stagger %zu B", s);
-    if (measure(label, arr, n)) return 1;
+  const size_t staggers[] = {0, 256, 1024, 4096, 8192, 65536, 2u << 20, 4352, 3u << 20};
+  for (int r = 0; r < rounds; ++r) {
+    if (measure("separate hipMalloc", sep, n)) return 1;
+    for (size_t s : (rounds > 1 ? std::initializer_list<size_t>{0, 65536} : std::initializer_list<size_t>{0, 256, 1024, 4096, 8192, 65536, 2u << 20, 4352, 3u << 20})) {
+      double *arr[A];
+      for (int i = 0; i < A; ++i) arr[i] = reinterpret_cast<double *>(pool + i * rounded + i * s);
+      char label[64];
+      snprintf(label, sizeof label, "pool, stagger %zu B", s);
+      if (measure(label, arr, n)) return 1;
+    }
   }
-  {  // power-of-two strides: 128 MiB apart (worst case for address bits alike)
+  (void)staggers;
+  if (rounds == 1) {  // power-of-two strides: 128 MiB apart (worst case for address bits alike)
     char *pool2;
     const size_t p2 = size_t(128) << 20;
     CHECK(hipMalloc(&pool2, A * p2));
@@ -133,5 +158,6 @@ int main() {
     CHECK(hipFree(pool2));
   }
   CHECK(hipFree(pool));
+  for (int i = 0; i < A; ++i) CHECK(hipFree(sep[i]));
   return 0;
 }

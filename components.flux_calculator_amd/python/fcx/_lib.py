@@ -112,6 +112,18 @@ def load():
     return _lib
 
 
+def load_path(path):
+    """A second libfcx build (A/B measurement tools: engines of two builds in one process
+    over the same arrays).  The process's own library is still load()'s."""
+    load()
+    lib = ctypes.CDLL(os.path.abspath(path))
+    for name, res, args in SIGNATURES:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
 def check(status):
     if status != FCX_OK:
         raise FcxError(status, load().fcx_last_error().decode(errors="replace"))

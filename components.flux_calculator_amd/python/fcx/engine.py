@@ -18,15 +18,17 @@ class Engine:
     """
 
     def __init__(self, lf: LocalFields, num_surface_types, methods, corrections=None,
-                 averages=(), regrid=None, device=0, stream=None, atmos=None, options=None, remaps=None):
+                 averages=(), regrid=None, device=0, stream=None, atmos=None, options=None, remaps=None,
+                 lib=None):
         """atmos: exchange -> atmosphere accumulation, dict with
              local   : fcx.parallel.LocalAtmos of this rank
              fields  : [(phase, surface_type, grid, name, out_array[n_atmos])]
              shared  : optional (device_buffer[n_boundaries * stride], stride)
         remaps: exchange -> model remaps, each {"n_dst", "src", "dst", "w" (0-based links),
                  "fields": [(phase, surface_type, grid, name, out_array[n_dst])]}
-        options: {name: value} for fcx_set_option."""
-        self.lib = _lib.load()
+        options: {name: value} for fcx_set_option.
+        lib: another libfcx build from _lib.load_path (A/B measurement tools only)."""
+        self.lib = lib if lib is not None else _lib.load()
         self.lf = lf
         self.T = int(num_surface_types)
         self.methods = {k: list(v) for k, v in methods.items()}
