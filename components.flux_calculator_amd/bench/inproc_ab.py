@@ -30,13 +30,16 @@ FIELDS = (("MEVA", 1), ("HLAT", 1), ("HSEN", 1), ("RBBR", 1), ("UMOM", 2), ("VMO
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--lib", action="append", default=[], help="NAME=PATH of another build")
+    ap.add_argument("--lib", action="append", default=[],
+                    help="NAME=PATH[:atmos0] of another build (PATH 'ref': the main build; "
+                         ":atmos0 = that build's engines without the accumulation)")
     ap.add_argument("--cells", type=int, default=10_000_000)
     ap.add_argument("--types", type=int, default=1)
     ap.add_argument("--rounds", type=int, default=10)
     ap.add_argument("--steps", type=int, default=40, help="steps per build and round")
     ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--variants", default=",".join(VARIANTS))
+    ap.add_argument("--atmos", type=int, default=1, help="0: flux pass only (no accumulation)")
     a = ap.parse_args()
 
     import torch
@@ -46,10 +49,13 @@ def main():
     from fcx.parallel import PeriodicAtmosMap
     from fcx.synthetic import build_case, inputs_for_bench
 
-    libs = {"ref": None}
+    libs, no_atmos = {"ref": None}, set()
     for spec in a.lib:
         name, path = spec.split("=", 1)
-        libs[name] = _lib.load_path(path)
+        if path.endswith(":atmos0"):
+            path = path[: -len(":atmos0")]
+            no_atmos.add(name)
+        libs[name] = None if path == "ref" else _lib.load_path(path)
     variants = [v for v in a.variants.split(",") if v]
     n = a.cells
     dev = torch.device("cuda", 0)
@@ -69,10 +75,11 @@ def main():
         engines[lname] = [
             Engine(c.lf, c.num_surface_types, c.methods, corrections=c.corrections, averages=c.averages,
                    device=0, stream=stream.cuda_stream,
-                   atmos={"local": la, "fields": [(PHASE_NORMAL, s0, g, name, o[name]) for name, g in FIELDS]},
+                   atmos=({"local": la, "fields": [(PHASE_NORMAL, s0, g, name, o[name]) for name, g in FIELDS]}
+                          if a.atmos and lname not in no_atmos else None),
                    options={"atmos_in_run": 0, "timing": 0}, lib=lib)
             for c, o in zip(cases, outs)]
-    alg = [engines["ref"][i].algorithmic_bytes(PHASE_ALL) for i in range(len(variants))]
+    alg = {k: [es[i].algorithmic_bytes(PHASE_ALL) for i in range(len(variants))] for k, es in engines.items()}
 
     def step(es, t, ev=None):
         for i, e in enumerate(es):
@@ -101,13 +108,13 @@ def main():
             torch.cuda.synchronize()
             wall[lname].append((time.perf_counter() - t0) / a.steps * 1e3)
             kern[lname].append([[x.elapsed_time(y) for x, y in row] for row in ev])
-    out = {"cells": n, "types": a.types, "rounds": a.rounds, "steps": a.steps, "builds": {}}
+    out = {"cells": n, "types": a.types, "atmos": a.atmos, "rounds": a.rounds, "steps": a.steps, "builds": {}}
     for lname in names:
         km = np.array(kern[lname]).reshape(-1, len(variants)).mean(axis=0)
         out["builds"][lname] = {
             "ms_per_step": round(float(np.mean(wall[lname])), 4),
             "ms_per_step_rounds": [round(x, 4) for x in wall[lname]],
-            "kernels": {v: {"ms": round(float(km[i]), 4), "GBps": round(alg[i] / (km[i] * 1e-3) / 1e9, 1)}
+            "kernels": {v: {"ms": round(float(km[i]), 4), "GBps": round(alg[lname][i] / (km[i] * 1e-3) / 1e9, 1)}
                         for i, v in enumerate(variants)},
         }
     for es in engines.values():

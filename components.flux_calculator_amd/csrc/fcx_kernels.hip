@@ -492,6 +492,10 @@ struct LdsEmit {
   int s;      // lds_slot(2 * lane)
   template <int C, class R>
   __device__ __forceinline__ void operator()(int k, const Vec<C, R> &x) const {
+#ifndef FCX_DBG_ATM_NOLDS  // A/B measurement builds only: no LDS products (sums of garbage)
+#define FCX_DBG_ATM_NOLDS 0
+#endif
+    if (FCX_DBG_ATM_NOLDS) return;
     const d2 q = {w0 * x.v[0], w1 * x.v[1]};  // one 16-B LDS store per field
     *reinterpret_cast<d2 *>(p + k * kRow + s) = q;
   }
@@ -505,6 +509,21 @@ __device__ __forceinline__ void wave_sync() {
 
 // lowest set bit index of m, 64 if none
 __device__ __forceinline__ int first_bit(uint64_t m) { return m ? __builtin_ctzll(m) : 64; }
+
+// XCD-aware block order.  Workgroups are dispatched round-robin over the 8 XCDs (block b on
+// XCD b % 8), each XCD with its own L2.  Neighbouring tiles share the 128-B lines of the
+// atmosphere outputs their segments end in; mapped to the same XCD, the two partial lines
+// merge in that L2 before write-back instead of reaching memory as two partial writes.  So
+// XCD x takes one contiguous run of the blocks: b -> x * (nb / 8) + min(x, nb % 8) + b / 8.
+#ifndef FCX_XCD_MAP
+#define FCX_XCD_MAP 1
+#endif
+constexpr uint32_t kXcds = 8;
+__device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb) {
+  if (!FCX_XCD_MAP) return b;
+  const uint32_t x = b % kXcds, q = nb / kXcds, r = nb % kXcds;
+  return x * q + min(x, r) + b / kXcds;
+}
 
 // Where a finished segment sum goes: a segment that continues into the next tile leaves its
 // prefix as the carry of this tile -- published for the next tile's wave (hand-off:
@@ -528,6 +547,10 @@ __device__ __forceinline__ void segment_done(const AtmosFused &af, int64_t tile,
     }
     return;
   }
+#ifndef FCX_DBG_ATM_NOSTORE  // A/B measurement builds only: drop the atmosphere stores
+#define FCX_DBG_ATM_NOSTORE 0
+#endif
+  if (FCX_DBG_ATM_NOSTORE) return;
 #pragma unroll
   for (int k = 0; k < kFusedFields; ++k) {
     if (!af.out[k]) continue;
@@ -537,12 +560,14 @@ __device__ __forceinline__ void segment_done(const AtmosFused &af, int64_t tile,
   }
 }
 
-// The carry of `tile` published with this run's epoch.  Every wait ends: the producer is an
-// earlier tile, so it was dispatched first (one trip per wave: it is resident or done);
-// should a flag never come, the wait gives up after ~2^16 polls and raises af.err.
+// The carry of `tile` published with this run's epoch.  Every wait ends: the producer of
+// tile - 1 is the previous block of the same XCD run (dispatched 8 blocks earlier, resident
+// or done) or, for the first tile of an XCD run, the last block of the previous run, which
+// the dispatcher reaches because at most 7 such waves wait at any time.  Should a flag never
+// come, the wait gives up after ~2^20 polls (about a second) and raises af.err.
 __device__ __forceinline__ void take_carry(const AtmosFused &af, int64_t tile, double *acc) {
   bool ok = false;
-  for (int it = 0; it < (1 << 16); ++it) {
+  for (int it = 0; it < (1 << 20); ++it) {
     if (__hip_atomic_load(af.flag + tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == af.epoch) {
       ok = true;
       break;
@@ -579,7 +604,7 @@ __global__ __launch_bounds__(256, RAVG ? FCX_RAVG_ATMOS_BLOCKS : FCX_T1_ATMOS_BL
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   double *wp = s_p[wv];
   const int64_t waves = (int64_t)gridDim.x * (blockDim.x >> 6);
-  const int64_t wave0 = (int64_t)blockIdx.x * (blockDim.x >> 6) + wv;
+  const int64_t wave0 = (int64_t)xcd_block(blockIdx.x, gridDim.x) * (blockDim.x >> 6) + wv;
   const uint64_t at_or_above = ~0ull << lane;
   const uint64_t above = lane == 63 ? 0ull : (~0ull << (lane + 1));
   for (int64_t tile = lo / kTile + wave0; tile < n_tiles; tile += waves) {
