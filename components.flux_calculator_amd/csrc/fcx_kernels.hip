@@ -551,10 +551,16 @@ __device__ __forceinline__ void segment_done(const AtmosFused &af, int64_t tile,
 #define FCX_DBG_ATM_NOSTORE 0
 #endif
   if (FCX_DBG_ATM_NOSTORE) return;
+#ifndef FCX_ATM_NT_STORE  // A/B: non-temporal atmosphere stores
+#define FCX_ATM_NT_STORE 0
+#endif
 #pragma unroll
   for (int k = 0; k < kFusedFields; ++k) {
     if (!af.out[k]) continue;
-    af.out[k][a] = acc[k];
+    if (FCX_ATM_NT_STORE)
+      __builtin_nontemporal_store(acc[k], af.out[k] + a);
+    else
+      af.out[k][a] = acc[k];
     if (a == 0 && af.left >= 0) af.shared[(int64_t)af.left * af.stride + k] = acc[k];
     if (a == af.n_atmos - 1 && af.right >= 0) af.shared[(int64_t)af.right * af.stride + k] = acc[k];
   }
@@ -721,7 +727,10 @@ __global__ __launch_bounds__(256) void regrid_csr_kernel(const int32_t *__restri
 // products w*x per field, then every lane adds the products of its own segment in link
 // order.  acc = acc + w*x from 0.0 in increasing link order is exactly the sequential
 // weight application, so the result is bit-identical to it (no atomics, no tree order).
-constexpr int kAtmChunk = 512;
+#ifndef FCX_ATM_CHUNK
+#define FCX_ATM_CHUNK 512
+#endif
+constexpr int kAtmChunk = FCX_ATM_CHUNK;
 
 __global__ __launch_bounds__(256) void atmos_kernel(const AtmosArgs a) {
   extern __shared__ double lds[];  // [nf][kAtmChunk] products
