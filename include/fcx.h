@@ -128,6 +128,9 @@ int fcx_run(fcx_engine *e, int phase, int32_t current_step_time); /* device comp
 int fcx_download(fcx_engine *e, int phase); /* D2H of host-bound outputs of the phase */
 /* the three above; with host-bound fields pipelined over cell chunks (FCX_OPT_PIPELINE_CHUNKS) */
 int fcx_step(fcx_engine *e, int phase, int32_t current_step_time);
+/* waits for the engine's stream.  Also reports (FCX_E_HIP) a fused accumulation whose
+ * in-launch carry hand-off timed out since the last check -- never in a correct run, but
+ * the atmosphere values of that run would be wrong; fcx_step checks the same. */
 int fcx_synchronize(fcx_engine *e);
 
 /* ---- per call: the reference subroutines one by one (exact drop-in semantics; each
