@@ -60,7 +60,8 @@ def parse():
     p.add_argument("--max-blocks", type=int, default=None,
                    help="A/B only: FCX_OPT_MAX_BLOCKS of every engine (default: the engine's)")
     p.add_argument("--precision", choices=("f64", "f32"), default="f64",
-                   help="f32: the fp32 cell-pass variant (config 5; no atmosphere accumulation)")
+                   help="f32: the fp32 variant (config 5): fp32 cell pass, then the accumulation as "
+                        "its own kernel (fp32 fluxes in, fp64 weights and sums, fp32 outputs)")
     return p.parse_args()
 
 
@@ -184,8 +185,6 @@ def main():
     from pmc_traffic import traffic_key
 
     f32 = args.precision == "f32"
-    if f32:
-        args.atmos = 0  # the accumulation runs in fp64 only (fcx.h fcx_set_precision)
 
     # this rank's APPLE range of the global grid (decomp_def.F90:23-31): weak scaling,
     # every rank owns args.cells cells; the seed follows the global offset
@@ -219,7 +218,8 @@ def main():
             c = as_dtype(c, "float32")
         atmos = None
         if la is not None:
-            outs = {name: torch.empty(max(la.n_atmos, 1), dtype=torch.float64, device=dev)
+            outs = {name: torch.empty(max(la.n_atmos, 1), dtype=torch.float32 if f32 else torch.float64,
+                                      device=dev)
                     for name, _ in atm_fields}
             atm_outs.append(outs)
             # OASIS sends the type-0 fields ('S A xxxx 00'): with several surface types those
@@ -298,7 +298,8 @@ def main():
     if os.path.exists(tfile):
         try:
             t = json.load(open(tfile))
-            traffic = t.get(traffic_key(variants[dom], n, args.types, args.bias, la is not None,
+            # the timed launch carries the accumulation only when it is fused (fp64)
+            traffic = t.get(traffic_key(variants[dom], n, args.types, args.bias, la is not None and not f32,
                                         args.precision))
         except Exception:
             traffic = None
@@ -320,6 +321,7 @@ def main():
             "workload": ("config3/4: synthetic exchange grid, CCLM+MOM5+RCO fused flux kernels "
                          "back-to-back per coupling step"
                          + (" + exchange->atmosphere accumulation" if la is not None else "")
+                         + (" (its own kernel after the flux pass)" if la is not None and f32 else "")
                          + (", fp32 variant (config 5)" if f32 else "") + ", inputs HBM-resident"),
             "cells_per_gpu": n,
             "cells_global": n_global,
@@ -336,7 +338,7 @@ def main():
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": (f"cells_atmos_kernel[{variants[dom]}]" if la is not None
+            "kernel": (f"cells_atmos_kernel[{variants[dom]}]" if la is not None and not f32
                        else f"cells_kernel[{variants[dom]}]"),
             "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBS,

@@ -551,8 +551,11 @@ static bool merge_ok(const fcx_engine *e) {
 // the phase is one of the six fluxes that launch holds in registers (AtmosFused order).
 static void plan_fused_atmos(fcx_engine *e, Plan &pl, uint32_t stages, int phase) {
   pl.atm_fused = false;
+  // (segments longer than half a tile, several hundred exchange cells per atmosphere cell,
+  // go to atmos_kernel: one lane summing a long segment would hold up its whole wave; the
+  // fp32 engine uses atmos_kernel too)
   if (!pl.variant || !e->d_atm_idx || e->atm_maxseg > kTile / 2 || e->any_regrid || phase <= 0 ||
-      phase >= 1000 || !e->specialize)
+      phase >= 1000 || !e->specialize || e->f32)
     return;
   const TypeParams &tp = pl.host.type[0];
   AtmosFused af{};
@@ -961,10 +964,10 @@ static void pin_host_arrays(fcx_engine *e) {
   for (auto &bf : e->bufs)
     if (!bf.external) add(bf.host, (size_t)bf.n * e->esize);
   for (auto &f : e->atm_fields)
-    if (!f.external) add(f.out_host, (size_t)std::max<int64_t>(e->n_atmos, 0) * sizeof(double));
+    if (!f.external) add(f.out_host, (size_t)std::max<int64_t>(e->n_atmos, 0) * e->esize);
   for (auto &rm : e->remaps)
     for (auto &f : rm.fields)
-      if (!f.external) add(f.out_host, (size_t)rm.n_dst * sizeof(double));
+      if (!f.external) add(f.out_host, (size_t)rm.n_dst * e->esize);
   std::sort(r.begin(), r.end());
   const uintptr_t sh = page_shift();
   std::vector<std::pair<uintptr_t, uintptr_t>> m;
@@ -1045,12 +1048,6 @@ extern "C" int fcx_commit(fcx_engine *e) {
   if (!e) return fail(FCX_E_ARG, "NULL engine");
   if (e->committed) return FCX_OK;
   if (int r = validate(e)) return r;
-  if (e->f32) {
-    bool rg = e->any_regrid;
-    for (auto &c : e->rg) rg = rg || c.set;
-    if (rg) return fail(FCX_E_UNSUPPORTED, "fp32 engine: regridding runs in fp64 only");
-    if (e->n_atmos >= 0) return fail(FCX_E_UNSUPPORTED, "fp32 engine: the atmosphere accumulation runs in fp64 only");
-  }
   if (int r = gpu_init(e)) return r;
   // auto: zero-copy exactly where the pipelined step would not apply (grids below two
   // chunks), i.e. where the step is latency-bound and per-array copies dominate it
@@ -1091,7 +1088,12 @@ extern "C" int fcx_commit(fcx_engine *e) {
     HIP_TRY(hipMemcpy(c.d_row, c.row_ptr.data(), c.row_ptr.size() * sizeof(int32_t), hipMemcpyHostToDevice));
     if (!c.col.empty()) {
       HIP_TRY(hipMemcpy(c.d_col, c.col.data(), c.col.size() * sizeof(int32_t), hipMemcpyHostToDevice));
-      HIP_TRY(hipMemcpy(c.d_w, c.w.data(), c.w.size() * sizeof(double), hipMemcpyHostToDevice));
+      if (e->f32) {  // REAL(wp) weights of the single-precision build: rounded once
+        std::vector<float> wf(c.w.begin(), c.w.end());
+        HIP_TRY(hipMemcpy(c.d_w, wf.data(), wf.size() * sizeof(float), hipMemcpyHostToDevice));
+      } else {
+        HIP_TRY(hipMemcpy(c.d_w, c.w.data(), c.w.size() * sizeof(double), hipMemcpyHostToDevice));
+      }
     }
   }
   if (e->n_atmos >= 0) {
@@ -1122,14 +1124,14 @@ extern "C" int fcx_commit(fcx_engine *e) {
     }
     size_t need = 0;
     for (auto &f : e->atm_fields)
-      if (!f.external) need += ((size_t)std::max<int64_t>(e->n_atmos, 1) * sizeof(double) + 255) / 256 * 256;
+      if (!f.external) need += ((size_t)std::max<int64_t>(e->n_atmos, 1) * e->esize + 255) / 256 * 256;
     if (need) {
       HIP_TRY(hipMalloc(&e->atm_pool, need));
       size_t off = 0;
       for (auto &f : e->atm_fields)
         if (!f.external) {
           f.out_dev = reinterpret_cast<double *>((char *)e->atm_pool + off);
-          off += ((size_t)std::max<int64_t>(e->n_atmos, 1) * sizeof(double) + 255) / 256 * 256;
+          off += ((size_t)std::max<int64_t>(e->n_atmos, 1) * e->esize + 255) / 256 * 256;
         }
     }
   }
@@ -1146,7 +1148,7 @@ extern "C" int fcx_commit(fcx_engine *e) {
       HIP_TRY(hipMemcpy(rm.d_col, rm.col.data(), rm.col.size() * sizeof(int32_t), hipMemcpyHostToDevice));
       HIP_TRY(hipMemcpy(rm.d_w, rm.w.data(), rm.w.size() * sizeof(double), hipMemcpyHostToDevice));
     }
-    const size_t one = ((size_t)std::max<int64_t>(rm.n_dst, 1) * sizeof(double) + 255) / 256 * 256;
+    const size_t one = ((size_t)std::max<int64_t>(rm.n_dst, 1) * e->esize + 255) / 256 * 256;
     size_t need = 0;
     for (auto &f : rm.fields) need += f.external ? 0 : one;
     if (need) {
@@ -1208,7 +1210,7 @@ static int launch_plan(fcx_engine *e, Plan *pl, const double *corr_m, int64_t lo
   lc.variant = (e->specialize && lc.merged) ? pl->variant : 0;
   lc.f32 = e->f32;
   lc.ravg = pl->host.ravg_on != 0;
-  const bool fused = pl->atm_fused && lc.variant && lc.cells_per_thread == 2;
+  const bool fused = pl->atm_fused && lc.variant && lc.cells_per_thread == 2 && !lc.f32;
   if (fused) {  // the shared-slot pointers may have been set after the plan was built
     pl->af.shared = e->atm_shared;
     pl->af.stride = e->atm_stride;
@@ -1273,7 +1275,7 @@ extern "C" int fcx_download(fcx_engine *e, int phase) {
   if (int r = copy_bufs(e, pl->writes, false)) return r;
   for (auto &f : e->atm_fields)
     if ((f.phase & phase) && !f.external && e->n_atmos > 0)
-      HIP_TRY(hipMemcpyAsync(f.out_host, f.out_dev, e->n_atmos * sizeof(double), hipMemcpyDeviceToHost,
+      HIP_TRY(hipMemcpyAsync(f.out_host, f.out_dev, e->n_atmos * e->esize, hipMemcpyDeviceToHost,
                              e->stream));
   if (int r = download_remaps(e, phase, e->stream)) return r;
   if (e->any_regrid) {  // device-side regrid destinations of the fields this phase computes
@@ -1298,6 +1300,7 @@ extern "C" int fcx_download(fcx_engine *e, int phase) {
 
 static AtmosArgs atmos_args(fcx_engine *e, int phase) {
   AtmosArgs a{};
+  a.f32 = e->f32 ? 1 : 0;
   a.row_ptr = e->d_atm_row;
   a.col = e->atm_contiguous ? nullptr : e->d_atm_col;
   a.w = e->d_atm_w;
@@ -1330,6 +1333,7 @@ static int run_atmos(fcx_engine *e, int phase) {
 static int run_remaps(fcx_engine *e, int phase) {
   for (auto &rm : e->remaps) {
     AtmosArgs a{};
+    a.f32 = e->f32 ? 1 : 0;
     a.row_ptr = rm.d_row;
     a.col = rm.d_col;
     a.w = rm.d_w;
@@ -1359,7 +1363,7 @@ static int download_remaps(fcx_engine *e, int phase, hipStream_t s) {
   for (auto &rm : e->remaps)
     for (auto &f : rm.fields)
       if ((f.phase & phase) && !f.external && rm.n_dst > 0)
-        HIP_TRY(hipMemcpyAsync(f.out_host, f.out_dev, rm.n_dst * sizeof(double), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(f.out_host, f.out_dev, rm.n_dst * e->esize, hipMemcpyDeviceToHost, s));
   return FCX_OK;
 }
 
@@ -1460,7 +1464,7 @@ static int step_pipelined(fcx_engine *e, int phase, int32_t t, Plan *pl) {
   if (e->atmos_in_run || e->atm_done_fused)
     for (auto &f : e->atm_fields)
       if ((f.phase & phase) && !f.external && e->n_atmos > 0)
-        HIP_TRY(hipMemcpyAsync(f.out_host, f.out_dev, e->n_atmos * sizeof(double), hipMemcpyDeviceToHost,
+        HIP_TRY(hipMemcpyAsync(f.out_host, f.out_dev, e->n_atmos * e->esize, hipMemcpyDeviceToHost,
                                e->s_out));
   if (int r = download_remaps(e, phase, e->s_out)) return r;
   if (e->timing) HIP_TRY(hipEventRecord(e->ev1, e->s_out));
@@ -1560,11 +1564,10 @@ static int regrid_var(fcx_engine *e, int var, int surface_type) {
       const double *src = e->dptr(s, from_g[k], var);
       if (!dst || !src) return fail(FCX_E_MISSING, "regridding %s: source or destination unbound", kVarNames[var0(var)]);
       if (!c.set) {
-        int r = launch_zero(dst, e->n[to_g[k] - 1], e->stream);
-        if (r) return fail(FCX_E_HIP, "zero: %s", hipGetErrorString((hipError_t)r));
+        HIP_TRY(hipMemsetAsync(dst, 0, (size_t)e->n[to_g[k] - 1] * e->esize, e->stream));
         continue;
       }
-      int r = launch_regrid_csr(c.d_row, c.d_col, c.d_w, src, dst, c.n_dst, e->stream);
+      int r = launch_regrid_csr(c.d_row, c.d_col, c.d_w, src, dst, c.n_dst, e->stream, e->f32);
       if (r) return fail(FCX_E_HIP, "regrid: %s", hipGetErrorString((hipError_t)r));
     }
   }
@@ -1852,7 +1855,6 @@ extern "C" int fcx_add_remap_field(fcx_engine *e, int32_t remap_id, int phase, i
                                    int flags) {
   if (!e) return fail(FCX_E_ARG, "NULL engine");
   if (e->committed) return fail(FCX_E_STATE, "engine already committed");
-  if (e->f32) return fail(FCX_E_UNSUPPORTED, "fp32 engine: remaps run in fp64 only");
   if (remap_id < 0 || remap_id >= (int32_t)e->remaps.size()) return fail(FCX_E_ARG, "remap %d unknown", remap_id);
   if (phase < 1 || phase > 3 || s < 0 || s > kMaxTypes || g < 1 || g > 3 || var < 1 || var > kNumVars || !out)
     return fail(FCX_E_ARG, "bad remap field arguments");

@@ -111,6 +111,8 @@ struct AtmosArgs {
   double *shared;
   const double *x[kMaxAtmosFields];
   double *out[kMaxAtmosFields];
+  int32_t f32;             // fields and outputs are float arrays (fp32 engine); the weights,
+                           // products and sums stay fp64 (OASIS maps in double)
 };
 int launch_atmos(const AtmosArgs &a, void *stream);
 
@@ -140,8 +142,10 @@ struct AtmosFused {
 int launch_atmos_fixup(const AtmosFused &af, int64_t n_cells, void *stream);
 int launch_atmos_finish(const AtmosArgs &a, int32_t n_boundaries, void *stream);
 
+// f32: w, src and dst are float arrays (the reference's single-precision build, where the
+// matrix weights and the fields are REAL(wp) = REAL(4), basic:117-122, and so is the sum)
 int launch_regrid_csr(const int32_t *row_ptr, const int32_t *col, const double *w,
-                      const double *src, double *dst, int64_t n_dst, void *stream);
+                      const double *src, double *dst, int64_t n_dst, void *stream, bool f32 = false);
 int launch_zero(double *x, int64_t n, void *stream);
 
 }  // namespace fcx

@@ -708,14 +708,16 @@ __global__ __launch_bounds__(256) void atmos_fixup_kernel(const AtmosFused af, i
 // do_regridding (basic:463-522) as CSR-by-destination: row d holds the links with
 // dst_index == d in their original link order, so the sequential sum from 0.0 reproduces
 // the reference's scatter-add order exactly (bit-identical) without atomics.
+// R = float: the single-precision build's REAL(4) arithmetic.
+template <class R>
 __global__ __launch_bounds__(256) void regrid_csr_kernel(const int32_t *__restrict__ row_ptr,
                                                          const int32_t *__restrict__ col,
-                                                         const double *__restrict__ w,
-                                                         const double *__restrict__ src,
-                                                         double *__restrict__ dst, int64_t n_dst) {
+                                                         const R *__restrict__ w,
+                                                         const R *__restrict__ src,
+                                                         R *__restrict__ dst, int64_t n_dst) {
   const int64_t d = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (d >= n_dst) return;
-  double acc = 0.0;
+  R acc = R(0);
   for (int32_t k = row_ptr[d]; k < row_ptr[d + 1]; ++k) acc = acc + src[col[k]] * w[k];
   dst[d] = acc;
 }
@@ -732,6 +734,9 @@ __global__ __launch_bounds__(256) void regrid_csr_kernel(const int32_t *__restri
 #endif
 constexpr int kAtmChunk = FCX_ATM_CHUNK;
 
+// R: element type of the fields and outputs (float in the fp32 engine; the weights, the
+// products and the sums are fp64 either way, and an fp32 output is rounded once).
+template <class R>
 __global__ __launch_bounds__(256) void atmos_kernel(const AtmosArgs a) {
   extern __shared__ double lds[];  // [nf][kAtmChunk] products
   const int64_t a0 = (int64_t)blockIdx.x * blockDim.x;
@@ -752,7 +757,7 @@ __global__ __launch_bounds__(256) void atmos_kernel(const AtmosArgs a) {
       const double wk = __builtin_nontemporal_load(a.w + k);
 #pragma unroll
       for (int f = 0; f < kMaxAtmosFields; ++f)
-        if (f < a.nf) lds[f * kAtmChunk + i] = wk * a.x[f][xi];
+        if (f < a.nf) lds[f * kAtmChunk + i] = wk * (double)reinterpret_cast<const R *>(a.x[f])[xi];
     }
     __syncthreads();
     const int32_t lo = max(k_lo, C0), hi = min(k_hi, C0 + len);
@@ -766,7 +771,7 @@ __global__ __launch_bounds__(256) void atmos_kernel(const AtmosArgs a) {
 #pragma unroll
   for (int f = 0; f < kMaxAtmosFields; ++f) {
     if (f >= a.nf) break;
-    a.out[f][c] = acc[f];
+    reinterpret_cast<R *>(a.out[f])[c] = (R)acc[f];
     if (c == 0 && a.left >= 0) a.shared[(int64_t)a.left * a.stride + f] = acc[f];
     if (c == a.n_atmos - 1 && a.right >= 0) a.shared[(int64_t)a.right * a.stride + f] = acc[f];
   }
@@ -774,11 +779,13 @@ __global__ __launch_bounds__(256) void atmos_kernel(const AtmosArgs a) {
 
 // after the all-reduce: completed boundary sums back into the outputs, then every slot of
 // this engine's region is zeroed for the next step (one block)
+template <class R>
 __global__ void atmos_finish_kernel(const AtmosArgs a, int32_t n_boundaries) {
   const int t = threadIdx.x;
   if (t < a.nf) {
-    if (a.left >= 0) a.out[t][0] = a.shared[(int64_t)a.left * a.stride + t];
-    if (a.right >= 0) a.out[t][a.n_atmos - 1] = a.shared[(int64_t)a.right * a.stride + t];
+    R *out = reinterpret_cast<R *>(a.out[t]);
+    if (a.left >= 0) out[0] = (R)a.shared[(int64_t)a.left * a.stride + t];
+    if (a.right >= 0) out[a.n_atmos - 1] = (R)a.shared[(int64_t)a.right * a.stride + t];
   }
   __syncthreads();
   for (int64_t i = t; i < (int64_t)n_boundaries * a.stride; i += blockDim.x) a.shared[i] = 0.0;
@@ -906,11 +913,16 @@ int launch_cells(const Params *hp, const Params *dp, const double *corr_m, const
 }
 
 int launch_regrid_csr(const int32_t *row_ptr, const int32_t *col, const double *w,
-                      const double *src, double *dst, int64_t n_dst, void *stream) {
+                      const double *src, double *dst, int64_t n_dst, void *stream, bool f32) {
   if (n_dst <= 0) return 0;
   const int blocks = (int)((n_dst + 255) / 256);
-  hipLaunchKernelGGL(regrid_csr_kernel, dim3(blocks), dim3(256), 0,
-                     reinterpret_cast<hipStream_t>(stream), row_ptr, col, w, src, dst, n_dst);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (f32)
+    hipLaunchKernelGGL(regrid_csr_kernel<float>, dim3(blocks), dim3(256), 0, s, row_ptr, col,
+                       reinterpret_cast<const float *>(w), reinterpret_cast<const float *>(src),
+                       reinterpret_cast<float *>(dst), n_dst);
+  else
+    hipLaunchKernelGGL(regrid_csr_kernel<double>, dim3(blocks), dim3(256), 0, s, row_ptr, col, w, src, dst, n_dst);
   return (int)hipGetLastError();
 }
 
@@ -918,14 +930,21 @@ int launch_atmos(const AtmosArgs &a, void *stream) {
   if (a.n_atmos <= 0 || a.nf <= 0) return 0;
   const int blocks = (int)((a.n_atmos + 255) / 256);
   const size_t lds = (size_t)a.nf * kAtmChunk * sizeof(double);
-  hipLaunchKernelGGL(atmos_kernel, dim3(blocks), dim3(256), lds, reinterpret_cast<hipStream_t>(stream), a);
+  if (a.f32)
+    hipLaunchKernelGGL(atmos_kernel<float>, dim3(blocks), dim3(256), lds, reinterpret_cast<hipStream_t>(stream), a);
+  else
+    hipLaunchKernelGGL(atmos_kernel<double>, dim3(blocks), dim3(256), lds, reinterpret_cast<hipStream_t>(stream), a);
   return (int)hipGetLastError();
 }
 
 int launch_atmos_finish(const AtmosArgs &a, int32_t n_boundaries, void *stream) {
   if (!a.shared) return 0;
-  hipLaunchKernelGGL(atmos_finish_kernel, dim3(1), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
-                     a, n_boundaries);
+  if (a.f32)
+    hipLaunchKernelGGL(atmos_finish_kernel<float>, dim3(1), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                       a, n_boundaries);
+  else
+    hipLaunchKernelGGL(atmos_finish_kernel<double>, dim3(1), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                       a, n_boundaries);
   return (int)hipGetLastError();
 }
 

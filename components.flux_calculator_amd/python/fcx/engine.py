@@ -84,6 +84,8 @@ class Engine:
                 _lib.check(self.lib.fcx_set_atmos_map(h, la.n_atmos, ctypes.c_void_p(idx.ctypes.data),
                                                       ctypes.c_void_p(w.ctypes.data)))
                 for phase, s, g, name, out in atmos["fields"]:
+                    if dtype_name(out) != dtype:
+                        raise TypeError(f"atmosphere output {name}: {dtype_name(out)} array in a {dtype} engine")
                     flags = _lib.FCX_MEM_DEVICE if is_device(out) else _lib.FCX_MEM_HOST
                     self._keep.append(out)
                     _lib.check(self.lib.fcx_add_atmos_field(h, phase, s, g, IDX[name],
@@ -103,6 +105,8 @@ class Engine:
                                                   ctypes.c_void_p(dst.ctypes.data), ctypes.c_void_p(w.ctypes.data),
                                                   ctypes.byref(rid)))
                 for phase, s, g, name, out in rm["fields"]:
+                    if dtype_name(out) != dtype:
+                        raise TypeError(f"remap output {name}: {dtype_name(out)} array in a {dtype} engine")
                     flags = _lib.FCX_MEM_DEVICE if is_device(out) else _lib.FCX_MEM_HOST
                     self._keep.append(out)
                     _lib.check(self.lib.fcx_add_remap_field(h, rid.value, phase, s, g, IDX[name],

@@ -115,8 +115,12 @@ int fcx_add_average(fcx_engine *e, int phase, int grid, int var);
  * fcx_bind_field / fcx_add_atmos_field / returned by fcx_device_ptr addresses float arrays
  * (the double* parameter type then only carries the address) and the kernels compute in
  * fp32 -- the SURVEY.md 8d config-5 variant, half the HBM bytes per cell.  Corrections are
- * still passed as double and rounded once at commit.  Not with regridding or the
- * atmosphere accumulation (FCX_E_UNSUPPORTED at commit).  Call before fcx_commit. */
+ * still passed as double and rounded once at commit.  do_regridding runs in fp32 with the
+ * matrix weights rounded once (the single-precision build's REAL(wp) arithmetic,
+ * basic:117-122, 463-522).  The atmosphere accumulation and the remaps read the fp32 fields
+ * and write fp32 outputs (fcx_add_atmos_field / fcx_add_remap_field then take float arrays)
+ * but weigh and sum in fp64, as OASIS maps in double; the shared boundary buffer of
+ * fcx_set_atmos_shared stays double.  Call before fcx_commit. */
 enum fcx_precision { FCX_PRECISION_F64 = 0, FCX_PRECISION_F32 = 1 };
 int fcx_set_precision(fcx_engine *e, int precision);
 /* validate (flux_calculator_prepare.F90 rules), allocate device mirrors, build plans */

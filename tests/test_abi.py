@@ -109,23 +109,21 @@ def test_engine_calls_before_commit_fail_cleanly():
     lib.fcx_destroy(h)
 
 
-def test_fp32_engine_refuses_regrid_and_atmosphere_before_any_hip_call():
-    """FCX_PRECISION_F32 covers the cell pass only: regridding and the atmosphere
-    accumulation stay fp64 (FCX_E_UNSUPPORTED at commit, before the device is touched)."""
+def test_fp32_engine_takes_fp32_outputs_only():
+    """The fp32 engine's atmosphere and remap outputs are float arrays (fcx.h
+    fcx_set_precision): a float64 output is refused before any HIP call."""
     from fcx.parallel import local_atmos, synthetic_atmos_map
     from fcx.synthetic import as_dtype
 
     c32 = as_dtype(build_case("CCLM", n=64, T=1), "float32")
     amap = synthetic_atmos_map(64)
-    out = np.zeros(amap.n_atmos)
-    atmos = {"local": local_atmos(amap, 0, 1), "fields": [(2, 1, 1, "MEVA", out)]}
-    with pytest.raises(_lib.FcxError) as ei:
+    atmos = {"local": local_atmos(amap, 0, 1), "fields": [(2, 1, 1, "MEVA", np.zeros(amap.n_atmos))]}
+    with pytest.raises(TypeError):
         Engine(c32.lf, 1, c32.methods, atmos=atmos)
-    assert ei.value.status == 3 and "fp32" in str(ei.value)
-    m = (np.array([1], np.int32), np.array([1], np.int32), np.ones(1))
-    with pytest.raises(_lib.FcxError) as ei:
-        Engine(c32.lf, 1, c32.methods, regrid={"matrices": {0: m}})
-    assert ei.value.status == 3
+    rm = {"n_dst": 4, "src": np.arange(64, dtype=np.int32), "dst": np.arange(64, dtype=np.int32) % 4,
+          "w": np.ones(64), "fields": [(2, 1, 1, "MEVA", np.zeros(4))]}
+    with pytest.raises(TypeError):
+        Engine(c32.lf, 1, c32.methods, remaps=[rm])
 
 
 def test_mixed_precision_bindings_rejected():

@@ -91,3 +91,105 @@ def test_fp32_device_resident_bytes_halved():
     e32.close()
     assert b32 * 2 == b64
     assert torch.isfinite(c32.lf.field[(1, 1, "MEVA")]).all()
+
+
+def regrid_f32(src1, dst1, w, x32, n_dst):
+    """do_regridding (basic:480-487) in the single-precision build's REAL(4) arithmetic:
+    dst = 0; dst(d_k) = dst(d_k) + src(s_k) * w_k in link order (1-based indices)."""
+    out = np.zeros(n_dst, np.float32)
+    w32 = np.asarray(w, np.float32)
+    for k in range(len(w32)):
+        d = int(dst1[k]) - 1
+        out[d] = np.float32(out[d] + np.float32(x32[int(src1[k]) - 1] * w32[k]))
+    return out
+
+
+def test_fp32_regridding_staged():
+    """Staged plan in fp32: QSUR t->u replaces the u-grid QSUR, MEVA t->v.  The regridded
+    arrays are bit-identical to the REAL(4) sequential sum of the GPU's own t-grid values;
+    every output is within the fp32 gate of the fp64 oracle."""
+    rng = np.random.default_rng(7)
+    case = build_case("CCLM", n=600, T=2, bias=False, sep_grids=(550, 520))
+    nt, nu, nv = case.grid_size
+    mats = {}
+    for which, (ns, nd) in {2: (nt, nu), 3: (nt, nv)}.items():
+        nnz = 3 * nd
+        mats[which] = (rng.integers(1, ns + 1, nnz), np.repeat(np.arange(1, nd + 1), 3)[rng.permutation(nnz)],
+                       rng.uniform(0.0, 1.0, nnz))
+    case.regrid = {"matrices": mats}
+    for s in (1, 2):
+        case.methods["which_spec_vapor_surface_u"][s - 1] = "none"
+        case.lf.put_to[(s, 1, "QSUR")] = 2
+        case.lf.put_to[(s, 1, "MEVA")] = 4
+        case.lf.allocate_localvar("MEVA", s, 3, value=np.nan)
+        case.outputs.append((s, 3, "MEVA"))
+    c32 = as_dtype(case, "float32")
+    c64 = as_dtype(c32, "float64")
+    ref = oracle_lib.run_case(c64, "c", current_step_time=STEP_T, regrid=True)
+    eng = Engine(c32.lf, c32.num_surface_types, c32.methods, corrections=c32.corrections,
+                 averages=c32.averages, regrid=c32.regrid)
+    eng.step(1, STEP_T)
+    eng.step(2, STEP_T)
+    eng.close()
+    got = {k: np.array(c32.lf.field[k], dtype=np.float64) for k in c32.outputs}
+    check(got, ref, "fp32 regrid")
+    for s in (1, 2):
+        src, dst, w = mats[2]
+        want = regrid_f32(src, dst, w, np.asarray(c32.lf.field[(s, 1, "QSUR")]), nu)
+        np.testing.assert_array_equal(np.asarray(c32.lf.field[(s, 2, "QSUR")]), want, err_msg=f"QSUR u s={s}")
+        src, dst, w = mats[3]
+        want = regrid_f32(src, dst, w, np.asarray(c32.lf.field[(s, 1, "MEVA")]), nv)
+        np.testing.assert_array_equal(np.asarray(c32.lf.field[(s, 3, "MEVA")]), want, err_msg=f"MEVA v s={s}")
+
+
+ATM_FIELDS = (("MEVA", 1), ("HLAT", 1), ("HSEN", 1), ("RBBR", 1), ("UMOM", 2), ("VMOM", 3))
+
+
+@pytest.mark.parametrize("device_out", [False, True])
+def test_fp32_atmos_accumulation_and_remap(device_out):
+    """fp32 engine with the exchange -> atmosphere accumulation and an exchange -> model
+    remap: fp32 fields in, fp32 outputs, weights and sums in fp64 (OASIS maps in double).
+    Bit-identical to the fp64 sequential sum of the GPU's own fp32 fluxes, rounded once."""
+    torch = pytest.importorskip("torch")
+    from fcx.parallel import local_atmos, synthetic_atmos_map, synthetic_model_map
+
+    n = 20_011
+    c32 = as_dtype(build_case("MOM5", n=n, T=1, bias=True), "float32")
+    amap = synthetic_atmos_map(n)
+    la = local_atmos(amap, 0, 1)
+    mmap = synthetic_model_map(n, 1_700, links_per_cell=2)
+
+    def out(m):
+        if device_out:
+            return torch.full((m,), float("nan"), dtype=torch.float32, device="cuda:0")
+        return np.full(m, np.nan, np.float32)
+
+    atm = {k: out(la.n_atmos) for k, _ in ATM_FIELDS}
+    rmo = {k: out(mmap.n_model) for k, _ in ATM_FIELDS}
+    eng = Engine(c32.lf, 1, c32.methods, corrections=c32.corrections,
+                 atmos={"local": la, "fields": [(2, 1, g, k, atm[k]) for k, g in ATM_FIELDS]},
+                 remaps=[{"n_dst": mmap.n_model, "src": mmap.src, "dst": mmap.dst, "w": mmap.weight,
+                          "fields": [(2, 1, g, k, rmo[k]) for k, g in ATM_FIELDS]}])
+    eng.step(PHASE_ALL, STEP_T)
+    eng.close()
+
+    def host(a):
+        return a.cpu().numpy() if device_out else a
+
+    for k, g in ATM_FIELDS:
+        flux = np.asarray(c32.lf.field[(1, g, k)], dtype=np.float64)
+        want = oracle_lib.atmos_accumulate(amap.atmos_index, amap.weight, flux, amap.n_atmos).astype(np.float32)
+        np.testing.assert_array_equal(host(atm[k]), want, err_msg=f"atmos {k}")
+        want = oracle_lib.remap_apply(mmap.src, mmap.dst, mmap.weight, flux, mmap.n_model).astype(np.float32)
+        np.testing.assert_array_equal(host(rmo[k]), want, err_msg=f"remap {k}")
+
+
+def test_fp32_engine_rejects_fp64_outputs():
+    from fcx.parallel import local_atmos, synthetic_atmos_map
+
+    n = 1_001
+    c32 = as_dtype(build_case("CCLM", n=n, T=1), "float32")
+    amap = synthetic_atmos_map(n)
+    la = local_atmos(amap, 0, 1)
+    with pytest.raises(TypeError):
+        Engine(c32.lf, 1, c32.methods, atmos={"local": la, "fields": [(2, 1, 1, "MEVA", np.zeros(la.n_atmos))]})

@@ -77,15 +77,16 @@ def random_run_map(n, lengths, seed):
     return AtmosMap(np.ascontiguousarray(idx, dtype=np.int32), np.ascontiguousarray(w), n_atmos)
 
 
-# run lengths: within a tile, every boundary crossed (130..140 > one 128-cell tile: carries
-# handed across several tiles in a chain), mixed 1..400
+# run lengths: 1..7 (the fused kernel: segments within a tile or crossing one boundary);
+# 130..140 and 1..400 (longer than half a tile: the engine runs atmos_kernel instead)
 @pytest.mark.parametrize("lengths", [(1, 7), (130, 140), (1, 400)])
 @pytest.mark.parametrize("mode", ["handoff", "capped", "pipelined"])
 def test_fused_accumulation_long_segments(lengths, mode):
-    """The fused accumulation with segments crossing one or several 128-cell wave tiles:
-    carries handed to the next tile's wave inside the launch (default one-trip grid), left
-    to the fix-up kernel (a grid-stride cap), and across the chunk launches of the pipelined
-    host step.  Bit-identical to the sequential sum of the GPU's own fluxes."""
+    """The accumulation with segments crossing 128-cell wave tiles: carries handed to the next
+    tile's wave inside the launch (default one-trip grid), left to the fix-up kernel (a
+    grid-stride cap), and across the chunk launches of the pipelined host step; long
+    segments through atmos_kernel.  Bit-identical to the sequential sum of the GPU's own
+    fluxes."""
     import torch
     from fcx.engine import Engine
     from fcx.parallel import local_atmos
