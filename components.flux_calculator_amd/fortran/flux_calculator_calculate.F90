@@ -154,10 +154,15 @@ CONTAINS
     SUBROUTINE set_matrix(which, m)
         INTEGER(c_int),                         INTENT(IN) :: which
         TYPE(sparse_regridding_matrix), TARGET, INTENT(IN) :: m
+        ! the C ABI takes double weights (copied at the call); REAL(wp) may be REAL(4)
+        REAL(c_double), ALLOCATABLE, TARGET :: w8(:)
         IF (m%num_elements <= 0) RETURN
+        ALLOCATE(w8(m%num_elements))
+        w8 = REAL(m%weight%field(1:m%num_elements), c_double)
         CALL check(fcx_set_regrid_matrix(engine, which, INT(m%num_elements, c_int64_t),          &
                                          c_loc(m%src_index%field(1)), c_loc(m%dst_index%field(1)), &
-                                         c_loc(m%weight%field(1))), 'fcx_set_regrid_matrix')
+                                         c_loc(w8(1))), 'fcx_set_regrid_matrix')
+        DEALLOCATE(w8)
     END SUBROUTINE set_matrix
 
     ! output_field(j) with surface_type 0 (flux_calculator.F90:909-918, 999-1008)
