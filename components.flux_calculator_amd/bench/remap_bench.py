@@ -10,6 +10,12 @@ Algorithmic bytes of one remap launch: per link 4 (column) + 8 (weight) + 8 per 
 gathered value); per model cell 4 (row pointer) + 8 per field (the written sum).
 
   python components.flux_calculator_amd/bench/remap_bench.py [--cells N] [--model M]
+  python components.flux_calculator_amd/bench/remap_bench.py --map geometric [--side 1300]
+
+--map geometric: the exchange grid of an atmosphere grid (side^2 cells) intersected with a
+finer ocean grid (fcx.parallel.geometric_maps; 9.2M exchange cells, 3.0M ocean cells at
+side 1300), the conservative exchange -> ocean remap (one link per exchange cell), so a
+model cell's links come from a few atmosphere rows as on the real grids.
 """
 import argparse
 import json
@@ -29,14 +35,19 @@ def main():
     ap.add_argument("--model", type=int, default=2_500_000)
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--map", choices=("synthetic", "geometric"), default="synthetic")
+    ap.add_argument("--side", type=int, default=1300, help="geometric: atmosphere cells per side")
     a = ap.parse_args()
     import torch
 
     from fcx.basic import PHASE_ALL
     from fcx.engine import Engine
-    from fcx.parallel import synthetic_model_map
+    from fcx.parallel import geometric_maps, synthetic_model_map
     from fcx.synthetic import build_case, inputs_for_bench
 
+    geo = geometric_maps(a.side)[1] if a.map == "geometric" else None
+    if geo is not None:
+        a.cells, a.model = geo.src.size, geo.n_model
     n, m = a.cells, a.model
     dev = torch.device("cuda", 0)
     stream = torch.cuda.current_stream(dev)
@@ -44,8 +55,8 @@ def main():
     case = build_case("CCLM", n=n, T=1, device=dev, data=data)
     engines = {"none": Engine(case.lf, 1, case.methods, device=0, stream=stream.cuda_stream)}
     alg = {}
-    for links in (1, 2):
-        mm = synthetic_model_map(n, m, links_per_cell=links)
+    for links in ((1,) if geo is not None else (1, 2)):
+        mm = geo if geo is not None else synthetic_model_map(n, m, links_per_cell=links)
         outs = {k: torch.empty(m, dtype=torch.float64, device=dev) for k, _ in FIELDS}
         rm = {"n_dst": m, "src": mm.src, "dst": mm.dst, "w": mm.weight,
               "fields": [(2, 1, g, k, outs[k]) for k, g in FIELDS]}
@@ -68,7 +79,8 @@ def main():
             e1.synchronize()
             times[k].append(e0.elapsed_time(e1) / a.reps)
     base = float(np.median(times["none"]))
-    out = {"cells": n, "model_cells": m, "fields": len(FIELDS), "step_ms_without_remap": round(base, 4)}
+    out = {"map": a.map, "cells": n, "model_cells": m, "fields": len(FIELDS),
+           "step_ms_without_remap": round(base, 4)}
     for k, v in alg.items():
         ms = float(np.median(times[k])) - base
         out[k] = {**v, "remap_ms": round(ms, 4), "GBps_algorithmic": round(v["bytes"] / (ms * 1e-3) / 1e9, 1)}

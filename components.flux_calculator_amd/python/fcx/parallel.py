@@ -212,3 +212,46 @@ def local_links(mmap: ModelMap, offset, size):
     keep = (mmap.src >= offset) & (mmap.src < offset + size)
     return (np.ascontiguousarray(mmap.src[keep] - offset, dtype=np.int32),
             np.ascontiguousarray(mmap.dst[keep], dtype=np.int32), np.ascontiguousarray(mmap.weight[keep]))
+
+
+def geometric_maps(n_atmos_side, ocean_ratio=0.75, offset=(0.3, 0.45)):
+    """Exchange grid of two overlapping regular grids, as the IOW ESM builds it: the
+    intersection of an atmosphere grid (n_atmos_side^2 unit cells) with a finer ocean grid
+    (cells of ocean_ratio, shifted by offset), one exchange cell per non-empty (atmosphere,
+    ocean) pair, ordered by atmosphere row, atmosphere column, then ocean row and column
+    (the exchange grid follows the atmosphere rows).  Returns the exchange ->
+    atmosphere map (contiguous runs, weights = area / atmosphere cell area) and the
+    conservative exchange -> ocean remap (one link per exchange cell, weights = area /
+    ocean cell area, links in exchange order), so a model cell's links come from a few
+    atmosphere rows, as on the real grids.  About (1 + 1/ocean_ratio)^2 exchange cells per
+    atmosphere cell."""
+    na = int(n_atmos_side)
+
+    def axis(off):
+        lo = off - ocean_ratio * np.ceil(off / ocean_ratio)  # first ocean edge <= 0
+        n_o = int(np.ceil((na - lo) / ocean_ratio))
+        edges = np.unique(np.concatenate([np.arange(na + 1, dtype=np.float64), lo + ocean_ratio * np.arange(n_o + 1)]))
+        edges = edges[(edges >= 0) & (edges <= na)]
+        mid = 0.5 * (edges[:-1] + edges[1:])
+        width = np.diff(edges)
+        keep = width > 1e-12
+        ia = np.floor(mid[keep]).astype(np.int64)
+        io = np.floor((mid[keep] - lo) / ocean_ratio).astype(np.int64)
+        return ia, io, width[keep], n_o
+
+    ax, ox, wx, nox = axis(offset[0])
+    ay, oy, wy, noy = axis(offset[1])
+    # every (y-segment, x-segment) pair is one exchange cell
+    sy, sx = np.meshgrid(np.arange(ay.size), np.arange(ax.size), indexing="ij")
+    sy, sx = sy.ravel(), sx.ravel()
+    order = np.lexsort((ox[sx], oy[sy], ax[sx], ay[sy]))  # last key is the primary one
+    sy, sx = sy[order], sx[order]
+    area = wy[sy] * wx[sx]
+    a_idx = (ay[sy] * na + ax[sx]).astype(np.int32)
+    o_idx = (oy[sy] * nox + ox[sx]).astype(np.int64)
+    n_model = int(noy * nox)
+    a_w = area / np.bincount(a_idx, weights=area, minlength=na * na)[a_idx]
+    o_w = area / np.bincount(o_idx, weights=area, minlength=n_model)[o_idx]
+    n = area.size
+    return (AtmosMap(np.ascontiguousarray(a_idx), np.ascontiguousarray(a_w), na * na),
+            ModelMap(np.arange(n, dtype=np.int32), o_idx.astype(np.int32), np.ascontiguousarray(o_w), n_model))
