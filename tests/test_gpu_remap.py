@@ -96,3 +96,30 @@ def test_sharded_remap_partial_sums_complete_by_summation():
         want = oracle_lib.remap_apply(mmap.src, mmap.dst, mmap.weight, np.asarray(full.lf.field[(1, g, name)]),
                                       mmap.n_model)
         assert mixed_error(total[name], want) <= 1e-12, name
+
+
+@pytest.mark.parametrize("variant", ["CCLM", "RCO"])
+def test_geometric_grid_accumulation_and_remap(variant):
+    """The exchange grid of an atmosphere grid intersected with a finer ocean grid
+    (fcx.parallel.geometric_maps): the fused exchange -> atmosphere accumulation (runs of 4, 6
+    or 9 cells) and the conservative exchange -> ocean remap in one step, both bit-identical
+    to the sequential applications on the GPU's own fluxes."""
+    from fcx.parallel import geometric_maps, local_atmos
+
+    am, mm = geometric_maps(70)
+    n = am.atmos_index.size
+    case = build_case(variant, n=n, T=1, bias=True)
+    la = local_atmos(am, 0, 1)
+    atm = {k: np.full(am.n_atmos, np.nan) for k, _ in FIELDS}
+    rmo = {k: np.full(mm.n_model, np.nan) for k, _ in FIELDS}
+    eng = Engine(case.lf, 1, case.methods, corrections=case.corrections,
+                 atmos={"local": la, "fields": [(2, 1, g, k, atm[k]) for k, g in FIELDS]},
+                 remaps=[remap_spec(mm, rmo)])
+    eng.step(PHASE_ALL, STEP_T)
+    eng.close()
+    for name, g in FIELDS:
+        flux = np.asarray(case.lf.field[(1, g, name)])
+        np.testing.assert_array_equal(atm[name], oracle_lib.atmos_accumulate(am.atmos_index, am.weight, flux,
+                                                                              am.n_atmos), err_msg=name)
+        np.testing.assert_array_equal(rmo[name], oracle_lib.remap_apply(mm.src, mm.dst, mm.weight, flux,
+                                                                         mm.n_model), err_msg=name)

@@ -186,3 +186,22 @@ def test_sharded_model_remap_one_allreduce():
     for _, vals in res:
         assert mixed_error(np.array(vals), ref) <= 1e-12
     np.testing.assert_array_equal(np.array(res[0][1]), np.array(res[1][1]))  # every rank gets it
+
+
+def test_geometric_maps_are_conservative_and_ordered():
+    """fcx.parallel.geometric_maps: every exchange cell in exactly one atmosphere and one
+    ocean cell, exchange cells ordered by atmosphere cell (contiguous runs), weights summing
+    to 1 per atmosphere and per (covered) ocean cell, areas tiling the domain."""
+    from fcx.parallel import geometric_maps
+
+    am, mm = geometric_maps(40)
+    n = am.atmos_index.size
+    assert mm.src.size == n and np.array_equal(mm.src, np.arange(n))
+    assert np.all(np.diff(am.atmos_index) >= 0) and am.n_atmos == 1600
+    runs = np.bincount(am.atmos_index, minlength=am.n_atmos)
+    assert runs.min() >= 1 and runs.max() <= 9
+    np.testing.assert_allclose(np.bincount(am.atmos_index, weights=am.weight), 1.0, rtol=1e-13)
+    s = np.bincount(mm.dst, weights=mm.weight, minlength=mm.n_model)
+    np.testing.assert_allclose(s[s > 0], 1.0, rtol=1e-13)
+    # within an atmosphere cell the ocean cells come row by row
+    assert n == pytest.approx(am.n_atmos * (1 + 1 / 0.75) ** 2, rel=0.05)
