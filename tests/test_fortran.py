@@ -34,3 +34,69 @@ def test_fortran_host_selftest_on_gpu():
     r = subprocess.run([SELFTEST], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "FCX_FORTRAN_SELFTEST OK" in r.stdout, r.stdout
+
+
+DROPIN = os.path.join(ROOT, "oracle", "_ref", "fcx_dropin_host")
+TABLES = ("which_spec_vapor_surface_t", "which_spec_vapor_surface_u", "which_spec_vapor_surface_v",
+          "which_flux_mass_evap", "which_flux_heat_latent", "which_flux_heat_sensible", "which_flux_momentum",
+          "which_flux_radiation_blackbody")  # fcx_attach's argument order
+
+
+def write_manifest(case, d, step_time):
+    """tests/fortran/dropin_host.F90's manifest of a synthetic case: every distinct array once
+    (aliases share a buffer), the slot map, the method tables, corrections, type-0 outputs."""
+    import numpy as np
+    from fcx.basic import IDX
+
+    bufs, lines, slots = {}, [], []
+    for (s, g, name), a in case.lf.field.items():
+        k = bufs.setdefault(id(a), (len(bufs) + 1, a))[0]
+        slots.append(f"S {s} {g} {IDX[name]} {k} {int((s, g, name) in case.lf.allocated)}")
+    nt, nu, nv = case.grid_size
+    lines.append(f"N {len(bufs)} {case.num_surface_types} {nt} {nu} {nv}")
+    for k, a in bufs.values():
+        np.ascontiguousarray(a, dtype=np.float64).tofile(os.path.join(d, f"a{k}.bin"))
+        lines.append(f"A {k} {a.shape[0]} a{k}.bin")
+    lines += slots
+    for t, table in enumerate(TABLES, start=1):
+        for s, m in enumerate(case.methods[table], start=1):
+            lines.append(f"M {t} {s} {m}")
+    if case.corrections is not None:
+        init_date, corr = case.corrections
+        np.ascontiguousarray(corr, dtype=np.float64).tofile(os.path.join(d, "corr.bin"))  # [n][12] = (12, n)
+        lines.append(f"C {init_date} corr.bin")
+    for phase, g, name in case.averages:
+        lines.append(f"V {phase} {g} {IDX[name]}")
+    lines.append(f"R {step_time}")
+    outs = list(dict.fromkeys(case.outputs))
+    for i, (s, g, name) in enumerate(outs):
+        lines.append(f"O {s} {g} {IDX[name]} o{i}.bin")
+    with open(os.path.join(d, "manifest.txt"), "w") as f:
+        f.write("\n".join(lines) + "\n")
+    return outs
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not os.path.exists(DROPIN), reason="Fortran drop-in host not built")
+@pytest.mark.parametrize("mode", ["percall", "fused"])
+@pytest.mark.parametrize("variant,T", [("CCLM", 2), ("MOM5", 3), ("RCO", 1)])
+def test_dropin_module_in_a_fortran_host(tmp_path, mode, variant, T):
+    """The drop-in module flux_calculator_calculate driven by a Fortran host whose
+    local_field is the reference's own flux_calculator_basic (tests/fortran/dropin_host.F90):
+    the reference subroutines one by one (percall), or the two fused phases (fused), against
+    the oracle on the same inputs (tests/parity.py tolerance)."""
+    import numpy as np
+
+    import oracle_lib
+    from fcx.synthetic import build_case
+    from parity import assert_parity
+
+    step_time = 3600 * 24 * 45  # February: the bias month changes from the init date's
+    case = build_case(variant, n=5003, T=T, bias=True)
+    outs = write_manifest(case, str(tmp_path), step_time)
+    ref = oracle_lib.run_case(case, "c", current_step_time=step_time)
+    r = subprocess.run([DROPIN, str(tmp_path), mode], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "DROPIN_HOST OK" in r.stdout, r.stdout
+    got = {key: np.fromfile(os.path.join(tmp_path, f"o{i}.bin"), dtype=np.float64) for i, key in enumerate(outs)}
+    assert_parity(got, {k: ref[k] for k in outs}, label=f"{variant} T={T} {mode}")
