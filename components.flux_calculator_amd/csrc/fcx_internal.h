@@ -64,6 +64,14 @@ struct AvgRegs {
   const double *fare[kMaxTypes];   // FARE(s) of the t grid (shared by every register slot)
 };
 
+// Tile-blocked field layout (FCX_OPT_TILED_LAYOUT).  Cell j of a field array lives at
+// element (j >> kLayoutShift) * tile_stride + (j & (kLayoutTile - 1)) of its buffer; the
+// kernels get tpad = tile_stride - kLayoutTile and address base + j + (j >> kLayoutShift) * tpad
+// (tpad = 0: plain contiguous arrays).  Chunk boundaries of a tiled engine are whole tiles.
+constexpr int kLayoutShift = 12;
+constexpr int64_t kLayoutTile = int64_t(1) << kLayoutShift;
+__host__ __device__ inline int64_t tiled(int64_t j, int64_t tpad) { return j + (j >> kLayoutShift) * tpad; }
+
 struct Params {
   int64_t n[3];          // cells per grid
   int64_t n_max;         // max of the grids in this launch
@@ -77,6 +85,7 @@ struct Params {
   AvgRegs ravg;
   int32_t ravg_on;        // any ravg.out set (selects the RAVG kernel instantiation)
   int32_t pad2;
+  int64_t tpad;           // tile-blocked layout of every field pointer above (0: contiguous)
 };
 
 // launchers (fcx_kernels.hip); return hipError_t as int
@@ -113,6 +122,7 @@ struct AtmosArgs {
   double *out[kMaxAtmosFields];
   int32_t f32;             // fields and outputs are float arrays (fp32 engine); the weights,
                            // products and sums stay fp64 (OASIS maps in double)
+  int64_t tpad;            // layout of the x fields (engine buffers); out is contiguous
 };
 int launch_atmos(const AtmosArgs &a, void *stream);
 
@@ -138,14 +148,17 @@ struct AtmosFused {
   int64_t n_atmos;
   double *shared;
   int32_t stride, left, right;
+  int64_t tpad;        // layout of x (engine buffers); idx, w, out are contiguous
 };
 int launch_atmos_fixup(const AtmosFused &af, int64_t n_cells, void *stream);
 int launch_atmos_finish(const AtmosArgs &a, int32_t n_boundaries, void *stream);
 
 // f32: w, src and dst are float arrays (the reference's single-precision build, where the
 // matrix weights and the fields are REAL(wp) = REAL(4), basic:117-122, and so is the sum)
+// src and dst: engine buffers in the layout tpad
 int launch_regrid_csr(const int32_t *row_ptr, const int32_t *col, const double *w,
-                      const double *src, double *dst, int64_t n_dst, void *stream, bool f32 = false);
+                      const double *src, double *dst, int64_t n_dst, void *stream, bool f32 = false,
+                      int64_t tpad = 0);
 int launch_zero(double *x, int64_t n, void *stream);
 
 }  // namespace fcx

@@ -89,8 +89,12 @@ __device__ __forceinline__ Vec<C, R> splat(R a) {
 // The parameter block holds every field pointer as double*; in the fp32 engine the same
 // pointers address float arrays, so every access reinterprets them as R*.
 #define FOR_C _Pragma("unroll") for (int i = 0; i < C; ++i)
-#define LD(p, j, n) ld<C, NT, R>(reinterpret_cast<const R *>(p), j, n)
-#define ST(p, j, n, ...) st<C, NT, R>(reinterpret_cast<R *>(p), j, n, __VA_ARGS__)
+// Field arrays may be tile-blocked (fcx_internal.h, FCX_OPT_TILED_LAYOUT): cell j is at
+// p + j + D_ with D_ = (j >> kLayoutShift) * tpad, the same shift for every array and for
+// the C cells of one lane (j0 is a multiple of C, C divides the tile).  D_ is in scope
+// wherever these are used; D_ = 0 for contiguous arrays.
+#define LD(p, j, n) ld<C, NT, R>(reinterpret_cast<const R *>(p) + D_, j, n)
+#define ST(p, j, n, ...) st<C, NT, R>(reinterpret_cast<R *>(p) + D_, j, n, __VA_ARGS__)
 
 // Momentum of one (type, u- or v-grid) cell group; `north` selects VMOM.
 struct NoEmit {
@@ -102,22 +106,22 @@ template <int C, bool NT, class R, class Emit>
 __device__ __forceinline__ void momentum(int8_t m, bool north, const UVGridPtrs &g,
                                          const Vec<C, R> &ts, const Vec<C, R> &ps, const Vec<C, R> &u,
                                          const Vec<C, R> &v, const Vec<C, R> &vel, const Vec<C, R> &qs,
-                                         const Vec<C, R> &a, int64_t j0, int64_t n, Emit &emit, int slot);
+                                         const Vec<C, R> &a, int64_t j0, int64_t n, int64_t D_, Emit &emit, int slot);
 
 template <int C, bool NT, class R>
 __device__ __forceinline__ void momentum(int8_t m, bool north, const UVGridPtrs &g,
                                          const Vec<C, R> &ts, const Vec<C, R> &ps, const Vec<C, R> &u,
                                          const Vec<C, R> &v, const Vec<C, R> &vel, const Vec<C, R> &qs,
-                                         const Vec<C, R> &a, int64_t j0, int64_t n) {
+                                         const Vec<C, R> &a, int64_t j0, int64_t n, int64_t D_) {
   NoEmit none;
-  momentum<C, NT, R>(m, north, g, ts, ps, u, v, vel, qs, a, j0, n, none, -1);
+  momentum<C, NT, R>(m, north, g, ts, ps, u, v, vel, qs, a, j0, n, D_, none, -1);
 }
 
 template <int C, bool NT, class R, class Emit>
 __device__ __forceinline__ void momentum(int8_t m, bool north, const UVGridPtrs &g,
                                          const Vec<C, R> &ts, const Vec<C, R> &ps, const Vec<C, R> &u,
                                          const Vec<C, R> &v, const Vec<C, R> &vel, const Vec<C, R> &qs,
-                                         const Vec<C, R> &a, int64_t j0, int64_t n, Emit &emit, int slot) {
+                                         const Vec<C, R> &a, int64_t j0, int64_t n, int64_t D_, Emit &emit, int slot) {
   if (!g.mom) return;
   Vec<C, R> out;
   if (m == FCX_ZERO) {
@@ -142,7 +146,7 @@ __device__ __forceinline__ void momentum(int8_t m, bool north, const UVGridPtrs 
 // QSUR + momentum on one separate u or v grid (non-merged layout).
 template <int C, bool NT, class R>
 __device__ __forceinline__ void uv_grid(const TypeParams &tp, int k, uint32_t stages, int64_t j0,
-                                        int64_t n) {
+                                        int64_t n, int64_t D_) {
   const UVGridPtrs &g = tp.uv[k];
   const uint32_t s_qsur = k == 0 ? S_QSUR_U : S_QSUR_V;
   const uint32_t s_mom = k == 0 ? S_UMOM : S_VMOM;
@@ -167,7 +171,7 @@ __device__ __forceinline__ void uv_grid(const TypeParams &tp, int k, uint32_t st
   if (do_m) {
     Vec<C, R> vel;
     FOR_C vel.v[i] = wind(u.v[i], v.v[i]);
-    momentum<C, NT, R>(tp.m_mom, k == 1, g, ts, ps, u, v, vel, qs, a, j0, n);
+    momentum<C, NT, R>(tp.m_mom, k == 1, g, ts, ps, u, v, vel, qs, a, j0, n, D_);
   }
 }
 
@@ -240,8 +244,9 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
   const int T = TM ? 1 : P->num_types;
   const int64_t nt = P->n[0];
   const bool do_t = j0 < nt;
-  Vec<C, R> corr = {};
-  if (do_t && corr_m && (stages & S_MEVA)) corr = LD(corr_m, j0, nt);
+  const int64_t D_ = (j0 >> kLayoutShift) * P->tpad;  // field layout shift of this lane's cells
+  Vec<C, R> corr = {};  // the month slice is a plain contiguous array
+  if (do_t && corr_m && (stages & S_MEVA)) corr = ld<C, NT, R>(reinterpret_cast<const R *>(corr_m), j0, nt);
   Vec<C, R> rsdd = {};
   if (do_t && P->rsdd0 && (stages & S_RSDR)) rsdd = LD(P->rsdd0, j0, nt);
   Sink<C, R, RAVG, Emit> sink(emit, P->ravg, acc_lds);
@@ -275,7 +280,7 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
     if constexpr (kReload) {                                                           \
       if (ptr_) {                                                                      \
         if (FCX_TEMPORAL_SHARED && s + 1 < T && P->type[s + 1].grp.member == ptr_)     \
-          var = ld<C, false, R>(reinterpret_cast<const R *>(ptr_), j0, nt);            \
+          var = ld<C, false, R>(reinterpret_cast<const R *>(ptr_) + D_, j0, nt);       \
         else                                                                           \
           var = LD(ptr_, j0, nt);                                                      \
       }                                                                                \
@@ -414,16 +419,16 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
         const bool do_v = (stages & S_VMOM) && tp.uv[1].mom;
         if (do_u || do_v) {
           const Vec<C, R> &a = (m_mo == FCX_MOM5) ? cmom : amom;
-          if (do_u) momentum<C, NT, R>(m_mo, false, tp.uv[0], ts, ps, u, v, vel, qs, a, j0, nt, sink, A_UMOM);
-          if (do_v) momentum<C, NT, R>(m_mo, true, tp.uv[1], ts, ps, u, v, vel, qs, a, j0, nt, sink, A_VMOM);
+          if (do_u) momentum<C, NT, R>(m_mo, false, tp.uv[0], ts, ps, u, v, vel, qs, a, j0, nt, D_, sink, A_UMOM);
+          if (do_v) momentum<C, NT, R>(m_mo, true, tp.uv[1], ts, ps, u, v, vel, qs, a, j0, nt, D_, sink, A_VMOM);
         }
       }
       // ---- distribute_shortwave_radiation_flux (calc:355-362): RSDR_s = RSDD_0
       if ((stages & S_RSDR) && g.rsdr) ST(g.rsdr, j0, nt, rsdd);
     }
     if constexpr (!MERGED) {
-      if (j0 < P->n[1]) uv_grid<C, NT, R>(tp, 0, stages, j0, P->n[1]);
-      if (j0 < P->n[2]) uv_grid<C, NT, R>(tp, 1, stages, j0, P->n[2]);
+      if (j0 < P->n[1]) uv_grid<C, NT, R>(tp, 0, stages, j0, P->n[1], D_);
+      if (j0 < P->n[2]) uv_grid<C, NT, R>(tp, 1, stages, j0, P->n[2], D_);
     }
   }
 #undef HOLD
@@ -694,7 +699,7 @@ __global__ __launch_bounds__(256) void atmos_fixup_kernel(const AtmosFused af, i
     const double wx = af.w[x];
 #pragma unroll
     for (int k = 0; k < kFusedFields; ++k)
-      if (af.out[k]) acc[k] = acc[k] + wx * af.x[k][x];
+      if (af.out[k]) acc[k] = acc[k] + wx * af.x[k][tiled(x, af.tpad)];
   }
 #pragma unroll
   for (int k = 0; k < kFusedFields; ++k) {
@@ -714,12 +719,12 @@ __global__ __launch_bounds__(256) void regrid_csr_kernel(const int32_t *__restri
                                                          const int32_t *__restrict__ col,
                                                          const R *__restrict__ w,
                                                          const R *__restrict__ src,
-                                                         R *__restrict__ dst, int64_t n_dst) {
+                                                         R *__restrict__ dst, int64_t n_dst, int64_t tpad) {
   const int64_t d = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (d >= n_dst) return;
   R acc = R(0);
-  for (int32_t k = row_ptr[d]; k < row_ptr[d + 1]; ++k) acc = acc + src[col[k]] * w[k];
-  dst[d] = acc;
+  for (int32_t k = row_ptr[d]; k < row_ptr[d + 1]; ++k) acc = acc + src[tiled(col[k], tpad)] * w[k];
+  dst[tiled(d, tpad)] = acc;
 }
 
 // exchange -> atmosphere accumulation (SCRIP weight application of the type-0 fields).
@@ -757,7 +762,7 @@ __global__ __launch_bounds__(256) void atmos_kernel(const AtmosArgs a) {
       const double wk = __builtin_nontemporal_load(a.w + k);
 #pragma unroll
       for (int f = 0; f < kMaxAtmosFields; ++f)
-        if (f < a.nf) lds[f * kAtmChunk + i] = wk * (double)reinterpret_cast<const R *>(a.x[f])[xi];
+        if (f < a.nf) lds[f * kAtmChunk + i] = wk * (double)reinterpret_cast<const R *>(a.x[f])[tiled(xi, a.tpad)];
     }
     __syncthreads();
     const int32_t lo = max(k_lo, C0), hi = min(k_hi, C0 + len);
@@ -913,16 +918,16 @@ int launch_cells(const Params *hp, const Params *dp, const double *corr_m, const
 }
 
 int launch_regrid_csr(const int32_t *row_ptr, const int32_t *col, const double *w,
-                      const double *src, double *dst, int64_t n_dst, void *stream, bool f32) {
+                      const double *src, double *dst, int64_t n_dst, void *stream, bool f32, int64_t tpad) {
   if (n_dst <= 0) return 0;
   const int blocks = (int)((n_dst + 255) / 256);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (f32)
     hipLaunchKernelGGL(regrid_csr_kernel<float>, dim3(blocks), dim3(256), 0, s, row_ptr, col,
                        reinterpret_cast<const float *>(w), reinterpret_cast<const float *>(src),
-                       reinterpret_cast<float *>(dst), n_dst);
+                       reinterpret_cast<float *>(dst), n_dst, tpad);
   else
-    hipLaunchKernelGGL(regrid_csr_kernel<double>, dim3(blocks), dim3(256), 0, s, row_ptr, col, w, src, dst, n_dst);
+    hipLaunchKernelGGL(regrid_csr_kernel<double>, dim3(blocks), dim3(256), 0, s, row_ptr, col, w, src, dst, n_dst, tpad);
   return (int)hipGetLastError();
 }
 

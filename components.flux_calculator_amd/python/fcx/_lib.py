@@ -61,6 +61,7 @@ SIGNATURES = [
     ("fcx_average_across_surface_types", _I, [_P, _I, _I]),
     ("fcx_do_regridding", _I, [_P, _I, _I]),
     ("fcx_device_ptr", _I, [_P, _I, _I, _I, _c.POINTER(_DP)]),
+    ("fcx_device_layout", _I, [_P, _c.POINTER(_I64), _c.POINTER(_I64)]),
     ("fcx_last_kernel_ms", _I, [_P, _c.POINTER(_c.c_float)]),
     ("fcx_pinned_bytes", _I, [_P, _P]),
     ("fcx_algorithmic_bytes", _I, [_P, _I, _c.POINTER(_I64)]),

@@ -162,7 +162,7 @@ class Engine:
     OPTIONS = {"cells_per_thread": 1, "max_blocks": 2, "nontemporal": 3, "specialize": 4,
                "atmos_in_run": 5, "pin_host": 6, "pipeline_chunks": 7,
                "pipeline_min_chunk": 8, "zero_copy": 9,
-               "timing": 10}
+               "timing": 10, "tiled_layout": 11}
 
     def run_atmos(self, phase=PHASE_ALL):
         _lib.check(self.lib.fcx_run_atmos(self.h, phase))
@@ -178,6 +178,13 @@ class Engine:
         p = ctypes.POINTER(ctypes.c_double)()
         _lib.check(self.lib.fcx_device_ptr(self.h, s, g, IDX[name], ctypes.byref(p)))
         return ctypes.cast(p, ctypes.c_void_p).value
+
+    def device_layout(self):
+        """(tile, tile_stride) of the engine-owned mirrors: cell j of a device buffer is at
+        element (j // tile) * tile_stride + j % tile (fcx_device_layout)."""
+        tile, stride = ctypes.c_int64(), ctypes.c_int64()
+        _lib.check(self.lib.fcx_device_layout(self.h, ctypes.byref(tile), ctypes.byref(stride)))
+        return tile.value, stride.value
 
     def close(self):
         if self.h is not None:

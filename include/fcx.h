@@ -151,8 +151,13 @@ int fcx_average_across_surface_types(fcx_engine *e, int which_grid, int var); /*
 int fcx_do_regridding(fcx_engine *e, int var, int surface_type);           /* basic:463 */
 
 /* ---- device-resident use and measurement ---- */
-/* device buffer behind a slot (NULL if unbound) */
+/* device buffer behind a slot (NULL if unbound).  Cell j of it sits at element
+ * (j / tile) * tile_stride + j % tile (fcx_device_layout); tile_stride == tile means the
+ * buffer is one contiguous array. */
 int fcx_device_ptr(fcx_engine *e, int surface_type, int grid, int var, double **dptr);
+/* layout of the engine-owned field mirrors (after fcx_commit): cells in tiles of `tile`
+ * elements, consecutive tiles of one array `tile_stride` elements apart (FCX_OPT_TILED_LAYOUT) */
+int fcx_device_layout(fcx_engine *e, int64_t *tile, int64_t *tile_stride);
 /* device time (hipEvents on the engine stream) of the kernels of the last fcx_run;
    needs FCX_OPT_TIMING = 1 */
 int fcx_last_kernel_ms(fcx_engine *e, float *ms);
@@ -216,8 +221,15 @@ enum fcx_option {
                                    no copy calls.  0 off, 1 on, 2 auto (default): on when
                                    every grid is below 2 x PIPELINE_MIN_CHUNK cells and
                                    PIN_HOST is on */
-  FCX_OPT_TIMING = 10           /* record the events behind fcx_last_kernel_ms (default 0:
+  FCX_OPT_TIMING = 10,          /* record the events behind fcx_last_kernel_ms (default 0:
                                    two event records per run cost ~8 us on small grids) */
+  FCX_OPT_TILED_LAYOUT = 11     /* engine-owned mirrors tile-blocked (default 1): tiles of
+                                   4096 cells, the read-only arrays' tiles interleaved in
+                                   one pool and the written arrays' in another, so a wave's
+                                   accesses fall in one contiguous region (+8-10 % streaming
+                                   rate, components.flux_calculator_amd/bench/layout_probe.hip).
+                                   Applied at fcx_commit when no field array is the caller's
+                                   device memory or used in place (zero-copy) */
 };
 int fcx_set_option(fcx_engine *e, int option, int64_t value);
 
