@@ -174,7 +174,7 @@ struct fcx_engine {
   // 0 when the field buffers are plain contiguous arrays
   bool tiled_opt = true;
   int64_t tpad = 0;
-  void *pool_out = nullptr;  // second pool of a tiled engine: the arrays some launch writes
+  std::vector<void *> tiled_pools;  // the pools of a tiled engine (alloc_tiled)
 
   fcx_engine() {
     for (auto &a : slot)
@@ -282,7 +282,7 @@ extern "C" int fcx_destroy(fcx_engine *e) {
     (void)hipFree(r.pool);
   }
   (void)hipFree(e->pool);
-  (void)hipFree(e->pool_out);
+  for (void *p : e->tiled_pools) (void)hipFree(p);
   if (e->ev0) (void)hipEventDestroy(e->ev0);
   if (e->ev1) (void)hipEventDestroy(e->ev1);
   for (hipEvent_t ev : e->ev_in) (void)hipEventDestroy(ev);
@@ -1044,44 +1044,71 @@ static void map_host_arrays(fcx_engine *e) {
 
 // Tile-blocked mirrors (FCX_OPT_TILED_LAYOUT).  Every field array is cut into tiles of
 // kLayoutTile cells; tile t of all arrays of one pool sits together: array k of the pool at
-// element t * S * kLayoutTile + k * kLayoutTile, S = slots per tile.  The arrays some launch
-// writes (flux outputs, averaged type-0 outputs) get one pool and the read-only inputs the
-// other, both with the same S, so one tile stride serves every field pointer.  A wave's
-// accesses then fall in one contiguous region per pool instead of 10-20 separate streams:
-// 6.35 vs 5.8 TB/s for the CCLM/MOM5/RCO access shapes (bench/layout_probe.hip; a single
-// mixed pool 6.28, tiles of 2048 / 8192 cells 6.25 / 6.31).
+// element t * S * kLayoutTile + k * kLayoutTile, S = slots per tile, the same S for every
+// pool so that one tile stride serves every field pointer.  Pools by use in the whole-step
+// launch (its plan, built here on the bindings): the arrays it only reads, the arrays it
+// writes, and the rest (bound but not touched by it, e.g. another variant's coefficients)
+// in pools of their own, so a launch touches every slot of the read pool and no gaps sit
+// between the arrays it streams.  A wave's accesses then fall in one contiguous region per
+// pool instead of 10-20 separate streams: 6.35 vs 5.8 TB/s for the CCLM/MOM5/RCO access
+// shapes (bench/layout_probe.hip; one mixed pool 6.28, a pool with unused slots between the
+// streamed arrays 6.1, tiles of 2048 / 8192 cells 6.25 / 6.31).
+static uint32_t phase_stages(int phase);
 static int alloc_tiled(fcx_engine *e) {
   static const int kOut[] = {FCX_QSUR, FCX_MEVA, FCX_HLAT, FCX_HSEN, FCX_RBBR, FCX_UMOM, FCX_VMOM, FCX_RSDR};
-  std::vector<char> written(e->bufs.size(), 0);
-  for (int s = 0; s <= e->T; ++s)
+  enum { kRead = 0, kWrite = 1, kCold = 2 };
+  std::vector<int> cls(e->bufs.size(), kCold);
+  {  // the whole-step plan's read and write sets (pointers are not assigned yet: dropped)
+    Plan p;
+    const std::string saved = g_err;
+    if (build_plan(e, phase_stages(FCX_PHASE_EARLY | FCX_PHASE_NORMAL), FCX_PHASE_EARLY | FCX_PHASE_NORMAL, p) ==
+        FCX_OK) {
+      for (int b : p.reads) cls[b] = kRead;
+      for (int b : p.writes) cls[b] = kWrite;
+    }
+    g_err = saved;
+    (void)hipFree(p.dev);
+  }
+  for (int s = 0; s <= e->T; ++s)  // outputs of other phases / staged launches
     for (int g = 1; g <= 3; ++g)
       for (int v : kOut)
-        if (e->buf(s, g, v) >= 0) written[e->buf(s, g, v)] = 1;
-  for (auto &a : e->averages)
-    if (e->buf(0, a.second.first, a.second.second) >= 0) written[e->buf(0, a.second.first, a.second.second)] = 1;
+        if (e->buf(s, g, v) >= 0 && cls[e->buf(s, g, v)] == kCold) cls[e->buf(s, g, v)] = kWrite;
+  for (auto &a : e->averages) {
+    const int b = e->buf(0, a.second.first, a.second.second);
+    if (b >= 0 && cls[b] == kCold) cls[b] = kWrite;
+  }
   int64_t n_max = 0;
-  int slots[2] = {0, 0};
-  std::vector<int> slot(e->bufs.size(), 0);
+  int count[3] = {0, 0, 0};
   for (size_t b = 0; b < e->bufs.size(); ++b) {
     n_max = std::max(n_max, e->bufs[b].n);
-    slot[b] = slots[(int)written[b]]++;
+    ++count[cls[b]];
   }
-  const int64_t S = std::max(1, std::max(slots[0], slots[1]));
+  const int64_t S = std::max(1, std::max(count[kRead], count[kWrite]));
   const int64_t tiles = std::max<int64_t>(1, (n_max + kLayoutTile - 1) / kLayoutTile);
   const size_t bytes = (size_t)tiles * S * kLayoutTile * e->esize;
-  void *pools[2] = {nullptr, nullptr};
-  for (int k = 0; k < 2; ++k) {
-    if (!slots[k]) continue;
-    hipError_t err = hipMalloc(&pools[k], bytes);
-    if (err != hipSuccess) {
-      (void)hipFree(pools[0]);
-      return fail(FCX_E_NOMEM, "hipMalloc(%zu) for the tiled field mirrors: %s", bytes, hipGetErrorString(err));
+  // pool and slot of every buffer: read pool, write pool, then the cold ones S to a pool
+  std::vector<std::pair<int, int>> at(e->bufs.size());
+  int npools = 0, fill[3] = {0, 0, 0}, pool_of[2] = {-1, -1}, cold_pool = -1;
+  for (size_t b = 0; b < e->bufs.size(); ++b) {
+    const int c = cls[b];
+    if (c != kCold) {
+      if (pool_of[c] < 0) pool_of[c] = npools++;
+      at[b] = {pool_of[c], fill[c]++};
+    } else {
+      if (cold_pool < 0 || fill[kCold] == S) cold_pool = npools++, fill[kCold] = 0;
+      at[b] = {cold_pool, fill[kCold]++};
     }
   }
-  e->pool = pools[0] ? pools[0] : pools[1];
-  e->pool_out = pools[0] ? pools[1] : nullptr;
+  for (int k = 0; k < npools; ++k) {
+    void *p = nullptr;
+    hipError_t err = hipMalloc(&p, bytes);
+    if (err != hipSuccess)
+      return fail(FCX_E_NOMEM, "hipMalloc(%zu) for the tiled field mirrors: %s", bytes, hipGetErrorString(err));
+    e->tiled_pools.push_back(p);
+  }
   for (size_t b = 0; b < e->bufs.size(); ++b)
-    e->bufs[b].dev = reinterpret_cast<double *>((char *)pools[(int)written[b]] + (size_t)slot[b] * kLayoutTile * e->esize);
+    e->bufs[b].dev = reinterpret_cast<double *>((char *)e->tiled_pools[at[b].first] +
+                                                (size_t)at[b].second * kLayoutTile * e->esize);
   e->tpad = (S - 1) * kLayoutTile;
   return FCX_OK;
 }
@@ -1162,7 +1189,7 @@ extern "C" int fcx_commit(fcx_engine *e) {
   // plain layout: one pooled allocation for all host-bound mirrors, 256-B aligned sub-buffers
   size_t total = 0;
   std::vector<size_t> off(e->bufs.size(), 0);
-  for (size_t b = 0; b < e->bufs.size() && !e->pool; ++b) {
+  for (size_t b = 0; b < e->bufs.size() && e->tiled_pools.empty(); ++b) {
     if (e->bufs[b].external) continue;
     off[b] = total;
     total += ((size_t)e->bufs[b].n * e->esize + 255) / 256 * 256;

@@ -35,8 +35,23 @@ def assert_parity(got: dict, ref: dict, tol=FP64_TOL, label=""):
         e = mixed_error(got[key], r)
         worst[key] = e
     bad = {k: v for k, v in worst.items() if not v <= tol}
-    assert not bad, f"{label}: fields over tolerance {tol}: {bad}"
+    assert not bad, f"{label}: fields over tolerance {tol}: {bad}; " + "; ".join(
+        _where(got[k], ref[k], tol, k) for k in bad)
     return worst
+
+
+def _where(x, ref, tol, key):
+    """the failing cells of one field (count, first indices and values) for the message"""
+    x = np.asarray(x, dtype=np.float64)
+    ref = np.asarray(ref, dtype=np.float64)
+    fin = np.isfinite(ref)
+    top = np.max(np.abs(ref[fin])) if fin.any() else 1.0
+    scale = np.maximum(np.abs(ref), 1e-6 * top)
+    with np.errstate(invalid="ignore"):
+        off = ~(np.abs(x - ref) <= tol * np.where(scale == 0.0, 1.0, scale)) & ~(np.isnan(x) & np.isnan(ref))
+    idx = np.nonzero(off)[0]
+    return (f"{key}: {idx.size} of {x.size} cells, first {idx[:8].tolist()}, "
+            f"got {x[idx[:4]].tolist()} want {ref[idx[:4]].tolist()}")
 
 
 def norm_error(x, ref):
