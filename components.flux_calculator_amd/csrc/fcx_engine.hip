@@ -136,6 +136,7 @@ struct fcx_engine {
   double *atm_shared = nullptr;
   int32_t atm_nb = 0, atm_stride = 0, atm_left = -1, atm_right = -1;
   void *atm_pool = nullptr;
+  int64_t atm_out_tpad = 0;  // tile-blocked atmosphere outputs (kernels: tiled(a, atm_out_tpad))
   bool atmos_in_run = true;
   bool atm_done_fused = false;  // the last fcx_run already accumulated the atmosphere fields
   // exchange -> model remaps (SCRIP links, CSR by destination in link order)
@@ -608,6 +609,7 @@ static void plan_fused_atmos(fcx_engine *e, Plan &pl, uint32_t stages, int phase
   af.left = e->atm_left;
   af.right = e->atm_right;
   af.tpad = e->tpad;
+  af.out_tpad = e->atm_out_tpad;
   pl.af = af;
   pl.atm_nf = nf;
   pl.atm_fused = true;
@@ -1053,6 +1055,9 @@ static void map_host_arrays(fcx_engine *e) {
 // pool instead of 10-20 separate streams: 6.35 vs 5.8 TB/s for the CCLM/MOM5/RCO access
 // shapes (bench/layout_probe.hip; one mixed pool 6.28, a pool with unused slots between the
 // streamed arrays 6.1, tiles of 2048 / 8192 cells 6.25 / 6.31).
+#ifndef FCX_TILED_ATM  // A/B builds: 0 keeps the atmosphere output mirrors contiguous
+#define FCX_TILED_ATM 1
+#endif
 static uint32_t phase_stages(int phase);
 static int alloc_tiled(fcx_engine *e) {
   static const int kOut[] = {FCX_QSUR, FCX_MEVA, FCX_HLAT, FCX_HSEN, FCX_RBBR, FCX_UMOM, FCX_VMOM, FCX_RSDR};
@@ -1254,8 +1259,23 @@ extern "C" int fcx_commit(fcx_engine *e) {
                           hipMemcpyHostToDevice));
     }
     size_t need = 0;
-    for (auto &f : e->atm_fields)
+    bool atm_ext = false;
+    for (auto &f : e->atm_fields) {
+      atm_ext = atm_ext || f.external;
       if (!f.external) need += ((size_t)std::max<int64_t>(e->n_atmos, 1) * e->esize + 255) / 256 * 256;
+    }
+    // tile-blocked outputs (with the field mirrors, FCX_TILED_ATM): the fields' tiles of 4096
+    // atmosphere cells side by side, so the fused kernel's segment-end stores of a wave land
+    // in one region instead of one per field
+    const int64_t nfa = (int64_t)e->atm_fields.size();
+    if (FCX_TILED_ATM && e->tpad && !atm_ext && nfa >= 2 && e->n_atmos > 0) {
+      const int64_t tiles = (e->n_atmos + kLayoutTile - 1) / kLayoutTile;
+      HIP_TRY(hipMalloc(&e->atm_pool, (size_t)tiles * nfa * kLayoutTile * e->esize));
+      for (int64_t k = 0; k < nfa; ++k)
+        e->atm_fields[k].out_dev = reinterpret_cast<double *>((char *)e->atm_pool + (size_t)k * kLayoutTile * e->esize);
+      e->atm_out_tpad = (nfa - 1) * kLayoutTile;
+      need = 0;
+    }
     if (need) {
       HIP_TRY(hipMalloc(&e->atm_pool, need));
       size_t off = 0;
@@ -1362,6 +1382,7 @@ static int launch_plan(fcx_engine *e, Plan *pl, const double *corr_m, int64_t lo
 }
 
 static int regrid_var(fcx_engine *e, int var, int surface_type);
+static hipError_t get_atm(const fcx_engine *e, double *host, const double *dev, hipStream_t s);
 static int run_remaps(fcx_engine *e, int phase);
 static int download_remaps(fcx_engine *e, int phase, hipStream_t s);
 
@@ -1403,8 +1424,7 @@ extern "C" int fcx_download(fcx_engine *e, int phase) {
   if (int r = copy_bufs(e, pl->writes, false)) return r;
   for (auto &f : e->atm_fields)
     if ((f.phase & phase) && !f.external && e->n_atmos > 0)
-      HIP_TRY(hipMemcpyAsync(f.out_host, f.out_dev, e->n_atmos * e->esize, hipMemcpyDeviceToHost,
-                             e->stream));
+      HIP_TRY(get_atm(e, f.out_host, f.out_dev, e->stream));
   if (int r = download_remaps(e, phase, e->stream)) return r;
   if (e->any_regrid) {  // device-side regrid destinations of the fields this phase computes
     std::vector<int> extra;
@@ -1426,6 +1446,20 @@ extern "C" int fcx_download(fcx_engine *e, int phase) {
   return FCX_OK;
 }
 
+// an atmosphere output mirror -> its host array (2-D copy of the whole tiles when tiled)
+static hipError_t get_atm(const fcx_engine *e, double *host, const double *dev, hipStream_t s) {
+  const size_t es = e->esize, n = (size_t)e->n_atmos;
+  if (!e->atm_out_tpad) return hipMemcpyAsync(host, dev, n * es, hipMemcpyDeviceToHost, s);
+  const size_t row = (size_t)kLayoutTile * es, pitch = (size_t)(kLayoutTile + e->atm_out_tpad) * es;
+  const size_t full = n / kLayoutTile;
+  if (full)
+    if (hipError_t r = hipMemcpy2DAsync(host, row, dev, pitch, row, full, hipMemcpyDeviceToHost, s)) return r;
+  if (n > full * kLayoutTile)
+    return hipMemcpyAsync((char *)host + full * row, (const char *)dev + full * pitch, (n - full * kLayoutTile) * es,
+                          hipMemcpyDeviceToHost, s);
+  return hipSuccess;
+}
+
 static AtmosArgs atmos_args(fcx_engine *e, int phase) {
   AtmosArgs a{};
   a.f32 = e->f32 ? 1 : 0;
@@ -1438,6 +1472,7 @@ static AtmosArgs atmos_args(fcx_engine *e, int phase) {
   a.right = e->atm_right;
   a.shared = e->atm_shared;
   a.tpad = e->tpad;
+  a.out_tpad = e->atm_out_tpad;
   for (auto &f : e->atm_fields) {
     if (!(f.phase & phase) || a.nf >= kMaxAtmosFields) continue;
     a.x[a.nf] = e->dptr(f.s, f.g, f.var);
@@ -1591,8 +1626,7 @@ static int step_pipelined(fcx_engine *e, int phase, int32_t t, Plan *pl) {
   if (e->atmos_in_run || e->atm_done_fused)
     for (auto &f : e->atm_fields)
       if ((f.phase & phase) && !f.external && e->n_atmos > 0)
-        HIP_TRY(hipMemcpyAsync(f.out_host, f.out_dev, e->n_atmos * e->esize, hipMemcpyDeviceToHost,
-                               e->s_out));
+        HIP_TRY(get_atm(e, f.out_host, f.out_dev, e->s_out));
   if (int r = download_remaps(e, phase, e->s_out)) return r;
   if (e->timing) HIP_TRY(hipEventRecord(e->ev1, e->s_out));
   e->timed = e->timing;

@@ -122,7 +122,8 @@ struct AtmosArgs {
   double *out[kMaxAtmosFields];
   int32_t f32;             // fields and outputs are float arrays (fp32 engine); the weights,
                            // products and sums stay fp64 (OASIS maps in double)
-  int64_t tpad;            // layout of the x fields (engine buffers); out is contiguous
+  int64_t tpad;            // layout of the x fields (engine buffers)
+  int64_t out_tpad;        // layout of out: the engine's tiled atmosphere pool, or 0
 };
 int launch_atmos(const AtmosArgs &a, void *stream);
 
@@ -148,7 +149,8 @@ struct AtmosFused {
   int64_t n_atmos;
   double *shared;
   int32_t stride, left, right;
-  int64_t tpad;        // layout of x (engine buffers); idx, w, out are contiguous
+  int64_t tpad;        // layout of x (engine buffers); idx, w are contiguous
+  int64_t out_tpad;    // layout of out (tiled atmosphere pool, or 0)
 };
 int launch_atmos_fixup(const AtmosFused &af, int64_t n_cells, void *stream);
 int launch_atmos_finish(const AtmosArgs &a, int32_t n_boundaries, void *stream);

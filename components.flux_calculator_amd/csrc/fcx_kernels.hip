@@ -563,9 +563,9 @@ __device__ __forceinline__ void segment_done(const AtmosFused &af, int64_t tile,
   for (int k = 0; k < kFusedFields; ++k) {
     if (!af.out[k]) continue;
     if (FCX_ATM_NT_STORE)
-      __builtin_nontemporal_store(acc[k], af.out[k] + a);
+      __builtin_nontemporal_store(acc[k], af.out[k] + tiled(a, af.out_tpad));
     else
-      af.out[k][a] = acc[k];
+      af.out[k][tiled(a, af.out_tpad)] = acc[k];
     if (a == 0 && af.left >= 0) af.shared[(int64_t)af.left * af.stride + k] = acc[k];
     if (a == af.n_atmos - 1 && af.right >= 0) af.shared[(int64_t)af.right * af.stride + k] = acc[k];
   }
@@ -704,7 +704,7 @@ __global__ __launch_bounds__(256) void atmos_fixup_kernel(const AtmosFused af, i
 #pragma unroll
   for (int k = 0; k < kFusedFields; ++k) {
     if (!af.out[k]) continue;
-    af.out[k][a] = acc[k];
+    af.out[k][tiled(a, af.out_tpad)] = acc[k];
     if (a == 0 && af.left >= 0) af.shared[(int64_t)af.left * af.stride + k] = acc[k];
     if (a == af.n_atmos - 1 && af.right >= 0) af.shared[(int64_t)af.right * af.stride + k] = acc[k];
   }
@@ -776,7 +776,7 @@ __global__ __launch_bounds__(256) void atmos_kernel(const AtmosArgs a) {
 #pragma unroll
   for (int f = 0; f < kMaxAtmosFields; ++f) {
     if (f >= a.nf) break;
-    reinterpret_cast<R *>(a.out[f])[c] = (R)acc[f];
+    reinterpret_cast<R *>(a.out[f])[tiled(c, a.out_tpad)] = (R)acc[f];
     if (c == 0 && a.left >= 0) a.shared[(int64_t)a.left * a.stride + f] = acc[f];
     if (c == a.n_atmos - 1 && a.right >= 0) a.shared[(int64_t)a.right * a.stride + f] = acc[f];
   }
@@ -790,7 +790,7 @@ __global__ void atmos_finish_kernel(const AtmosArgs a, int32_t n_boundaries) {
   if (t < a.nf) {
     R *out = reinterpret_cast<R *>(a.out[t]);
     if (a.left >= 0) out[0] = (R)a.shared[(int64_t)a.left * a.stride + t];
-    if (a.right >= 0) out[a.n_atmos - 1] = (R)a.shared[(int64_t)a.right * a.stride + t];
+    if (a.right >= 0) out[tiled(a.n_atmos - 1, a.out_tpad)] = (R)a.shared[(int64_t)a.right * a.stride + t];
   }
   __syncthreads();
   for (int64_t i = t; i < (int64_t)n_boundaries * a.stride; i += blockDim.x) a.shared[i] = 0.0;
