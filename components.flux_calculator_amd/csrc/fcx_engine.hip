@@ -1473,6 +1473,7 @@ static AtmosArgs atmos_args(fcx_engine *e, int phase) {
   a.shared = e->atm_shared;
   a.tpad = e->tpad;
   a.out_tpad = e->atm_out_tpad;
+  a.vec = a.col == nullptr && e->aligned16;
   for (auto &f : e->atm_fields) {
     if (!(f.phase & phase) || a.nf >= kMaxAtmosFields) continue;
     a.x[a.nf] = e->dptr(f.s, f.g, f.var);

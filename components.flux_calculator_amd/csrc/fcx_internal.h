@@ -124,6 +124,8 @@ struct AtmosArgs {
                            // products and sums stay fp64 (OASIS maps in double)
   int64_t tpad;            // layout of the x fields (engine buffers)
   int64_t out_tpad;        // layout of out: the engine's tiled atmosphere pool, or 0
+  int32_t vec;             // col == nullptr and every x 16-B aligned: vector staging loads
+  int32_t pad;
 };
 int launch_atmos(const AtmosArgs &a, void *stream);
 

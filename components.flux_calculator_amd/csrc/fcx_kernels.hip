@@ -730,7 +730,8 @@ __global__ __launch_bounds__(256) void regrid_csr_kernel(const int32_t *__restri
 // exchange -> atmosphere accumulation (SCRIP weight application of the type-0 fields).
 // One thread per local atmosphere cell, 256 cells per block.  The block's exchange range
 // [row_ptr[a0], row_ptr[a0 + 256]) is streamed through LDS in chunks of kAtmChunk cells:
-// the whole block loads weights and fields with coalesced 8-B loads and stores the
+// the whole block loads weights and fields with coalesced loads (16-B vectors of consecutive
+// links when the links are the exchange cells in order, `vec`) and stores the
 // products w*x per field, then every lane adds the products of its own segment in link
 // order.  acc = acc + w*x from 0.0 in increasing link order is exactly the sequential
 // weight application, so the result is bit-identical to it (no atomics, no tree order).
@@ -748,6 +749,9 @@ __global__ __launch_bounds__(256) void atmos_kernel(const AtmosArgs a) {
   const int64_t c = a0 + threadIdx.x;
   const int64_t a_end = min(a0 + (int64_t)blockDim.x, a.n_atmos);
   const int32_t K0 = a.row_ptr[a0], K1 = a.row_ptr[a_end];
+  constexpr int V = 16 / sizeof(R);  // elements per 16-B vector (2 fp64, 4 fp32)
+  using VecT = typename std::conditional<sizeof(R) == 8, d2, f4>::type;
+  const int32_t n_links = a.vec ? a.row_ptr[a.n_atmos] : 0;
   const bool mine = c < a.n_atmos;
   const int32_t k_lo = mine ? a.row_ptr[c] : 0, k_hi = mine ? a.row_ptr[c + 1] : 0;
   double acc[kMaxAtmosFields];
@@ -756,13 +760,50 @@ __global__ __launch_bounds__(256) void atmos_kernel(const AtmosArgs a) {
   for (int32_t C0 = K0; C0 < K1; C0 += kAtmChunk) {
     const int32_t len = min(kAtmChunk, K1 - C0);
     __syncthreads();
-    for (int32_t i = threadIdx.x; i < len; i += blockDim.x) {
-      const int32_t k = C0 + i;
-      const int32_t xi = a.col ? a.col[k] : k;
-      const double wk = __builtin_nontemporal_load(a.w + k);
+    if (a.vec) {  // link k = exchange cell k: 16-B loads of V consecutive weights and fields
+      const int32_t hi_k = C0 + len;
+      for (int32_t v = (C0 & ~(V - 1)) + (int32_t)threadIdx.x * V; v < hi_k; v += (int32_t)blockDim.x * V) {
+        const bool full = v + V <= n_links;  // v..v+V-1 share a layout tile (V divides it)
+        double wv[V];
+        if (full) {
 #pragma unroll
-      for (int f = 0; f < kMaxAtmosFields; ++f)
-        if (f < a.nf) lds[f * kAtmChunk + i] = wk * (double)reinterpret_cast<const R *>(a.x[f])[tiled(xi, a.tpad)];
+          for (int h = 0; h < V / 2; ++h) {
+            const d2 t = __builtin_nontemporal_load(reinterpret_cast<const d2 *>(a.w + v) + h);
+            wv[2 * h] = t[0];
+            wv[2 * h + 1] = t[1];
+          }
+        } else {
+#pragma unroll
+          for (int i = 0; i < V; ++i) wv[i] = v + i < n_links ? a.w[v + i] : 0.0;
+        }
+        const int64_t xo = tiled(v, a.tpad);
+#pragma unroll
+        for (int f = 0; f < kMaxAtmosFields; ++f) {
+          if (f >= a.nf) break;
+          const R *xf = reinterpret_cast<const R *>(a.x[f]) + xo;
+          R xv[V];
+          if (full) {
+            const VecT t = __builtin_nontemporal_load(reinterpret_cast<const VecT *>(xf));
+#pragma unroll
+            for (int i = 0; i < V; ++i) xv[i] = t[i];
+          } else {
+#pragma unroll
+            for (int i = 0; i < V; ++i) xv[i] = v + i < n_links ? xf[i] : R(0);
+          }
+#pragma unroll
+          for (int i = 0; i < V; ++i)
+            if (v + i >= C0 && v + i < hi_k) lds[f * kAtmChunk + (v + i - C0)] = wv[i] * (double)xv[i];
+        }
+      }
+    } else {
+      for (int32_t i = threadIdx.x; i < len; i += blockDim.x) {
+        const int32_t k = C0 + i;
+        const int32_t xi = a.col ? a.col[k] : k;
+        const double wk = __builtin_nontemporal_load(a.w + k);
+#pragma unroll
+        for (int f = 0; f < kMaxAtmosFields; ++f)
+          if (f < a.nf) lds[f * kAtmChunk + i] = wk * (double)reinterpret_cast<const R *>(a.x[f])[tiled(xi, a.tpad)];
+      }
     }
     __syncthreads();
     const int32_t lo = max(k_lo, C0), hi = min(k_hi, C0 + len);
