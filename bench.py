@@ -65,8 +65,8 @@ def parse():
                         "(tile-blocked, FCX_OPT_TILED_LAYOUT) are uploaded once before the timed region")
     p.add_argument("--tiled", type=int, default=1, help="FCX_OPT_TILED_LAYOUT of the engines (A/B)")
     p.add_argument("--precision", choices=("f64", "f32"), default="f64",
-                   help="f32: the fp32 variant (config 5): fp32 cell pass, then the accumulation as "
-                        "its own kernel (fp32 fluxes in, fp64 weights and sums, fp32 outputs)")
+                   help="f32: the fp32 variant (config 5): fp32 cell pass with the accumulation fused in "
+                        "(fp32 fluxes, fp64 weights, products and sums, fp32 outputs)")
     return p.parse_args()
 
 
@@ -308,14 +308,16 @@ def main():
             "bytes_per_cell": round(alg_bytes[i] / n, 3),
             "GBps": round(alg_bytes[i] / (mean_ms[i] * 1e-3) / 1e9, 1)}
         for i, v in enumerate(variants)}
+    # the accumulation runs inside the flux kernel (T = 1, or T >= 2 with the register averages
+    # in fp64) unless a grid-stride cap is set; otherwise it is its own kernel after it
+    fused = la is not None and (args.max_blocks is None or args.max_blocks <= 0) and (args.types == 1 or not f32)
     traffic = None
     tfile = os.path.join(ROOT, "profiles", "traffic.json")
     if os.path.exists(tfile):
         try:
             t = json.load(open(tfile))
             # the timed launch carries the accumulation only when it is fused (fp64)
-            traffic = t.get(traffic_key(variants[dom], n, args.types, args.bias, la is not None and not f32,
-                                        args.precision))
+            traffic = t.get(traffic_key(variants[dom], n, args.types, args.bias, fused, args.precision))
         except Exception:
             traffic = None
 
@@ -336,7 +338,7 @@ def main():
             "workload": ("config3/4: synthetic exchange grid, CCLM+MOM5+RCO fused flux kernels "
                          "back-to-back per coupling step"
                          + (" + exchange->atmosphere accumulation" if la is not None else "")
-                         + (" (its own kernel after the flux pass)" if la is not None and f32 else "")
+                         + (" (its own kernel after the flux pass)" if la is not None and not fused else "")
                          + (", fp32 variant (config 5)" if f32 else "") + ", inputs HBM-resident"),
             "cells_per_gpu": n,
             "cells_global": n_global,
@@ -357,8 +359,7 @@ def main():
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": (f"cells_atmos_kernel[{variants[dom]}]" if la is not None and not f32
-                       else f"cells_kernel[{variants[dom]}]"),
+            "kernel": (f"cells_atmos_kernel[{variants[dom]}]" if fused else f"cells_kernel[{variants[dom]}]"),
             "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",

@@ -27,9 +27,9 @@ def kernel_key(name):
     m = re.search(r"cells_kernel<(\d), (true|false), (\d), (true|false), (double|float)", name)
     if m:
         return VARIANTS[m.group(3)], 0, "f64" if m.group(5) == "double" else "f32"
-    m = re.search(r"cells_atmos_kernel<(\d), (true|false)", name)
+    m = re.search(r"cells_atmos_kernel<(\d), (double|float), (\d), (true|false)", name)
     if m:
-        return VARIANTS[m.group(1)], 1, "f64"
+        return VARIANTS[m.group(3)], 1, "f64" if m.group(2) == "double" else "f32"
     return None
 
 

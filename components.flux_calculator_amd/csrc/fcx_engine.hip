@@ -561,8 +561,9 @@ static void plan_fused_atmos(fcx_engine *e, Plan &pl, uint32_t stages, int phase
   // (segments longer than half a tile, several hundred exchange cells per atmosphere cell,
   // go to atmos_kernel: one lane summing a long segment would hold up its whole wave; the
   // fp32 engine uses atmos_kernel too)
+  // (fp32 engine: T = 1 only, the register averages of several types are fp64-only)
   if (!pl.variant || !e->d_atm_idx || e->atm_maxseg > kTile / 2 || e->any_regrid || phase <= 0 ||
-      phase >= 1000 || !e->specialize || e->f32)
+      phase >= 1000 || !e->specialize || (e->f32 && e->T >= 2))
     return;
   const TypeParams &tp = pl.host.type[0];
   AtmosFused af{};
@@ -1358,7 +1359,9 @@ static int launch_plan(fcx_engine *e, Plan *pl, const double *corr_m, int64_t lo
   lc.variant = (e->specialize && lc.merged) ? pl->variant : 0;
   lc.f32 = e->f32;
   lc.ravg = pl->host.ravg_on != 0;
-  const bool fused = pl->atm_fused && lc.variant && lc.cells_per_thread == 2 && !lc.f32;
+  // the fp32 fused kernel has no fix-up kernel: it needs the in-launch hand-off (no grid cap)
+  const bool fused = pl->atm_fused && lc.variant && lc.cells_per_thread == 2 &&
+                     (!lc.f32 || (lc.max_blocks <= 0 && pl->af.err != nullptr));
   if (fused) {  // the shared-slot pointers may have been set after the plan was built
     pl->af.shared = e->atm_shared;
     pl->af.stride = e->atm_stride;
@@ -1808,12 +1811,14 @@ extern "C" int fcx_algorithmic_bytes(fcx_engine *e, int phase, int64_t *bytes) {
   int64_t extra = 0;  // atmosphere accumulation: weights (+cols), re-read fields, outputs
   int nf = 0;
   for (auto &f : e->atm_fields) nf += (f.phase & phase) ? 1 : 0;
-  if (pl->atm_fused && e->specialize && e->launch.cells_per_thread == 2 && e->aligned16) {
+  const int64_t es = (int64_t)e->esize;
+  if (pl->atm_fused && e->specialize && e->launch.cells_per_thread == 2 && e->aligned16 &&
+      (!e->f32 || e->launch.max_blocks <= 0)) {
     nf = 0;  // fused: index + weight per cell, the atmosphere outputs (fluxes not re-read)
-    extra = e->n[0] * (4 + 8) + (int64_t)pl->atm_nf * e->n_atmos * 8;
+    extra = e->n[0] * (4 + 8) + (int64_t)pl->atm_nf * e->n_atmos * es;
   } else if (nf && e->n_atmos >= 0 && e->atmos_in_run) {
     extra += e->n[0] * 8 + (e->atm_contiguous ? 0 : e->n[0] * 4) + (e->n_atmos + 1) * 4;
-    extra += (int64_t)nf * (e->n[0] + e->n_atmos) * 8;
+    extra += (int64_t)nf * (e->n[0] + e->n_atmos) * es;
   }
   *bytes = b * (int64_t)e->esize + extra;
   return FCX_OK;

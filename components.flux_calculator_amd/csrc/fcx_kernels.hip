@@ -488,21 +488,31 @@ __global__ __launch_bounds__(256, RAVG ? 3 : 1) void cells_kernel(const Params *
 // 16-B pad slot after every 16 cells.  Unpadded, cells 16 apart share a bank pair of the
 // 16-lane ds_read2_b64 groups and the segment-start lanes (3-5 cells apart) collide; the
 // pad shifts every 16-cell block by 2 banks and keeps the pair (2l, 2l+1) 16-B aligned.
-constexpr int kRow = kTile + 2 * (kTile / 16);
+// The fp32 engine's fused kernel holds C = 4 cells per lane: 256-cell wave tiles, rows of
+// row_len<4>() products (the products and sums stay fp64, as in atmos_kernel).
+template <int C>
+constexpr int tile_cells() { return 64 * C; }
+template <int C>
+constexpr int row_len() { return tile_cells<C>() + 2 * (tile_cells<C>() / 16); }
 __device__ __forceinline__ int lds_slot(int e) { return e + 2 * (e >> 4); }
 
-struct LdsEmit {
-  double *p;  // this wave's [kFusedFields][kRow] products
-  double w0, w1;
-  int s;      // lds_slot(2 * lane)
-  template <int C, class R>
-  __device__ __forceinline__ void operator()(int k, const Vec<C, R> &x) const {
+template <int C>
+struct LdsEmitT {
+  double *p;    // this wave's [kFusedFields][row_len<C>()] products
+  double w[C];  // the weights of the lane's cells
+  int s;        // lds_slot(C * lane)
+  template <int CC, class R>
+  __device__ __forceinline__ void operator()(int k, const Vec<CC, R> &x) const {
+    static_assert(CC == C, "one emitter per cell width");
 #ifndef FCX_DBG_ATM_NOLDS  // A/B measurement builds only: no LDS products (sums of garbage)
 #define FCX_DBG_ATM_NOLDS 0
 #endif
     if (FCX_DBG_ATM_NOLDS) return;
-    const d2 q = {w0 * x.v[0], w1 * x.v[1]};  // one 16-B LDS store per field
-    *reinterpret_cast<d2 *>(p + k * kRow + s) = q;
+#pragma unroll
+    for (int h = 0; h < C / 2; ++h) {  // 16-B LDS stores, w * x in fp64
+      const d2 q = {w[2 * h] * (double)x.v[2 * h], w[2 * h + 1] * (double)x.v[2 * h + 1]};
+      *reinterpret_cast<d2 *>(p + k * row_len<C>() + s + 2 * h) = q;
+    }
   }
 };
 
@@ -535,6 +545,8 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb) {
 // write-through agent-scope stores, then once they have completed flag[tile] = epoch) or
 // left for atmos_fixup_kernel; a complete one is the atmosphere value (and the boundary
 // slot of a first/last atmosphere cell shared with a neighbour rank).
+// R: the engine's output type (an fp32 engine's atmosphere outputs are float, rounded once)
+template <class R>
 __device__ __forceinline__ void segment_done(const AtmosFused &af, int64_t tile, int32_t a, const double *acc,
                                              bool cont) {
   if (cont) {
@@ -562,10 +574,11 @@ __device__ __forceinline__ void segment_done(const AtmosFused &af, int64_t tile,
 #pragma unroll
   for (int k = 0; k < kFusedFields; ++k) {
     if (!af.out[k]) continue;
+    R *o = reinterpret_cast<R *>(af.out[k]) + tiled(a, af.out_tpad);
     if (FCX_ATM_NT_STORE)
-      __builtin_nontemporal_store(acc[k], af.out[k] + tiled(a, af.out_tpad));
+      __builtin_nontemporal_store((R)acc[k], o);
     else
-      af.out[k][tiled(a, af.out_tpad)] = acc[k];
+      *o = (R)acc[k];
     if (a == 0 && af.left >= 0) af.shared[(int64_t)af.left * af.stride + k] = acc[k];
     if (a == af.n_atmos - 1 && af.right >= 0) af.shared[(int64_t)af.right * af.stride + k] = acc[k];
   }
@@ -602,82 +615,117 @@ __device__ __forceinline__ void take_carry(const AtmosFused &af, int64_t tile, d
 #ifndef FCX_T1_ATMOS_BLOCKS
 #define FCX_T1_ATMOS_BLOCKS 1
 #endif
-template <int VAR, bool NT, int TM, bool RAVG>
-__global__ __launch_bounds__(256, RAVG ? FCX_RAVG_ATMOS_BLOCKS : FCX_T1_ATMOS_BLOCKS) void cells_atmos_kernel(const Params *__restrict__ P,
+// waves per block of the fused kernel: 4, or 2 for the fp32 kernel, whose 256-cell product
+// rows take 13.8 KB of LDS per wave (smaller blocks pack the CUs' LDS better: 3 waves/SIMD)
+#ifndef FCX_F32_ATMOS_WAVES
+#define FCX_F32_ATMOS_WAVES 2
+#endif
+template <int C>
+constexpr int atmos_waves() { return C == 4 ? FCX_F32_ATMOS_WAVES : 4; }
+template <int C, class R, int VAR, bool NT, int TM, bool RAVG>
+__global__ __launch_bounds__(64 * atmos_waves<C>(), RAVG ? FCX_RAVG_ATMOS_BLOCKS : FCX_T1_ATMOS_BLOCKS) void cells_atmos_kernel(const Params *__restrict__ P,
                                                           const double *__restrict__ corr_m,
                                                           const AtmosFused af, int64_t lo, int64_t hi) {
-  // product rows [kFusedFields][kRow]; with RAVG they first serve as the accumulators of
+  static_assert(!RAVG || (C == 2 && sizeof(R) == 8), "register averages: fp64 engine only");
+  constexpr int kT = tile_cells<C>();  // cells per wave tile (lane l: cells C*l .. C*l+C-1)
+  constexpr int kR = row_len<C>();
+  // product rows [kFusedFields][kR]; with RAVG they first serve as the accumulators of
   // the type-0 averages (slot k = row k, TSUR in an extra row), then hold w * average
   constexpr int kRows = RAVG ? kAvgSlots : kFusedFields;
-  __shared__ double s_p[4][kRows * kRow];
+  __shared__ double s_p[atmos_waves<C>()][kRows * kR];
   const int64_t n = P->n_max;
-  const int64_t n_tiles = (hi + kTile - 1) / kTile;  // tiles [lo/kTile, n_tiles) of this launch
+  const int64_t n_tiles = (hi + kT - 1) / kT;  // tiles [lo/kT, n_tiles) of this launch
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   double *wp = s_p[wv];
   const int64_t waves = (int64_t)gridDim.x * (blockDim.x >> 6);
   const int64_t wave0 = (int64_t)xcd_block(blockIdx.x, gridDim.x) * (blockDim.x >> 6) + wv;
   const uint64_t at_or_above = ~0ull << lane;
   const uint64_t above = lane == 63 ? 0ull : (~0ull << (lane + 1));
-  for (int64_t tile = lo / kTile + wave0; tile < n_tiles; tile += waves) {
-    const int64_t t0 = tile * kTile;
-    const int64_t j0 = t0 + 2 * lane;
-    LdsEmit emit{wp, 0.0, 0.0, lds_slot(2 * lane)};
-    int32_t a0 = -1, a1 = -1;  // -1: past the grid end
-    if (j0 + 2 <= n) {
-      const int2 ii = *reinterpret_cast<const int2 *>(af.idx + j0);
-      const d2 ww = __builtin_nontemporal_load(reinterpret_cast<const d2 *>(af.w + j0));
-      a0 = ii.x;
-      a1 = ii.y;
-      emit.w0 = ww[0];
-      emit.w1 = ww[1];
-    } else if (j0 < n) {
-      a0 = af.idx[j0];
-      emit.w0 = af.w[j0];
+  for (int64_t tile = lo / kT + wave0; tile < n_tiles; tile += waves) {
+    const int64_t t0 = tile * kT;
+    const int64_t j0 = t0 + C * lane;
+    LdsEmitT<C> emit{wp, {}, lds_slot(C * lane)};
+    int32_t a[C];  // -1: past the grid end
+#pragma unroll
+    for (int i = 0; i < C; ++i) a[i] = -1;
+    if (j0 + C <= n) {
+      if constexpr (C == 2) {
+        const int2 ii = *reinterpret_cast<const int2 *>(af.idx + j0);
+        a[0] = ii.x;
+        a[1] = ii.y;
+      } else {
+        const int4 ii = *reinterpret_cast<const int4 *>(af.idx + j0);
+        a[0] = ii.x;
+        a[1] = ii.y;
+        a[2] = ii.z;
+        a[3] = ii.w;
+      }
+#pragma unroll
+      for (int h = 0; h < C / 2; ++h) {
+        const d2 ww = __builtin_nontemporal_load(reinterpret_cast<const d2 *>(af.w + j0) + h);
+        emit.w[2 * h] = ww[0];
+        emit.w[2 * h + 1] = ww[1];
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < C; ++i)
+        if (j0 + i < n) {
+          a[i] = af.idx[j0 + i];
+          emit.w[i] = af.w[j0 + i];
+        }
     }
     const int32_t prev_tile = t0 > 0 ? af.idx[t0 - 1] : -2;  // wave-uniform loads
-    const int64_t tend = t0 + kTile;
+    const int64_t tend = t0 + kT;
     const int32_t next_a = (tend < n) ? af.idx[tend] : -3;
     if (j0 < n)
-      process<2, true, VAR, NT, double, TM, RAVG>(P, corr_m, j0, emit, AccLds<2, double>{wp + emit.s, kRow});
-    // segment starts: cell 2l+i begins a segment when its atmosphere cell differs from the
+      process<C, true, VAR, NT, R, TM, RAVG>(P, corr_m, j0, emit,
+                                             AccLds<C, R>{reinterpret_cast<R *>(wp + emit.s), kR});
+    // segment starts: cell C*l+i begins a segment when its atmosphere cell differs from the
     // previous cell's (the first cell past the grid end also "starts", which ends the last
     // real segment)
-    int32_t prev = __shfl_up(a1, 1);
+    int32_t prev = __shfl_up(a[C - 1], 1);
     if (lane == 0) prev = prev_tile;
-    const bool s0 = a0 != prev, s1 = a1 != a0;
-    const uint64_t m0 = __ballot(s0), m1 = __ballot(s1);
+    bool st[C];
+    uint64_t m[C];
+#pragma unroll
+    for (int i = 0; i < C; ++i) {
+      st[i] = a[i] != (i ? a[i - 1] : prev);
+      m[i] = __ballot(st[i]);
+    }
     wave_sync();  // the wave's LDS products are visible to all its lanes
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int32_t a = i ? a1 : a0;
-      if (!(i ? s1 : s0) || a < 0) continue;
-      const int c = 2 * lane + i;
-      // next start after cell c: an even cell 2j (j > l) or an odd cell 2j+1 (j >= l for
-      // c even, j > l for c odd)
-      const int e_end = min(2 * first_bit(m0 & above), 2 * first_bit(m1 & (i ? above : at_or_above)) + 1);
-      const int end = min(e_end, kTile);
+    for (int i = 0; i < C; ++i) {
+      if (!st[i] || a[i] < 0) continue;
+      const int c = C * lane + i;
+      // next start after cell c: cell C*j+i' with j > l, or j == l and i' > i
+      int e_end = kT;
+#pragma unroll
+      for (int q = 0; q < C; ++q) e_end = min(e_end, C * first_bit(m[q] & (q > i ? at_or_above : above)) + q);
+      const int end = min(e_end, kT);
       double acc[kFusedFields];
 #pragma unroll
       for (int k = 0; k < kFusedFields; ++k) acc[k] = 0.0;
       for (int e = c; e < end; ++e) {
         const double *q = wp + lds_slot(e);
 #pragma unroll
-        for (int k = 0; k < kFusedFields; ++k) acc[k] = acc[k] + q[k * kRow];
+        for (int k = 0; k < kFusedFields; ++k) acc[k] = acc[k] + q[k * kR];
       }
-      segment_done(af, tile, a, acc, end == kTile && next_a == a);
+      segment_done<R>(af, tile, a[i], acc, end == kT && next_a == a[i]);
     }
     // hand-off: the segment the previous tile carried into this one is continued here, from
     // its carry over this tile's products of the segment's cells, in link order
-    if (af.handoff && lane == 0 && a0 >= 0 && a0 == prev_tile) {
-      const int end = min(min(2 * first_bit(m0), 2 * first_bit(m1) + 1), kTile);
+    if (af.handoff && lane == 0 && a[0] >= 0 && a[0] == prev_tile) {
+      int end = kT;
+#pragma unroll
+      for (int q = 0; q < C; ++q) end = min(end, C * first_bit(m[q]) + q);
       double acc[kFusedFields];
       take_carry(af, tile - 1, acc);
       for (int e = 0; e < end; ++e) {
         const double *q = wp + lds_slot(e);
 #pragma unroll
-        for (int k = 0; k < kFusedFields; ++k) acc[k] = acc[k] + q[k * kRow];
+        for (int k = 0; k < kFusedFields; ++k) acc[k] = acc[k] + q[k * kR];
       }
-      segment_done(af, tile, a0, acc, end == kTile && next_a == a0);
+      segment_done<R>(af, tile, a[0], acc, end == kT && next_a == a[0]);
     }
     wave_sync();  // every lane is done reading before the next tile overwrites the region
   }
@@ -777,9 +825,7 @@ __global__ __launch_bounds__(256) void atmos_kernel(const AtmosArgs a) {
           for (int i = 0; i < V; ++i) wv[i] = v + i < n_links ? a.w[v + i] : 0.0;
         }
         const int64_t xo = tiled(v, a.tpad);
-#pragma unroll
-        for (int f = 0; f < kMaxAtmosFields; ++f) {
-          if (f >= a.nf) break;
+        for (int f = 0; f < a.nf; ++f) {
           const R *xf = reinterpret_cast<const R *>(a.x[f]) + xo;
           R xv[V];
           if (full) {
@@ -893,15 +939,15 @@ static void launch_r(const Params *hp, const LaunchConfig &lc, int blocks, hipSt
     launch_c<C, R, 0, false>(lc, blocks, s, dp, corr_m, lo, hi);
 }
 
-template <int VAR, int TM, bool RAVG>
+template <int C, class R, int VAR, int TM, bool RAVG>
 static void launch_atm(bool nt, int blocks, hipStream_t s, const Params *dp, const double *corr_m,
                        const AtmosFused &af, int64_t lo, int64_t hi) {
   if (nt)
-    hipLaunchKernelGGL((cells_atmos_kernel<VAR, true, TM, RAVG>), dim3(blocks), dim3(256), 0, s, dp, corr_m,
-                       af, lo, hi);
+    hipLaunchKernelGGL((cells_atmos_kernel<C, R, VAR, true, TM, RAVG>), dim3(blocks), dim3(64 * atmos_waves<C>()), 0,
+                       s, dp, corr_m, af, lo, hi);
   else
-    hipLaunchKernelGGL((cells_atmos_kernel<VAR, false, TM, RAVG>), dim3(blocks), dim3(256), 0, s, dp, corr_m,
-                       af, lo, hi);
+    hipLaunchKernelGGL((cells_atmos_kernel<C, R, VAR, false, TM, RAVG>), dim3(blocks), dim3(64 * atmos_waves<C>()), 0,
+                       s, dp, corr_m, af, lo, hi);
 }
 
 // fused accumulation: one surface type (its fluxes), or several with the type-0 averages in
@@ -909,10 +955,14 @@ static void launch_atm(bool nt, int blocks, hipStream_t s, const Params *dp, con
 template <int VAR>
 static int launch_atm_r(const Params *hp, const LaunchConfig &lc, int blocks, hipStream_t s, const Params *dp,
                         const double *corr_m, const AtmosFused &af, int64_t lo, int64_t hi) {
-  if (hp->num_types == 1)
-    launch_atm<VAR, 1, false>(lc.nontemporal, blocks, s, dp, corr_m, af, lo, hi);
+  if (hp->num_types == 1 && lc.f32)  // fp32 engine: 4 cells per lane, T = 1 only
+    launch_atm<4, float, VAR, 1, false>(lc.nontemporal, blocks, s, dp, corr_m, af, lo, hi);
+  else if (lc.f32)
+    return (int)hipErrorInvalidValue;
+  else if (hp->num_types == 1)
+    launch_atm<2, double, VAR, 1, false>(lc.nontemporal, blocks, s, dp, corr_m, af, lo, hi);
   else if (lc.ravg)
-    launch_atm<VAR, 0, true>(lc.nontemporal, blocks, s, dp, corr_m, af, lo, hi);
+    launch_atm<2, double, VAR, 0, true>(lc.nontemporal, blocks, s, dp, corr_m, af, lo, hi);
   else
     return (int)hipErrorInvalidValue;
   return 0;
@@ -925,10 +975,12 @@ int launch_cells(const Params *hp, const Params *dp, const double *corr_m, const
   if (lo % kChunkAlign || lo < 0) return (int)hipErrorInvalidValue;
   if (hi <= lo) return 0;
   if (atm) {  // fused accumulation: T=1 specialised merged kernel, 2 cells per lane
-    // four waves per block, one 128-cell tile per wave and trip.  Default: one trip (full
+    // four waves per block (fp32: two), one 128-cell (fp32: 256-cell) tile per wave and trip.  Default: one trip (full
     // grid) -- +2 % per T=1 step over the 8192-block cap, equal at T=2 (profiles/r01/grid_ab)
-    const int64_t tiles = (hi - lo + kTile - 1) / kTile;
-    const int64_t full = (tiles + 3) / 4;
+    const int64_t kt = lc.f32 ? tile_cells<4>() : tile_cells<2>();
+    const int64_t kw = lc.f32 ? atmos_waves<4>() : atmos_waves<2>();
+    const int64_t tiles = (hi - lo + kt - 1) / kt;
+    const int64_t full = (tiles + kw - 1) / kw;
     const int blocks = (int)std::max<int64_t>(1, lc.max_blocks > 0 ? std::min<int64_t>(full, lc.max_blocks) : full);
     int r = 0;
     switch (lc.variant) {

@@ -193,3 +193,41 @@ def test_fp32_engine_rejects_fp64_outputs():
     la = local_atmos(amap, 0, 1)
     with pytest.raises(TypeError):
         Engine(c32.lf, 1, c32.methods, atmos={"local": la, "fields": [(2, 1, 1, "MEVA", np.zeros(la.n_atmos))]})
+
+
+# run lengths: 1..7 and 40..64 (the fp32 fused kernel, 256-cell wave tiles: segments within
+# a tile or crossing one boundary), 1..400 (longer than half a 128-cell tile: atmos_kernel)
+@pytest.mark.parametrize("lengths", [(1, 7), (40, 64), (1, 400)])
+@pytest.mark.parametrize("mode", ["handoff", "capped", "pipelined"])
+@pytest.mark.parametrize("variant", ["CCLM", "MOM5", "RCO"])
+def test_fp32_fused_accumulation(variant, mode, lengths):
+    """The fp32 engine's flux kernel with the accumulation fused in (4 cells per lane,
+    products and sums in fp64, outputs rounded once): carries handed between 256-cell tiles
+    inside the launch, across the chunk launches of the pipelined step, and the separate
+    kernel under a grid-stride cap.  Bit-identical to the sequential fp64 sum of the GPU's own
+    fp32 fluxes, rounded once; the fluxes within the fp32 gate of the oracle."""
+    from fcx.parallel import local_atmos
+    from test_gpu_multirank import random_run_map
+
+    n = 300_001 if mode == "pipelined" else 70_001
+    case = build_case(variant, n=n, T=1, bias=True, seed=23)
+    c32 = as_dtype(case, "float32")
+    amap = random_run_map(n, lengths, seed=lengths[1] + 5)
+    la = local_atmos(amap, 0, 1)
+    outs = {k: np.full(la.n_atmos, np.nan, np.float32) for k, _ in ATM_FIELDS}
+    opts = {"handoff": {}, "capped": {"max_blocks": 64},
+            "pipelined": {"pipeline_chunks": 4, "pipeline_min_chunk": 65536, "zero_copy": 0}}[mode]
+    eng = Engine(c32.lf, 1, c32.methods, corrections=c32.corrections,
+                 atmos={"local": la, "fields": [(2, 1, g, k, outs[k]) for k, g in ATM_FIELDS]}, options=opts)
+    for step in range(2):  # later runs' epochs must not see stale flags
+        for o in outs.values():
+            o[:] = np.nan
+        eng.step(PHASE_ALL, STEP_T + 3600 * step)
+        for k, g in ATM_FIELDS:
+            flux = np.asarray(c32.lf.field[(1, g, k)], dtype=np.float64)
+            want = oracle_lib.atmos_accumulate(amap.atmos_index, amap.weight, flux, amap.n_atmos).astype(np.float32)
+            np.testing.assert_array_equal(outs[k], want, err_msg=f"{variant} {mode} {k} step {step}")
+    eng.close()
+    c64 = as_dtype(c32, "float64")
+    ref = oracle_lib.run_case(c64, "c", current_step_time=STEP_T + 3600)
+    check({k: np.array(c32.lf.field[k], dtype=np.float64) for k in c32.outputs}, ref, f"{variant} fused fp32")
