@@ -109,6 +109,19 @@ def test_engine_calls_before_commit_fail_cleanly():
     lib.fcx_destroy(h)
 
 
+def test_tiled_layout_option_and_query_before_commit():
+    """FCX_OPT_TILED_LAYOUT (11) is set before fcx_commit; the layout is only known after it."""
+    lib = _lib.load()
+    h = ctypes.c_void_p()
+    gs = (ctypes.c_int32 * 3)(10, 10, 10)
+    _lib.check(lib.fcx_create(0, 1, gs, ctypes.byref(h)))
+    _lib.check(lib.fcx_set_option(h, 11, 0))
+    _lib.check(lib.fcx_set_option(h, 11, 1))
+    tile, stride = ctypes.c_int64(), ctypes.c_int64()
+    assert lib.fcx_device_layout(h, ctypes.byref(tile), ctypes.byref(stride)) == 2  # FCX_E_STATE
+    lib.fcx_destroy(h)
+
+
 def test_fp32_engine_takes_fp32_outputs_only():
     """The fp32 engine's atmosphere and remap outputs are float arrays (fcx.h
     fcx_set_precision): a float64 output is refused before any HIP call."""
