@@ -64,6 +64,7 @@ def parse():
                         "by the variants) instead of host arrays whose engine-owned device mirrors "
                         "(tile-blocked, FCX_OPT_TILED_LAYOUT) are uploaded once before the timed region")
     p.add_argument("--tiled", type=int, default=1, help="FCX_OPT_TILED_LAYOUT of the engines (A/B)")
+    p.add_argument("--nontemporal", type=int, default=1, help="FCX_OPT_NONTEMPORAL of the engines (A/B)")
     p.add_argument("--precision", choices=("f64", "f32"), default="f64",
                    help="f32: the fp32 variant (config 5): fp32 cell pass with the accumulation fused in "
                         "(fp32 fluxes, fp64 weights, products and sums, fp32 outputs)")
@@ -243,7 +244,7 @@ def main():
                    # the engine's internal ones would add a second event pair per launch
                    # (measured +2.5 % per step, components.flux_calculator_amd/bench/event_probe.py)
                    # host-bound: no page-locking (the inputs are uploaded once, not per step)
-                   options={"atmos_in_run": 0, "timing": 0, "pin_host": 0, "tiled_layout": args.tiled,
+                   options={"atmos_in_run": 0, "timing": 0, "pin_host": 0, "tiled_layout": args.tiled, "nontemporal": args.nontemporal,
                             **({"max_blocks": args.max_blocks} if args.max_blocks is not None else {})})
         if case_dev is None:
             e.upload(PHASE_ALL)  # inputs resident in HBM before the timed region

@@ -68,7 +68,10 @@ struct AvgRegs {
 // element (j >> kLayoutShift) * tile_stride + (j & (kLayoutTile - 1)) of its buffer; the
 // kernels get tpad = tile_stride - kLayoutTile and address base + j + (j >> kLayoutShift) * tpad
 // (tpad = 0: plain contiguous arrays).  Chunk boundaries of a tiled engine are whole tiles.
-constexpr int kLayoutShift = 12;
+#ifndef FCX_LAYOUT_SHIFT  // A/B builds: tiles of 2^shift cells (4096 measured best)
+#define FCX_LAYOUT_SHIFT 12
+#endif
+constexpr int kLayoutShift = FCX_LAYOUT_SHIFT;
 constexpr int64_t kLayoutTile = int64_t(1) << kLayoutShift;
 __host__ __device__ inline int64_t tiled(int64_t j, int64_t tpad) { return j + (j >> kLayoutShift) * tpad; }
 
