@@ -496,9 +496,20 @@ template <int C>
 constexpr int row_len() { return tile_cells<C>() + 2 * (tile_cells<C>() / 16); }
 __device__ __forceinline__ int lds_slot(int e) { return e + 2 * (e >> 4); }
 
+// fp32 fields (the fp32 engine): the wave's LDS holds the fluxes themselves, [kFusedFields]
+// rows of tile_cells<C>() floats, and one row of weights (fp64, lds_slot layout) behind them;
+// the segment sums form w * (double)x as they read them -- the same products in the same
+// order, in 4 instead of 6 row-lengths of fp64 per wave (more waves per CU).
+template <int C>
+constexpr int xrows_doubles() { return kFusedFields * tile_cells<C>() / 2; }
+template <class R, int C>
+constexpr int wave_lds_doubles(int rows) {
+  return sizeof(R) == 4 ? xrows_doubles<C>() + row_len<C>() : rows * row_len<C>();
+}
+
 template <int C>
 struct LdsEmitT {
-  double *p;    // this wave's [kFusedFields][row_len<C>()] products
+  double *p;    // this wave's [kFusedFields][row_len<C>()] products (fp32: flux rows, weights)
   double w[C];  // the weights of the lane's cells
   int s;        // lds_slot(C * lane)
   template <int CC, class R>
@@ -508,6 +519,12 @@ struct LdsEmitT {
 #define FCX_DBG_ATM_NOLDS 0
 #endif
     if (FCX_DBG_ATM_NOLDS) return;
+    if constexpr (sizeof(R) == 4 && C == 4) {  // one 16-B store of the lane's four fluxes
+      const int lane = threadIdx.x & 63;
+      *reinterpret_cast<f4 *>(reinterpret_cast<float *>(p) + k * tile_cells<C>() + C * lane) =
+          f4{x.v[0], x.v[1], x.v[2], x.v[3]};
+      return;
+    }
 #pragma unroll
     for (int h = 0; h < C / 2; ++h) {  // 16-B LDS stores, w * x in fp64
       const d2 q = {w[2 * h] * (double)x.v[2 * h], w[2 * h + 1] * (double)x.v[2 * h + 1]};
@@ -615,10 +632,9 @@ __device__ __forceinline__ void take_carry(const AtmosFused &af, int64_t tile, d
 #ifndef FCX_T1_ATMOS_BLOCKS
 #define FCX_T1_ATMOS_BLOCKS 1
 #endif
-// waves per block of the fused kernel: 4, or 2 for the fp32 kernel, whose 256-cell product
-// rows take 13.8 KB of LDS per wave (smaller blocks pack the CUs' LDS better: 3 waves/SIMD)
-#ifndef FCX_F32_ATMOS_WAVES
-#define FCX_F32_ATMOS_WAVES 2
+// waves per block of the fused kernel (the fp32 kernel's as an A/B knob)
+#ifndef FCX_F32_ATMOS_WAVES  // A/B: 2 paid while the fp32 rows held fp64 products (13.8 KB/wave)
+#define FCX_F32_ATMOS_WAVES 4
 #endif
 template <int C>
 constexpr int atmos_waves() { return C == 4 ? FCX_F32_ATMOS_WAVES : 4; }
@@ -632,7 +648,9 @@ __global__ __launch_bounds__(64 * atmos_waves<C>(), RAVG ? FCX_RAVG_ATMOS_BLOCKS
   // product rows [kFusedFields][kR]; with RAVG they first serve as the accumulators of
   // the type-0 averages (slot k = row k, TSUR in an extra row), then hold w * average
   constexpr int kRows = RAVG ? kAvgSlots : kFusedFields;
-  __shared__ double s_p[atmos_waves<C>()][kRows * kR];
+  constexpr bool kXF = sizeof(R) == 4;  // LDS holds fp32 fluxes + fp64 weights
+  static_assert(!kXF || C == 4, "fp32 flux rows: 4 cells per lane");
+  __shared__ double s_p[atmos_waves<C>()][wave_lds_doubles<R, C>(kRows)];
   const int64_t n = P->n_max;
   const int64_t n_tiles = (hi + kT - 1) / kT;  // tiles [lo/kT, n_tiles) of this launch
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -680,6 +698,24 @@ __global__ __launch_bounds__(64 * atmos_waves<C>(), RAVG ? FCX_RAVG_ATMOS_BLOCKS
     if (j0 < n)
       process<C, true, VAR, NT, R, TM, RAVG>(P, corr_m, j0, emit,
                                              AccLds<C, R>{reinterpret_cast<R *>(wp + emit.s), kR});
+    if constexpr (kXF) {  // the weights row of the fp32 fluxes (dead cells: weight 0)
+#pragma unroll
+      for (int h = 0; h < C / 2; ++h)
+        *reinterpret_cast<d2 *>(wp + xrows_doubles<C>() + emit.s + 2 * h) = d2{emit.w[2 * h], emit.w[2 * h + 1]};
+    }
+    // cell e of the tile added to a segment sum, in link order: its products w * x
+    auto add_cell = [&](double *acc, int e) {
+      if constexpr (kXF) {
+        const float *xr = reinterpret_cast<const float *>(wp);
+        const double we = wp[xrows_doubles<C>() + lds_slot(e)];
+#pragma unroll
+        for (int k = 0; k < kFusedFields; ++k) acc[k] = acc[k] + we * (double)xr[k * kT + e];
+      } else {
+        const double *q = wp + lds_slot(e);
+#pragma unroll
+        for (int k = 0; k < kFusedFields; ++k) acc[k] = acc[k] + q[k * kR];
+      }
+    };
     // segment starts: cell C*l+i begins a segment when its atmosphere cell differs from the
     // previous cell's (the first cell past the grid end also "starts", which ends the last
     // real segment)
@@ -705,11 +741,7 @@ __global__ __launch_bounds__(64 * atmos_waves<C>(), RAVG ? FCX_RAVG_ATMOS_BLOCKS
       double acc[kFusedFields];
 #pragma unroll
       for (int k = 0; k < kFusedFields; ++k) acc[k] = 0.0;
-      for (int e = c; e < end; ++e) {
-        const double *q = wp + lds_slot(e);
-#pragma unroll
-        for (int k = 0; k < kFusedFields; ++k) acc[k] = acc[k] + q[k * kR];
-      }
+      for (int e = c; e < end; ++e) add_cell(acc, e);
       segment_done<R>(af, tile, a[i], acc, end == kT && next_a == a[i]);
     }
     // hand-off: the segment the previous tile carried into this one is continued here, from
@@ -720,11 +752,7 @@ __global__ __launch_bounds__(64 * atmos_waves<C>(), RAVG ? FCX_RAVG_ATMOS_BLOCKS
       for (int q = 0; q < C; ++q) end = min(end, C * first_bit(m[q]) + q);
       double acc[kFusedFields];
       take_carry(af, tile - 1, acc);
-      for (int e = 0; e < end; ++e) {
-        const double *q = wp + lds_slot(e);
-#pragma unroll
-        for (int k = 0; k < kFusedFields; ++k) acc[k] = acc[k] + q[k * kR];
-      }
+      for (int e = 0; e < end; ++e) add_cell(acc, e);
       segment_done<R>(af, tile, a[0], acc, end == kT && next_a == a[0]);
     }
     wave_sync();  // every lane is done reading before the next tile overwrites the region
