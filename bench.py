@@ -33,6 +33,9 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 METRIC = "exchange-grid Mcells/s per coupling step; achieved HBM GB/s vs MI355X peak"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md chip-level parameters)
 VARIANTS = ("CCLM", "MOM5", "RCO")
+MIN_WARMUP_S = 0.15  # back-to-back device work before the timed steps, whatever --warmup says
+WARMUP_BLOCK = 10    # warm-up steps between two synchronisations
+COLD_IDLE_S = 0.5    # idle gap before the cold step
 
 
 def parse():
@@ -55,6 +58,12 @@ def parse():
     p.add_argument("--atmos", type=int, default=1,
                    help="exchange->atmosphere accumulation (+ one RCCL all-reduce when N>1)")
     p.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL)")
+    p.add_argument("--collective", choices=("rccl", "torch"), default="rccl",
+                   help="N > 1: the boundary all-reduce through libfcx's RCCL communicator (default) or "
+                        "torch.distributed (rehearsals)")
+    p.add_argument("--config4", type=int, default=40_000_000,
+                   help="also time config 4's fixed grid of this many cells sharded over the ranks "
+                        "(strong scaling, a 'config4' sub-object); 0 = off")
     p.add_argument("--same-device", action="store_true",
                    help="rehearsal only: every rank on GPU 0 (with --backend gloo on a 1-GPU box)")
     p.add_argument("--max-blocks", type=int, default=None,
@@ -124,7 +133,10 @@ def cpu_all_cores(args, variants):
     import oracle_lib
     from fcx.synthetic import build_case, inputs_for_bench
 
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    # the box's CPU share: OMP_NUM_THREADS is set to it on the GPU box (16 of the machine's
+    # cores per GPU); without it, every CPU of this process's affinity set
+    affinity = len(os.sched_getaffinity(0))
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or affinity
     n = args.cpu_cells_mt
     data = inputs_for_bench(n)
     cases = [build_case(v, n=n, T=args.types, bias=args.bias, data=data if args.types == 1 else None)
@@ -143,6 +155,9 @@ def cpu_all_cores(args, variants):
         if el >= args.cpu_seconds / 2 and reps >= 2:
             break
     return {"value": cells / el / 1e6, "unit": "Mcells/s", "cores": threads, "kind": "port",
+            "cores_note": (f"OMP_NUM_THREADS={threads}: the CPU share of this GPU's box "
+                           f"(process affinity set: {affinity} CPUs)" if threads != affinity
+                           else "every CPU of the process affinity set"),
             "sample": f"{reps} coupling steps x {len(variants)} variants over {n} cells, OpenMP "
                       f"APPLE ranges on {threads} threads, {el:.1f} s"}
 
@@ -160,6 +175,68 @@ def relaunch(n):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
     return subprocess.call(cmd)
+
+
+def measure(wl, args, world, dist, comm, steps, warmup, t_base=0, cold=False):
+    """Warm-up (at least `warmup` steps and MIN_WARMUP_S of device work), then EXACTLY
+    `steps` timed steps bracketed by barrier + synchronize, max over ranks.  A step is
+    fcx_run of every variant's engine plus, for N > 1, the ONE all-reduce of the boundary
+    slots of all variants (libfcx's RCCL communicator) and their finish."""
+    import torch
+
+    stream = wl.stream
+
+    def step(t, events=None):
+        wl.run(t, events)
+        if comm is not None:
+            comm.atmos_allreduce(wl.engines)  # the one collective of the step (RCCL over xGMI)
+
+    # the timed steps' events exist before the warm-up starts: nothing host-side sits between
+    # the warm-up and the timed region (an idle GPU drops its clocks, DESIGN.md section 7)
+    ev = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in wl.engines] for _ in range(steps)]
+    step(t_base)  # builds the engines' plans
+    torch.cuda.synchronize()
+    cold_ms = None
+    if cold:
+        # cold step: one step after an idle gap, as a coupled model runs its flux step
+        # between the other components' steps
+        if world > 1:
+            dist.barrier()
+        time.sleep(COLD_IDLE_S)
+        t_c = time.perf_counter()
+        step(t_base)
+        torch.cuda.synchronize()
+        cold_ms = (time.perf_counter() - t_c) * 1e3
+    # warm-up: the clocks reach steady state after ~40 ms of load; a short warm-up timed the
+    # ramp (34.7 Gcells/s with 5 steps against 37.5 at steady state, round 1)
+    warm, t_w = 0, time.perf_counter()
+    while True:
+        for _ in range(WARMUP_BLOCK):
+            step(t_base + warm * 3600)
+            warm += 1
+        torch.cuda.synchronize()
+        if warm >= warmup and time.perf_counter() - t_w >= MIN_WARMUP_S:
+            break
+    warmup_s = time.perf_counter() - t_w
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        step(t_base + k * 3600, ev[k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = np.array([[a.elapsed_time(b) for (a, b) in row] for row in ev])  # [steps][variant]
+    t_max = elapsed
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=wl.dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t_max = float(tt.item())
+    del stream
+    return {"t_max": t_max, "kern_ms": kern_ms, "cold_ms": cold_ms, "warm": warm, "warmup_s": warmup_s}
 
 
 def main():
@@ -183,119 +260,48 @@ def main():
         else:
             dist.init_process_group(args.backend)
 
-    from fcx.basic import PHASE_ALL, PHASE_NORMAL
-    from fcx.engine import Engine
-    from fcx.parallel import PeriodicAtmosMap, apple_range
-    from fcx.synthetic import BASE_SEED, as_dtype, build_case, inputs_for_bench
+    from fcx.workload import Workload
     sys.path.insert(0, os.path.join(ROOT, "components.flux_calculator_amd", "bench"))
     from pmc_traffic import traffic_key
 
     f32 = args.precision == "f32"
+    # the library's own RCCL communicator for the boundary exchange (N > 1); the unique id is
+    # broadcast over torch.distributed.  --backend gloo (same-device rehearsals on one GPU,
+    # where RCCL refuses two ranks per device) keeps torch's all-reduce of the slots instead.
+    comm = None
+    if world > 1 and args.collective == "rccl" and not args.same_device:
+        from fcx.comm import Comm
 
-    # this rank's APPLE range of the global grid (decomp_def.F90:23-31): weak scaling,
-    # every rank owns args.cells cells; the seed follows the global offset
-    if args.global_cells:  # config 4: one fixed grid, decomp_def.F90 ranges
-        n_global = args.global_cells
-        offset, n = apple_range(n_global, rank, world)
-    else:  # weak scaling: every rank owns args.cells cells of a grid of world * cells
-        n = args.cells
-        n_global = n * world
-        offset, size = apple_range(n_global, rank, world)
-        assert size == n
-    host = inputs_for_bench(n, seed=BASE_SEED + offset)
-    if args.caller_device:  # the caller's contiguous device arrays, shared by the variants
-        data = {k: torch.as_tensor(v).to(dev) for k, v in host.items()}
-        if f32:  # inputs rounded once; every variant's case shares them
-            data = {k: v.float() for k, v in data.items()}
-        case_dev = dev
-        del host
-    else:  # host arrays: every engine owns its device mirrors, uploaded before the timing
-        data, case_dev = host, None
-    stream = torch.cuda.current_stream(dev)
+        comm = Comm.from_torch(gpu)
 
-    # exchange -> atmosphere accumulation of the six fluxes sent to the atmosphere; the
-    # first/last local atmosphere cells shared with the neighbour ranks are completed by
-    # ONE all-reduce per step over all variants' boundary slots
-    atm_fields = (("MEVA", 1), ("HLAT", 1), ("HSEN", 1), ("RBBR", 1), ("UMOM", 2), ("VMOM", 3))
-    la = PeriodicAtmosMap().local(offset, n, rank, world, n_global) if args.atmos else None
-    nb, stride = max(world - 1, 0), len(atm_fields)
-    shared = torch.zeros(max(len(variants) * nb * stride, 1), dtype=torch.float64, device=dev)
-    cases, engines, atm_outs = [], [], []
-    for i, v in enumerate(variants):
-        c = build_case(v, n=n, T=args.types, bias=args.bias, device=case_dev,
-                       data=data if args.types == 1 else None)
-        if f32:
-            c = as_dtype(c, "float32")
-        atmos = None
-        if la is not None:
-            outs = {name: (torch.empty(max(la.n_atmos, 1), dtype=torch.float32 if f32 else torch.float64,
-                                       device=dev) if case_dev is not None
-                           else np.empty(max(la.n_atmos, 1), dtype=np.float32 if f32 else np.float64))
-                    for name, _ in atm_fields}
-            atm_outs.append(outs)
-            # OASIS sends the type-0 fields ('S A xxxx 00'): with several surface types those
-            # are the averages over the types, with one type the type-1 fluxes themselves
-            s0 = 0 if args.types >= 2 else 1
-            atmos = {"local": la, "fields": [(PHASE_NORMAL, s0, g, name, outs[name]) for name, g in atm_fields],
-                     "shared": (shared[i * nb * stride:], stride) if nb else None}
-        e = Engine(c.lf, c.num_surface_types, c.methods, corrections=c.corrections,
-                   averages=c.averages, device=gpu, stream=stream.cuda_stream, atmos=atmos,
-                   # per-kernel times come from the bench's own events on the same stream;
-                   # the engine's internal ones would add a second event pair per launch
-                   # (measured +2.5 % per step, components.flux_calculator_amd/bench/event_probe.py)
-                   # host-bound: no page-locking (the inputs are uploaded once, not per step)
-                   options={"atmos_in_run": 0, "timing": 0, "pin_host": 0, "tiled_layout": args.tiled, "nontemporal": args.nontemporal,
-                            **({"max_blocks": args.max_blocks} if args.max_blocks is not None else {})})
-        if case_dev is None:
-            e.upload(PHASE_ALL)  # inputs resident in HBM before the timed region
-        cases.append(c)
-        engines.append(e)
+    class TorchCollective:  # rehearsal only
+        def atmos_allreduce(self, engines):
+            dist.all_reduce(wl.shared)
+            wl.finish()
+
+    coll = comm if comm is not None else (TorchCollective() if world > 1 else None)
+
+    engine_options = {"tiled_layout": args.tiled, "nontemporal": args.nontemporal}
+    if args.max_blocks is not None:
+        engine_options["max_blocks"] = args.max_blocks
+    # this rank's APPLE range (decomp_def.F90:23-31): weak scaling (every rank owns args.cells
+    # cells of a grid of world * cells) or a fixed global grid (--global-cells, strong)
+    n_global = args.global_cells if args.global_cells else args.cells * world
+    wl = Workload(n_global, rank, world, variants, types=args.types, bias=args.bias, precision=args.precision,
+                  atmos=bool(args.atmos), caller_device=args.caller_device, device=gpu,
+                  stream=torch.cuda.current_stream(dev), engine_options=engine_options)
+    n, la = wl.n, wl.la
     torch.cuda.synchronize()
-    layout = engines[0].device_layout()
+    layout = wl.engines[0].device_layout()
     # algorithmic bytes of one fcx_run: every distinct field array read once / written once,
     # plus (fused accumulation) 4+8 B/cell of atmosphere index and weight and the outputs
-    alg_bytes = [e.algorithmic_bytes(PHASE_ALL) for e in engines]
-
-    def step(t, events=None):
-        for i, e in enumerate(engines):
-            if events is not None:
-                events[i][0].record(stream)
-            e.run(PHASE_ALL, t)
-            if events is not None:
-                events[i][1].record(stream)
-            if la is not None:
-                e.run_atmos(PHASE_ALL)
-        if la is not None and world > 1:
-            dist.all_reduce(shared)  # the one collective of the step (RCCL over xGMI)
-            for e in engines:
-                e.atmos_finish()
+    alg_bytes = wl.alg_bytes
 
     # config 5 (--bias): hourly steps whose timed half crosses 1961-01-31 -> 02-01, so the
     # bias month slice changes inside the timed region (init_date 19610101)
     t_base = 31 * 86400 - 3600 * (args.steps // 2) if args.bias else 0
-    for w in range(args.warmup):
-        step(t_base + w * 3600)
-    torch.cuda.synchronize()
-
-    ev = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in engines] for _ in range(args.steps)]
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        step(t_base + k * 3600, ev[k])
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    kern_ms = np.array([[a.elapsed_time(b) for (a, b) in row] for row in ev])  # [steps][variant]
-
-    t_max = elapsed
-    if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        t_max = float(tt.item())
+    m = measure(wl, args, world, dist, coll, args.steps, args.warmup, t_base, cold=True)
+    t_max, kern_ms = m["t_max"], m["kern_ms"]
     ms_per_step = t_max / args.steps * 1e3
     cells_per_step = n_global * len(variants)
     value = cells_per_step * args.steps / t_max / 1e6
@@ -312,13 +318,15 @@ def main():
     # the accumulation runs inside the flux kernel (T = 1, or T >= 2 with the register averages
     # in fp64) unless a grid-stride cap is set; otherwise it is its own kernel after it
     fused = la is not None and (args.max_blocks is None or args.max_blocks <= 0) and (args.types == 1 or not f32)
-    traffic = None
+    traffic, traffic_source = None, None
     tfile = os.path.join(ROOT, "profiles", "traffic.json")
     if os.path.exists(tfile):
         try:
             t = json.load(open(tfile))
             # the timed launch carries the accumulation only when it is fused (fp64)
             traffic = t.get(traffic_key(variants[dom], n, args.types, args.bias, fused, args.precision))
+            if traffic is not None:
+                traffic_source = t.get("_source")
         except Exception:
             traffic = None
 
@@ -330,6 +338,10 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 4),
+        "warmup_run": {"steps": m["warm"], "seconds": round(m["warmup_s"], 3),
+                       "rule": f"at least --warmup steps and at least {MIN_WARMUP_S} s of device work"},
+        "timed_ms": round(t_max * 1e3, 3),
+        "cold_step_ms": round(m["cold_ms"], 4),
         "higher_is_better": True,
         "scaling": "strong" if args.global_cells else "weak",
         "vs_baseline": None,
@@ -348,7 +360,7 @@ def main():
             "surface_types": args.types,
             "bias_corrections": bool(args.bias),
             "grids": "u/v grids = t grid",
-            "field_layout": ("caller's contiguous device arrays" if case_dev is not None else
+            "field_layout": ("caller's contiguous device arrays" if args.caller_device else
                              "engine-owned mirrors, " + (f"tile-blocked ({layout[0]}-cell tiles, tile stride "
                                                          f"{layout[1]} elements)" if layout[1] > layout[0]
                                                          else "contiguous")),
@@ -356,6 +368,8 @@ def main():
                            + (f", REHEARSAL: all ranks on GPU 0 over {args.backend}" if args.same_device else ""),
             "atmos_accumulation": (f"6 fluxes -> {la.n_atmos} atmosphere cells per GPU (1 per ~4 "
                                    "exchange cells), one all-reduce of the shared boundary cells per step"
+                                   + (" (libfcx RCCL communicator)" if comm is not None else
+                                      " (torch.distributed, rehearsal)" if world > 1 else " (none needed at N=1)")
                                    if la is not None else "off"),
         },
         "roofline": {
@@ -366,11 +380,43 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic,
+            "traffic_source": traffic_source,
             "alg_bytes_per_launch": int(alg_bytes[dom]),
             "mean_kernel_ms": round(float(mean_ms[dom]), 4),
         },
         "kernels": per_variant,
     }
+    wl.close()
+    del wl
+    torch.cuda.synchronize()
+
+    # config 4 at this N: the fixed 40M-cell grid over the same ranks (strong scaling)
+    if args.config4 and not args.global_cells:
+        w4 = Workload(args.config4, rank, world, variants, types=1, precision=args.precision,
+                      atmos=bool(args.atmos), device=gpu, stream=torch.cuda.current_stream(dev),
+                      engine_options=engine_options)
+        wl = w4
+        m4 = measure(w4, args, world, dist, coll if comm is None else comm, args.steps, args.warmup)
+        k4 = m4["kern_ms"].mean(axis=0)
+        d4 = int(np.argmax(k4))
+        out["config4"] = {
+            "workload": "config 4: fixed synthetic grid sharded by APPLE ranges over the ranks (strong scaling), "
+                        "CCLM+MOM5+RCO fused kernels + accumulation, one all-reduce of the boundary slots per step",
+            "cells_global": args.config4,
+            "cells_per_gpu": w4.n,
+            "value": round(args.config4 * len(variants) * args.steps / m4["t_max"] / 1e6, 1),
+            "unit": "Mcells/s",
+            "ms_per_step": round(m4["t_max"] / args.steps * 1e3, 4),
+            "scaling": "strong",
+            "steps": args.steps,
+            "warmup_steps_run": m4["warm"],
+            "dominant_kernel_ms": round(float(k4[d4]), 4),
+            "frac": round(w4.alg_bytes[d4] / (k4[d4] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+        }
+        w4.close()
+        del w4, wl
+        torch.cuda.synchronize()
+
     if rank == 0 and world == 1 and not args.no_cpu:
         cb = cpu_baseline(args, variants)
         out["cpu_baseline"] = cb
@@ -378,8 +424,8 @@ def main():
         out["host_cpu"] = host_cpu()
     if rank == 0:
         print(json.dumps(out), flush=True)
-    for e in engines:
-        e.close()
+    if comm is not None:
+        comm.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -108,10 +108,20 @@ def main():
         e.close()
 
     # ---- host-bound: fcx_step per variant (upload, run, download, synchronise)
-    for mode, opts in (("host_mirrors", {"zero_copy": 0}), ("host_zero_copy", {"zero_copy": 1})):
+    # host_mirrors: caller heap arrays, device mirrors (the default for heap arrays);
+    # host_zero_copy: caller heap arrays registered and used in place (FCX_OPT_ZERO_COPY=1);
+    # host_library_arrays: arrays from fcx_host_malloc, used in place by default (auto)
+    from fcx.host_alloc import Arena
+
+    for mode, opts, lib_arrays in (("host_mirrors", {"zero_copy": 0}, False),
+                                   ("host_zero_copy", {"zero_copy": 1}, False),
+                                   ("host_library_arrays", {}, True)):
         hb = {}
         for v in VARIANTS:
             c = build_case(v, n=n, T=1, bias=bool(a.bias), data=host)
+            arena = Arena()
+            if lib_arrays:
+                arena.adopt(c.lf)
             e = Engine(c.lf, 1, c.methods, corrections=c.corrections, options=opts)
             e.set_option("timing", 0)
             for k in range(50):
@@ -125,8 +135,10 @@ def main():
             e.run(PHASE_ALL, 0)
             e.synchronize()
             kms = e.last_kernel_ms()
+            zc = e.zero_copy_bytes()
             e.close()
-            hb[v] = {"us_per_step_median": round(float(np.median(ts)) * 1e6, 1),
+            arena.close()
+            hb[v] = {"zero_copy_bytes": zc,"us_per_step_median": round(float(np.median(ts)) * 1e6, 1),
                      "us_per_step_p90": round(float(np.percentile(ts, 90)) * 1e6, 1),
                      "kernel_us": round(kms * 1e3, 1)}
         out[mode] = hb

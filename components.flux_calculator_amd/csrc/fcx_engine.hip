@@ -54,7 +54,8 @@ struct Buffer {
   double *host = nullptr;  // caller array (nullptr for device-bound)
   double *dev = nullptr;   // device memory (engine pool or caller's)
   int64_t n = 0;
-  bool external = false;   // caller-owned device memory
+  bool external = false;   // caller-owned device memory (or a host array used in place)
+  bool in_place = false;   // a host array the kernels use through its mapped address
 };
 
 struct Csr {
@@ -74,6 +75,7 @@ struct Plan {
   bool atm_fused = false;          // exchange -> atmosphere accumulation inside the launch
   AtmosFused af{};
   int atm_nf = 0;
+  int atm_phase = 0;               // the phase whose fields the fused accumulation writes
 };
 
 int var0(int var) { return var - 1; }
@@ -135,10 +137,18 @@ struct fcx_engine {
   std::vector<AtmosField> atm_fields;
   double *atm_shared = nullptr;
   int32_t atm_nb = 0, atm_stride = 0, atm_left = -1, atm_right = -1;
+  bool own_shared = false;        // fcx_set_atmos_boundaries: the engine allocates the slots
+  double *atm_shared_own = nullptr;
+  struct fcx_comm *comm = nullptr;  // fcx_set_comm: the engine completes its boundary slots
+  bool atm_done = false;            // the accumulation of the current run has been launched
+  bool exchanged = false;           // ... and its boundary slots completed (comm attached)
   void *atm_pool = nullptr;
   int64_t atm_out_tpad = 0;  // tile-blocked atmosphere outputs (kernels: tiled(a, atm_out_tpad))
   bool atmos_in_run = true;
   bool atm_done_fused = false;  // the last fcx_run already accumulated the atmosphere fields
+  int last_phase = FCX_PHASE_ALL;     // phase of the last fused accumulation
+  int64_t handoff_recoveries = 0;     // fused accumulations recomputed after a hand-off timeout
+  bool test_handoff_timeout = false;  // FCX_OPT_TEST_HANDOFF_TIMEOUT
   // exchange -> model remaps (SCRIP links, CSR by destination in link order)
   struct RemapField {
     int phase, s, g, var;
@@ -164,7 +174,9 @@ struct fcx_engine {
   // pipeline chunks, where per-array copy calls dominate the step, and only when page-locking
   // is allowed)
   int zero_copy = 2;
-  bool zc_active = false;
+  bool zc_active = false;        // some field array is used in place (host-mapped)
+  bool zc_mapped_flags = false;  // caller ranges registered mapped (FCX_OPT_ZERO_COPY = 1)
+  int64_t zc_bytes = 0;          // bytes of host arrays used in place
   // ev0/ev1 around every run (fcx_last_kernel_ms).  Off by default: on the 32K-cell grid the
   // two event records per run made the 3-variant step 41 us instead of 16.5 us
   bool timing = false;
@@ -276,6 +288,7 @@ extern "C" int fcx_destroy(fcx_engine *e) {
   (void)hipFree(e->d_atm_col);
   (void)hipFree(e->d_atm_w);
   (void)hipFree(e->atm_pool);
+  (void)hipFree(e->atm_shared_own);
   for (auto &r : e->remaps) {
     (void)hipFree(r.d_row);
     (void)hipFree(r.d_col);
@@ -570,7 +583,8 @@ static void plan_fused_atmos(fcx_engine *e, Plan &pl, uint32_t stages, int phase
   int nf = 0;
   const bool multi = e->T >= 2;
   if (multi && !pl.host.ravg_on) return;  // several types: only register averages are fused
-  for (auto &f : e->atm_fields) {
+  for (size_t fi = 0; fi < e->atm_fields.size(); ++fi) {
+    const auto &f = e->atm_fields[fi];
     if (!(f.phase & phase)) continue;
     const int b = e->buf(f.s, f.g, f.var);
     int k = -1;
@@ -580,6 +594,7 @@ static void plan_fused_atmos(fcx_engine *e, Plan &pl, uint32_t stages, int phase
       if (k < 0 || af.out[k]) return;
       af.out[k] = f.out_dev;
       af.x[k] = e->bufs[b].dev;
+      af.scol[k] = (int32_t)fi;
       ++nf;
       continue;
     }
@@ -596,6 +611,7 @@ static void plan_fused_atmos(fcx_engine *e, Plan &pl, uint32_t stages, int phase
     if (k < 0 || af.out[k]) return;  // not in registers (or twice): separate kernel
     af.out[k] = f.out_dev;
     af.x[k] = e->bufs[b].dev;
+    af.scol[k] = (int32_t)fi;
     ++nf;
   }
   if (nf == 0) return;
@@ -613,6 +629,7 @@ static void plan_fused_atmos(fcx_engine *e, Plan &pl, uint32_t stages, int phase
   af.out_tpad = e->atm_out_tpad;
   pl.af = af;
   pl.atm_nf = nf;
+  pl.atm_phase = phase;
   pl.atm_fused = true;
 }
 
@@ -895,6 +912,64 @@ static int get_plan(fcx_engine *e, uint32_t stages, int avg_phases, Plan **pl) {
   return FCX_OK;
 }
 
+// Library-owned page-locked host memory (fcx_host_malloc).  A host that allocates its
+// local_field arrays here hands the engine memory the library itself locked and mapped at
+// allocation, page-exclusive by construction and alive until fcx_host_free: the kernels can
+// use it in place (zero-copy, the default for small grids) and the copies of large grids
+// DMA from it directly, with no registration of caller memory at all.
+namespace {
+
+struct HostBlock {
+  size_t bytes;
+  void *dev;  // device-visible address of the block
+};
+std::mutex g_blk_mu;
+std::map<uintptr_t, HostBlock> g_blocks;  // keyed by the block's host address
+
+// device-visible address of [h, h + bytes) if it lies inside one fcx_host_malloc block
+void *lib_block_device_ptr(const void *h, size_t bytes) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(h);
+  std::lock_guard<std::mutex> lk(g_blk_mu);
+  auto it = g_blocks.upper_bound(a);
+  if (it == g_blocks.begin()) return nullptr;
+  --it;
+  if (a + bytes > it->first + it->second.bytes) return nullptr;
+  return reinterpret_cast<char *>(it->second.dev) + (a - it->first);
+}
+
+}  // namespace
+
+extern "C" int fcx_host_malloc(size_t bytes, void **ptr) {
+  if (!ptr) return fail(FCX_E_ARG, "ptr is NULL");
+  *ptr = nullptr;
+  void *h = nullptr, *d = nullptr;
+  hipError_t err = hipHostMalloc(&h, bytes ? bytes : 1, hipHostMallocMapped);
+  if (err != hipSuccess) return fail(FCX_E_NOMEM, "hipHostMalloc(%zu): %s", bytes, hipGetErrorString(err));
+  err = hipHostGetDevicePointer(&d, h, 0);
+  if (err != hipSuccess || !d) {
+    (void)hipHostFree(h);
+    return fail(FCX_E_HIP, "hipHostGetDevicePointer: %s", hipGetErrorString(err));
+  }
+  {
+    std::lock_guard<std::mutex> lk(g_blk_mu);
+    g_blocks[reinterpret_cast<uintptr_t>(h)] = HostBlock{bytes ? bytes : 1, d};
+  }
+  *ptr = h;
+  return FCX_OK;
+}
+
+extern "C" int fcx_host_free(void *ptr) {
+  if (!ptr) return FCX_OK;
+  {
+    std::lock_guard<std::mutex> lk(g_blk_mu);
+    auto it = g_blocks.find(reinterpret_cast<uintptr_t>(ptr));
+    if (it == g_blocks.end()) return fail(FCX_E_ARG, "%p was not allocated by fcx_host_malloc", ptr);
+    g_blocks.erase(it);
+  }
+  HIP_TRY(hipHostFree(ptr));
+  return FCX_OK;
+}
+
 // Process-wide page-lock registry.  The runtime locks whole pages, so two registrations
 // that touch one page -- two arrays of one engine, or arrays of two live engines, sharing a
 // page -- would tear down each other's lock when either is unregistered (the runtime aborts
@@ -972,13 +1047,16 @@ static void pin_host_arrays(fcx_engine *e) {
     const uintptr_t a = reinterpret_cast<uintptr_t>(p);
     r.push_back({a, a + bytes});
   };
+  auto add_own = [&](const void *p, size_t bytes) {  // library blocks are locked already
+    if (p && !lib_block_device_ptr(p, bytes)) add(p, bytes);
+  };
   for (auto &bf : e->bufs)
-    if (!bf.external) add(bf.host, (size_t)bf.n * e->esize);
+    if (!bf.external) add_own(bf.host, (size_t)bf.n * e->esize);
   for (auto &f : e->atm_fields)
-    if (!f.external) add(f.out_host, (size_t)std::max<int64_t>(e->n_atmos, 0) * e->esize);
+    if (!f.external) add_own(f.out_host, (size_t)std::max<int64_t>(e->n_atmos, 0) * e->esize);
   for (auto &rm : e->remaps)
     for (auto &f : rm.fields)
-      if (!f.external) add(f.out_host, (size_t)rm.n_dst * e->esize);
+      if (!f.external) add_own(f.out_host, (size_t)rm.n_dst * e->esize);
   std::sort(r.begin(), r.end());
   const uintptr_t sh = page_shift();
   std::vector<std::pair<uintptr_t, uintptr_t>> m;
@@ -988,7 +1066,7 @@ static void pin_host_arrays(fcx_engine *e) {
     else
       m.push_back(x);
   }
-  const unsigned flags = e->zc_active ? hipHostRegisterMapped : hipHostRegisterDefault;
+  const unsigned flags = e->zc_mapped_flags ? hipHostRegisterMapped : hipHostRegisterDefault;
   for (auto &x : m)
     if (pin_range(x.first, x.second, flags))
       e->pinned.push_back({reinterpret_cast<char *>(x.first), x.second - x.first});
@@ -999,17 +1077,20 @@ static void unpin_host_arrays(fcx_engine *e) {
   e->pinned.clear();
 }
 
-// Zero-copy (FCX_OPT_ZERO_COPY): a host array inside a page-locked range is used by the
-// kernels in place through its device-visible address -- no device mirror, no copy call;
-// the cells kernel streams it over the host link.  For the latency-bound small grids this
-// replaces ~17 copy calls per step by one launch.  Arrays whose range was not registered
-// keep a mirror.
-static void map_host_arrays(fcx_engine *e) {
-  auto mapped = [&](void *host) -> void * {
+// Zero-copy (FCX_OPT_ZERO_COPY): a host array is used by the kernels in place through its
+// device-visible address -- no device mirror, no copy call; the cells kernel streams it over
+// the host link.  For the latency-bound small grids this replaces ~17 copy calls per step
+// by one launch.  Candidates: arrays inside fcx_host_malloc blocks (auto and on), and with
+// FCX_OPT_ZERO_COPY = 1 also caller arrays inside this engine's page-locked ranges.  Every
+// other array keeps a mirror.  Returns the number of arrays used in place.
+static int map_host_arrays(fcx_engine *e, bool caller_ranges) {
+  auto mapped = [&](void *host, size_t bytes) -> void * {
+    if (void *d = lib_block_device_ptr(host, bytes)) return d;
+    if (!caller_ranges) return nullptr;
     const uintptr_t h = reinterpret_cast<uintptr_t>(host);
     for (auto &r : e->pinned) {
       const uintptr_t a = reinterpret_cast<uintptr_t>(r.first);
-      if (h >= a && h < a + r.second) {
+      if (h >= a && h + bytes <= a + r.second) {
         void *d = nullptr;
         if (hipHostGetDevicePointer(&d, r.first, 0) != hipSuccess || !d) {
           (void)hipGetLastError();
@@ -1020,29 +1101,38 @@ static void map_host_arrays(fcx_engine *e) {
     }
     return nullptr;
   };
+  int count = 0;
   for (auto &bf : e->bufs) {
     if (bf.external || !bf.host) continue;
-    if (void *d = mapped(bf.host)) {
+    if (void *d = mapped(bf.host, (size_t)bf.n * e->esize)) {
       bf.dev = reinterpret_cast<double *>(d);
       bf.external = true;  // the engine neither owns nor copies it
+      bf.in_place = true;
+      e->zc_bytes += bf.n * (int64_t)e->esize;
+      ++count;
       if (reinterpret_cast<uintptr_t>(d) % 16) e->aligned16 = false;
     }
   }
   for (auto &f : e->atm_fields) {
     if (f.external || !f.out_host) continue;
-    if (void *d = mapped(f.out_host)) {
+    if (void *d = mapped(f.out_host, (size_t)std::max<int64_t>(e->n_atmos, 1) * e->esize)) {
       f.out_dev = reinterpret_cast<double *>(d);
       f.external = true;
+      e->zc_bytes += std::max<int64_t>(e->n_atmos, 0) * (int64_t)e->esize;
+      ++count;
     }
   }
   for (auto &rm : e->remaps)
     for (auto &f : rm.fields) {
       if (f.external || !f.out_host) continue;
-      if (void *d = mapped(f.out_host)) {
+      if (void *d = mapped(f.out_host, (size_t)std::max<int64_t>(rm.n_dst, 1) * e->esize)) {
         f.out_dev = reinterpret_cast<double *>(d);
         f.external = true;
+        e->zc_bytes += rm.n_dst * (int64_t)e->esize;
+        ++count;
       }
     }
+  return count;
 }
 
 // Tile-blocked mirrors (FCX_OPT_TILED_LAYOUT).  Every field array is cut into tiles of
@@ -1179,12 +1269,17 @@ extern "C" int fcx_commit(fcx_engine *e) {
   if (e->committed) return FCX_OK;
   if (int r = validate(e)) return r;
   if (int r = gpu_init(e)) return r;
-  // auto: zero-copy exactly where the pipelined step would not apply (grids below two
-  // chunks), i.e. where the step is latency-bound and per-array copies dominate it
+  // Zero-copy.  1: every host array in place (library blocks, and caller arrays page-locked
+  // and mapped here).  2 (auto, default): library blocks in place where the pipelined step
+  // would not apply (grids below two chunks, where the step is latency-bound and per-array
+  // copies dominate it); caller heap arrays always take mirrors (in-place
+  // use of registered caller memory is opt-in).  0: mirrors for everything.
   const int64_t n_big = std::max(e->n[0], std::max(e->n[1], e->n[2]));
-  e->zc_active = e->zero_copy == 1 || (e->zero_copy == 2 && e->pin_host && n_big < 2 * e->min_chunk);
-  if (e->pin_host || e->zc_active) pin_host_arrays(e);
-  if (e->zc_active) map_host_arrays(e);
+  const bool small = n_big < 2 * e->min_chunk;
+  const bool caller_zc = e->zero_copy == 1;
+  e->zc_mapped_flags = caller_zc;
+  if (e->pin_host || caller_zc) pin_host_arrays(e);
+  if (caller_zc || (e->zero_copy == 2 && small)) e->zc_active = map_host_arrays(e, caller_zc) > 0;
   bool any_external = false;
   for (auto &bf : e->bufs) any_external = any_external || bf.external;
   if (e->tiled_opt && !any_external && !e->bufs.empty()) {
@@ -1287,6 +1382,16 @@ extern "C" int fcx_commit(fcx_engine *e) {
         }
     }
   }
+  if (e->own_shared && e->n_atmos >= 0) {  // [n_boundaries][fields] slots, zero on entry
+    const size_t stride = std::max<size_t>(e->atm_fields.size(), 1);
+    const size_t cnt = std::max<size_t>((size_t)e->atm_nb * stride, 1);
+    HIP_TRY(hipMalloc(&e->atm_shared_own, cnt * sizeof(double)));
+    HIP_TRY(hipMemset(e->atm_shared_own, 0, cnt * sizeof(double)));
+    if (e->atm_left >= 0 && e->atm_right >= 0 && e->n_atmos < 2)
+      return fail(FCX_E_UNSUPPORTED, "one atmosphere cell shared on both sides (shard too small)");
+    e->atm_shared = e->atm_nb > 0 ? e->atm_shared_own : nullptr;
+    e->atm_stride = (int32_t)stride;
+  }
   for (auto &rm : e->remaps) {
     for (auto &f : rm.fields)
       if (rm.max_src >= e->n[f.g - 1])
@@ -1354,6 +1459,9 @@ static int launch_plan(fcx_engine *e, Plan *pl, const double *corr_m, int64_t lo
   LaunchConfig lc = e->launch;
   lc.lo = lo;
   lc.hi = hi;
+  // host-mapped fields: plain loads and stores (the non-temporal hint is for HBM streams;
+  // over the host link it buys nothing, and plain stores are the well-trodden path)
+  if (e->zc_active) lc.nontemporal = false;
   if (!e->aligned16) lc.cells_per_thread = 1;
   lc.merged = pl->host.merged_uv != 0;
   lc.variant = (e->specialize && lc.merged) ? pl->variant : 0;
@@ -1380,11 +1488,19 @@ static int launch_plan(fcx_engine *e, Plan *pl, const double *corr_m, int64_t lo
     const int r2 = launch_atmos_fixup(pl->af, pl->host.n_max, e->stream);
     if (r2) return fail(FCX_E_HIP, "atmos_fixup launch: %s", hipGetErrorString((hipError_t)r2));
   }
-  if (fused) e->atm_done_fused = true;
+  if (fused) {
+    e->atm_done_fused = true;
+    e->last_phase = pl->atm_phase;
+    if (e->test_handoff_timeout && pl->af.handoff) {  // test hook: as if a wait had given up
+      HIP_TRY(hipStreamSynchronize(e->stream));
+      __atomic_store_n(e->h_atm_err, 1u, __ATOMIC_RELEASE);
+    }
+  }
   return FCX_OK;
 }
 
 static int regrid_var(fcx_engine *e, int var, int surface_type);
+static int comm_exchange(fcx_engine *e);
 static hipError_t get_atm(const fcx_engine *e, double *host, const double *dev, hipStream_t s);
 static int run_remaps(fcx_engine *e, int phase);
 static int download_remaps(fcx_engine *e, int phase, hipStream_t s);
@@ -1477,10 +1593,12 @@ static AtmosArgs atmos_args(fcx_engine *e, int phase) {
   a.tpad = e->tpad;
   a.out_tpad = e->atm_out_tpad;
   a.vec = a.col == nullptr && e->aligned16;
-  for (auto &f : e->atm_fields) {
+  for (size_t i = 0; i < e->atm_fields.size(); ++i) {
+    const auto &f = e->atm_fields[i];
     if (!(f.phase & phase) || a.nf >= kMaxAtmosFields) continue;
     a.x[a.nf] = e->dptr(f.s, f.g, f.var);
     a.out[a.nf] = f.out_dev;
+    a.scol[a.nf] = (int32_t)i;
     ++a.nf;
   }
   return a;
@@ -1544,6 +1662,7 @@ extern "C" int fcx_run(fcx_engine *e, int phase, int32_t t) {
   if (rc) return rc;
   if (e->timing) HIP_TRY(hipEventRecord(e->ev0, e->stream));
   e->atm_done_fused = false;
+  e->atm_done = e->exchanged = false;
   if (!e->any_regrid) {
     Plan *pl;
     if (int r = get_plan(e, phase_stages(phase), phase, &pl)) return r;
@@ -1564,6 +1683,9 @@ extern "C" int fcx_run(fcx_engine *e, int phase, int32_t t) {
   }
   if (e->atmos_in_run && !e->atm_done_fused)
     if (int r = run_atmos(e, phase)) return r;
+  e->atm_done = e->atmos_in_run || e->atm_done_fused;
+  if (e->atm_done)
+    if (int r = comm_exchange(e)) return r;
   if (int r = run_remaps(e, phase)) return r;
   if (e->timing) HIP_TRY(hipEventRecord(e->ev1, e->stream));
   e->timed = e->timing;
@@ -1609,6 +1731,7 @@ static int step_pipelined(fcx_engine *e, int phase, int32_t t, Plan *pl) {
   }
   if (e->timing) HIP_TRY(hipEventRecord(e->ev0, e->s_in));
   e->atm_done_fused = false;
+  e->atm_done = e->exchanged = false;
   for (int k = 0; k < K; ++k) {
     const int64_t lo = k * per, hi = std::min(n, lo + per);
     const bool last = k == K - 1;
@@ -1624,6 +1747,9 @@ static int step_pipelined(fcx_engine *e, int phase, int32_t t, Plan *pl) {
   }
   if (e->atmos_in_run && !e->atm_done_fused)
     if (int r = run_atmos(e, phase)) return r;
+  e->atm_done = e->atmos_in_run || e->atm_done_fused;
+  if (e->atm_done)
+    if (int r = comm_exchange(e)) return r;
   if (int r = run_remaps(e, phase)) return r;
   HIP_TRY(hipEventRecord(e->ev_comp[K - 1], e->stream));
   HIP_TRY(hipStreamWaitEvent(e->s_out, e->ev_comp[K - 1], 0));
@@ -1661,13 +1787,19 @@ extern "C" int fcx_step(fcx_engine *e, int phase, int32_t t) {
   return fcx_synchronize(e);
 }
 
-// a fused accumulation whose carry hand-off gave up (a flag that never came) has wrong
-// atmosphere values: report it at the next synchronisation
+// A fused accumulation whose carry hand-off gave up (a flag that never came: a producer
+// wave not resident, e.g. another process holding the CUs) left wrong atmosphere values.
+// Recompute them with the separate accumulation kernel over the fluxes the run stored (the
+// same sums in the same order, bit-identical), refresh the host copies, and count it.
 static int check_handoff(fcx_engine *e) {
-  if (e->h_atm_err && __atomic_load_n(e->h_atm_err, __ATOMIC_ACQUIRE)) {
-    *e->h_atm_err = 0;
-    return fail(FCX_E_HIP, "fused atmosphere accumulation: a carry hand-off timed out");
-  }
+  if (!e->h_atm_err || !__atomic_load_n(e->h_atm_err, __ATOMIC_ACQUIRE)) return FCX_OK;
+  *e->h_atm_err = 0;
+  ++e->handoff_recoveries;
+  if (int r = run_atmos(e, e->last_phase)) return r;
+  for (auto &f : e->atm_fields)
+    if ((f.phase & e->last_phase) && !f.external && e->n_atmos > 0)
+      HIP_TRY(get_atm(e, f.out_host, f.out_dev, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
   return FCX_OK;
 }
 
@@ -1799,6 +1931,19 @@ extern "C" int fcx_pinned_bytes(fcx_engine *e, int64_t *bytes) {
   return FCX_OK;
 }
 
+extern "C" int fcx_handoff_recoveries(fcx_engine *e, int64_t *count) {
+  if (!e || !count) return fail(FCX_E_ARG, "NULL argument");
+  *count = e->handoff_recoveries;
+  return FCX_OK;
+}
+
+extern "C" int fcx_zero_copy_bytes(fcx_engine *e, int64_t *bytes) {
+  if (int r = check(e)) return r;
+  if (!bytes) return fail(FCX_E_ARG, "NULL argument");
+  *bytes = e->zc_bytes;
+  return FCX_OK;
+}
+
 extern "C" int fcx_algorithmic_bytes(fcx_engine *e, int phase, int64_t *bytes) {
   if (int r = check(e)) return r;
   if (!bytes || phase < 1 || phase > 3) return fail(FCX_E_ARG, "bad arguments");
@@ -1894,6 +2039,9 @@ extern "C" int fcx_set_option(fcx_engine *e, int option, int64_t value) {
       if (value < 1 || value > 1024) return fail(FCX_E_ARG, "pipeline chunks %lld outside 1..1024", (long long)value);
       e->chunks = (int)value;
       return FCX_OK;
+    case FCX_OPT_TEST_HANDOFF_TIMEOUT:
+      e->test_handoff_timeout = value != 0;
+      return FCX_OK;
     case FCX_OPT_TILED_LAYOUT:
       if (e->committed) return fail(FCX_E_STATE, "tiled_layout is applied at fcx_commit");
       e->tiled_opt = value != 0;
@@ -1975,6 +2123,7 @@ extern "C" int fcx_set_atmos_shared(fcx_engine *e, double *shared, int32_t nb, i
     return fail(FCX_E_ARG, "stride %d < %zu atmosphere fields", stride, e->atm_fields.size());
   if (left >= 0 && right >= 0 && e->n_atmos < 2)
     return fail(FCX_E_UNSUPPORTED, "one atmosphere cell shared on both sides (shard too small)");
+  if (e->own_shared) return fail(FCX_E_STATE, "boundary slots already owned by the engine (fcx_set_atmos_boundaries)");
   e->atm_shared = shared;
   e->atm_nb = nb;
   e->atm_stride = stride;
@@ -1995,8 +2144,11 @@ extern "C" int fcx_atmos_finish(fcx_engine *e) {
 extern "C" int fcx_run_atmos(fcx_engine *e, int phase) {
   if (int r = check(e)) return r;
   if (phase < 1 || phase > 3) return fail(FCX_E_ARG, "phase %d unknown", phase);
-  if (e->atm_done_fused) return FCX_OK;  // done inside the last fcx_run
-  return run_atmos(e, phase);
+  if (!e->atm_done) {  // not done inside the last fcx_run (FCX_OPT_ATMOS_IN_RUN = 0, not fused)
+    if (int r = run_atmos(e, phase)) return r;
+    e->atm_done = true;
+  }
+  return comm_exchange(e);  // no-op without a communicator or once done for this run
 }
 
 // ------------------------------------------------------------------ exchange -> model remaps
@@ -2049,5 +2201,209 @@ extern "C" int fcx_add_remap_field(fcx_engine *e, int32_t remap_id, int phase, i
     f.out_host = out;
   }
   e->remaps[(size_t)remap_id].fields.push_back(f);
+  return FCX_OK;
+}
+
+// ------------------------------------------------------------------ RCCL: the one collective
+//
+// The exchange -> atmosphere accumulation is the only cross-rank step of the path
+// (flux_calculator.F90:1015 oasis_put of the 'S A xxxx 00' fields,
+// create_namcouple.F90:92-98): the partial sums of the atmosphere cells shared by two
+// neighbouring APPLE ranges are completed by ONE all-reduce (sum, fp64) of the boundary
+// slots per step, over xGMI on an MI355X node.  RCCL is bound at run time (dlopen) so that
+// a process that already carries an RCCL -- PyTorch-ROCm ships its own librccl.so -- uses
+// that one, and a Fortran host gets /opt/rocm's; libfcx has no link-time RCCL dependency.
+#include <dlfcn.h>
+#include <rccl/rccl.h>
+
+namespace {
+
+struct RcclApi {
+  bool ok = false;
+  std::string why;
+  ncclResult_t (*GetUniqueId)(ncclUniqueId *) = nullptr;
+  ncclResult_t (*CommInitRank)(ncclComm_t *, int, ncclUniqueId, int) = nullptr;
+  ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+  ncclResult_t (*AllReduce)(const void *, void *, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
+                            hipStream_t) = nullptr;
+  ncclResult_t (*GroupStart)() = nullptr;
+  ncclResult_t (*GroupEnd)() = nullptr;
+  const char *(*GetErrorString)(ncclResult_t) = nullptr;
+};
+
+const RcclApi &rccl() {
+  static RcclApi api = [] {
+    RcclApi a;
+    void *h = dlopen("librccl.so", RTLD_NOW | RTLD_NOLOAD);  // already in the process (torch)
+    if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) {
+      const char *m = dlerror();
+      a.why = m ? m : "librccl.so not found";
+      return a;
+    }
+    bool all = true;
+    auto sym = [&](const char *name) {
+      void *p = dlsym(h, name);
+      if (!p) all = false;
+      return p;
+    };
+    a.GetUniqueId = reinterpret_cast<decltype(a.GetUniqueId)>(sym("ncclGetUniqueId"));
+    a.CommInitRank = reinterpret_cast<decltype(a.CommInitRank)>(sym("ncclCommInitRank"));
+    a.CommDestroy = reinterpret_cast<decltype(a.CommDestroy)>(sym("ncclCommDestroy"));
+    a.AllReduce = reinterpret_cast<decltype(a.AllReduce)>(sym("ncclAllReduce"));
+    a.GroupStart = reinterpret_cast<decltype(a.GroupStart)>(sym("ncclGroupStart"));
+    a.GroupEnd = reinterpret_cast<decltype(a.GroupEnd)>(sym("ncclGroupEnd"));
+    a.GetErrorString = reinterpret_cast<decltype(a.GetErrorString)>(sym("ncclGetErrorString"));
+    a.ok = all;
+    if (!all) a.why = "librccl.so lacks an nccl* entry point";
+    return a;
+  }();
+  return api;
+}
+
+#define RCCL_TRY(expr)                                                                               \
+  do {                                                                                               \
+    ncclResult_t r_ = (expr);                                                                        \
+    if (r_ != ncclSuccess) return fail(FCX_E_HIP, "%s: %s", #expr, rccl().GetErrorString(r_));      \
+  } while (0)
+
+}  // namespace
+
+struct fcx_comm {
+  ncclComm_t comm = nullptr;
+  int nranks = 0, rank = 0, device = 0;
+  std::vector<hipEvent_t> events;  // stream joins of fcx_atmos_allreduce (engines on several streams)
+};
+
+extern "C" int fcx_comm_unique_id(void *id) {
+  if (!id) return fail(FCX_E_ARG, "id is NULL");
+  if (!rccl().ok) return fail(FCX_E_UNSUPPORTED, "RCCL unavailable: %s", rccl().why.c_str());
+  RCCL_TRY(rccl().GetUniqueId(reinterpret_cast<ncclUniqueId *>(id)));
+  return FCX_OK;
+}
+
+extern "C" int fcx_comm_create(int device, int nranks, int rank, const void *id, fcx_comm **out) {
+  if (!out || !id) return fail(FCX_E_ARG, "NULL argument");
+  *out = nullptr;
+  if (nranks < 1 || rank < 0 || rank >= nranks) return fail(FCX_E_ARG, "rank %d of %d", rank, nranks);
+  if (!rccl().ok) return fail(FCX_E_UNSUPPORTED, "RCCL unavailable: %s", rccl().why.c_str());
+  HIP_TRY(hipSetDevice(device));
+  ncclUniqueId uid;
+  std::memcpy(&uid, id, sizeof uid);
+  auto *c = new fcx_comm();
+  c->nranks = nranks;
+  c->rank = rank;
+  c->device = device;
+  const ncclResult_t r = rccl().CommInitRank(&c->comm, nranks, uid, rank);
+  if (r != ncclSuccess) {
+    delete c;
+    return fail(FCX_E_HIP, "ncclCommInitRank(%d of %d): %s", rank, nranks, rccl().GetErrorString(r));
+  }
+  *out = c;
+  return FCX_OK;
+}
+
+extern "C" int fcx_comm_destroy(fcx_comm *c) {
+  if (!c) return FCX_OK;
+  for (hipEvent_t ev : c->events) (void)hipEventDestroy(ev);
+  if (c->comm) (void)rccl().CommDestroy(c->comm);
+  delete c;
+  return FCX_OK;
+}
+
+extern "C" int fcx_comm_allreduce_sum(fcx_comm *c, double *buf, size_t count, void *stream) {
+  if (!c || (count && !buf)) return fail(FCX_E_ARG, "NULL argument");
+  if (!count) return FCX_OK;
+  RCCL_TRY(rccl().AllReduce(buf, buf, count, ncclFloat64, ncclSum, c->comm, reinterpret_cast<hipStream_t>(stream)));
+  return FCX_OK;
+}
+
+// the boundary exchange of one or several engines of this rank: one all-reduce over their
+// boundary slots on the first engine's stream (one call when the engines' slot regions are
+// adjacent in one buffer, else one per engine inside one RCCL group), then fcx_atmos_finish
+// of each engine.  Engines on other streams are joined with events before and after.
+static int atmos_exchange(fcx_comm *c, fcx_engine *const *es, int n) {
+  std::vector<fcx_engine *> v;
+  for (int i = 0; i < n; ++i)
+    if (es[i] && !es[i]->exchanged && es[i]->atm_shared && es[i]->atm_nb > 0 && es[i]->atm_stride > 0)
+      v.push_back(es[i]);
+  if (v.empty()) return FCX_OK;
+  hipStream_t s0 = v[0]->stream;
+  size_t joins = 0;
+  for (auto *e : v) joins += e->stream != s0 ? 2 : 0;
+  while (c->events.size() < joins) {
+    hipEvent_t ev;
+    HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    c->events.push_back(ev);
+  }
+  size_t k = 0;
+  for (auto *e : v)
+    if (e->stream != s0) {  // the all-reduce waits for that engine's accumulation
+      HIP_TRY(hipEventRecord(c->events[k], e->stream));
+      HIP_TRY(hipStreamWaitEvent(s0, c->events[k++], 0));
+    }
+  std::vector<fcx_engine *> byptr(v);
+  std::sort(byptr.begin(), byptr.end(), [](fcx_engine *a, fcx_engine *b) { return a->atm_shared < b->atm_shared; });
+  bool adjacent = true;
+  for (size_t i = 1; i < byptr.size(); ++i)
+    adjacent = adjacent && byptr[i - 1]->atm_shared + (size_t)byptr[i - 1]->atm_nb * byptr[i - 1]->atm_stride ==
+                               byptr[i]->atm_shared;
+  if (adjacent) {
+    size_t count = 0;
+    for (auto *e : byptr) count += (size_t)e->atm_nb * e->atm_stride;
+    RCCL_TRY(rccl().AllReduce(byptr[0]->atm_shared, byptr[0]->atm_shared, count, ncclFloat64, ncclSum, c->comm, s0));
+  } else {
+    RCCL_TRY(rccl().GroupStart());
+    for (auto *e : v) {
+      const ncclResult_t r = rccl().AllReduce(e->atm_shared, e->atm_shared, (size_t)e->atm_nb * e->atm_stride,
+                                              ncclFloat64, ncclSum, c->comm, s0);
+      if (r != ncclSuccess) {
+        (void)rccl().GroupEnd();
+        return fail(FCX_E_HIP, "ncclAllReduce: %s", rccl().GetErrorString(r));
+      }
+    }
+    RCCL_TRY(rccl().GroupEnd());
+  }
+  for (auto *e : v) {
+    if (e->stream != s0) {  // the finish of that engine waits for the all-reduce
+      HIP_TRY(hipEventRecord(c->events[k], s0));
+      HIP_TRY(hipStreamWaitEvent(e->stream, c->events[k++], 0));
+    }
+    if (int r = fcx_atmos_finish(e)) return r;
+    e->exchanged = true;
+  }
+  return FCX_OK;
+}
+
+extern "C" int fcx_atmos_allreduce(fcx_comm *c, fcx_engine *const *engines, int n_engines) {
+  if (!c || n_engines < 0 || (n_engines && !engines)) return fail(FCX_E_ARG, "bad arguments");
+  for (int i = 0; i < n_engines; ++i)
+    if (int r = check(engines[i])) return r;
+  return atmos_exchange(c, engines, n_engines);
+}
+
+extern "C" int fcx_set_comm(fcx_engine *e, fcx_comm *c) {
+  if (!e) return fail(FCX_E_ARG, "NULL engine");
+  e->comm = c;
+  return FCX_OK;
+}
+
+// the engine's own boundary exchange after its accumulation (fcx_set_comm)
+static int comm_exchange(fcx_engine *e) {
+  if (!e->comm) return FCX_OK;
+  fcx_engine *one[1] = {e};
+  return atmos_exchange(e->comm, one, 1);
+}
+
+extern "C" int fcx_set_atmos_boundaries(fcx_engine *e, int32_t n_boundaries, int32_t left, int32_t right) {
+  if (!e) return fail(FCX_E_ARG, "NULL engine");
+  if (e->committed) return fail(FCX_E_STATE, "engine already committed");
+  if (n_boundaries < 0 || left >= n_boundaries || right >= n_boundaries || left < -1 || right < -1)
+    return fail(FCX_E_ARG, "boundaries: %d slots, left %d, right %d", n_boundaries, left, right);
+  e->own_shared = true;
+  e->atm_nb = n_boundaries;
+  e->atm_left = left;
+  e->atm_right = right;
   return FCX_OK;
 }

@@ -129,6 +129,9 @@ struct AtmosArgs {
   int64_t out_tpad;        // layout of out: the engine's tiled atmosphere pool, or 0
   int32_t vec;             // col == nullptr and every x 16-B aligned: vector staging loads
   int32_t pad;
+  int32_t scol[kMaxAtmosFields];  // column of field f in the shared boundary slots: the
+                                  // field's registration index (fcx_add_atmos_field order),
+                                  // the same for every phase and for the fused kernel
 };
 int launch_atmos(const AtmosArgs &a, void *stream);
 
@@ -156,6 +159,7 @@ struct AtmosFused {
   int32_t stride, left, right;
   int64_t tpad;        // layout of x (engine buffers); idx, w are contiguous
   int64_t out_tpad;    // layout of out (tiled atmosphere pool, or 0)
+  int32_t scol[kFusedFields];  // shared-slot column of fused field k (AtmosArgs::scol)
 };
 int launch_atmos_fixup(const AtmosFused &af, int64_t n_cells, void *stream);
 int launch_atmos_finish(const AtmosArgs &a, int32_t n_boundaries, void *stream);

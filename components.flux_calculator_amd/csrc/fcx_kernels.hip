@@ -558,11 +558,26 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb) {
 }
 
 // Where a finished segment sum goes: a segment that continues into the next tile leaves its
-// prefix as the carry of this tile -- published for the next tile's wave (hand-off:
-// write-through agent-scope stores, then once they have completed flag[tile] = epoch) or
-// left for atmos_fixup_kernel; a complete one is the atmosphere value (and the boundary
+// prefix as the carry of this tile -- published for the next tile's wave (hand-off, below)
+// or left for atmos_fixup_kernel; a complete one is the atmosphere value (and the boundary
 // slot of a first/last atmosphere cell shared with a neighbour rank).
 // R: the engine's output type (an fp32 engine's atmosphere outputs are float, rounded once)
+//
+// Hand-off ordering.  The carries and the flag are agent-scope atomics: each is a
+// `global_store/load ... sc1`, coherent across the XCDs at the memory side, so the only
+// question is order.  Producer: the carry stores, then s_waitcnt vmcnt(0) (every carry store
+// acknowledged by the coherence point), then the flag store; the compiler fences around the
+// wait keep the compiler from moving the stores across it.  Consumer: the flag poll loop
+// exits on the loaded value, so the carry loads issue only after the flag load returned
+// (a control dependency; the compiler fence keeps them behind the loop, and the GPU does
+// not issue loads speculatively).  The C++-model form of the same protocol (flag store
+// __ATOMIC_RELEASE, poll __ATOMIC_ACQUIRE, agent scope) compiles on gfx950 to a
+// `buffer_wbl2 sc1` (write-back of the XCD's whole L2) per published carry and a
+// `buffer_inv sc1` (invalidate of its L2) per taken one; FCX_HANDOFF_ACQREL=1 builds it
+// for the A/B measurement.
+#ifndef FCX_HANDOFF_ACQREL
+#define FCX_HANDOFF_ACQREL 0
+#endif
 template <class R>
 __device__ __forceinline__ void segment_done(const AtmosFused &af, int64_t tile, int32_t a, const double *acc,
                                              bool cont) {
@@ -576,8 +591,14 @@ __device__ __forceinline__ void segment_done(const AtmosFused &af, int64_t tile,
         af.carry[tile * kFusedFields + k] = acc[k];
     }
     if (af.handoff) {
-      __builtin_amdgcn_s_waitcnt(0);  // the carry stores have completed before the flag is set
-      __hip_atomic_store(af.flag + tile, af.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (FCX_HANDOFF_ACQREL) {
+        __hip_atomic_store(af.flag + tile, af.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        __builtin_amdgcn_s_waitcnt(0);  // the carry stores have completed before the flag is set
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        __hip_atomic_store(af.flag + tile, af.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
     return;
   }
@@ -596,8 +617,8 @@ __device__ __forceinline__ void segment_done(const AtmosFused &af, int64_t tile,
       __builtin_nontemporal_store((R)acc[k], o);
     else
       *o = (R)acc[k];
-    if (a == 0 && af.left >= 0) af.shared[(int64_t)af.left * af.stride + k] = acc[k];
-    if (a == af.n_atmos - 1 && af.right >= 0) af.shared[(int64_t)af.right * af.stride + k] = acc[k];
+    if (a == 0 && af.left >= 0) af.shared[(int64_t)af.left * af.stride + af.scol[k]] = acc[k];
+    if (a == af.n_atmos - 1 && af.right >= 0) af.shared[(int64_t)af.right * af.stride + af.scol[k]] = acc[k];
   }
 }
 
@@ -605,11 +626,15 @@ __device__ __forceinline__ void segment_done(const AtmosFused &af, int64_t tile,
 // tile - 1 is the previous block of the same XCD run (dispatched 8 blocks earlier, resident
 // or done) or, for the first tile of an XCD run, the last block of the previous run, which
 // the dispatcher reaches because at most 7 such waves wait at any time.  Should a flag never
-// come, the wait gives up after ~2^20 polls (about a second) and raises af.err.
+// come (a producer not resident, e.g. another process holding the CUs), the wait gives up
+// after ~2^20 polls (about a second) and raises af.err; the engine then recomputes the
+// atmosphere outputs with atmos_kernel at its next synchronisation (fcx_engine.hip,
+// check_handoff), so the results stay exact.
 __device__ __forceinline__ void take_carry(const AtmosFused &af, int64_t tile, double *acc) {
   bool ok = false;
   for (int it = 0; it < (1 << 20); ++it) {
-    if (__hip_atomic_load(af.flag + tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == af.epoch) {
+    if (__hip_atomic_load(af.flag + tile, FCX_HANDOFF_ACQREL ? __ATOMIC_ACQUIRE : __ATOMIC_RELAXED,
+                          __HIP_MEMORY_SCOPE_AGENT) == af.epoch) {
       ok = true;
       break;
     }
@@ -781,8 +806,8 @@ __global__ __launch_bounds__(256) void atmos_fixup_kernel(const AtmosFused af, i
   for (int k = 0; k < kFusedFields; ++k) {
     if (!af.out[k]) continue;
     af.out[k][tiled(a, af.out_tpad)] = acc[k];
-    if (a == 0 && af.left >= 0) af.shared[(int64_t)af.left * af.stride + k] = acc[k];
-    if (a == af.n_atmos - 1 && af.right >= 0) af.shared[(int64_t)af.right * af.stride + k] = acc[k];
+    if (a == 0 && af.left >= 0) af.shared[(int64_t)af.left * af.stride + af.scol[k]] = acc[k];
+    if (a == af.n_atmos - 1 && af.right >= 0) af.shared[(int64_t)af.right * af.stride + af.scol[k]] = acc[k];
   }
 }
 
@@ -892,8 +917,8 @@ __global__ __launch_bounds__(256) void atmos_kernel(const AtmosArgs a) {
   for (int f = 0; f < kMaxAtmosFields; ++f) {
     if (f >= a.nf) break;
     reinterpret_cast<R *>(a.out[f])[tiled(c, a.out_tpad)] = (R)acc[f];
-    if (c == 0 && a.left >= 0) a.shared[(int64_t)a.left * a.stride + f] = acc[f];
-    if (c == a.n_atmos - 1 && a.right >= 0) a.shared[(int64_t)a.right * a.stride + f] = acc[f];
+    if (c == 0 && a.left >= 0) a.shared[(int64_t)a.left * a.stride + a.scol[f]] = acc[f];
+    if (c == a.n_atmos - 1 && a.right >= 0) a.shared[(int64_t)a.right * a.stride + a.scol[f]] = acc[f];
   }
 }
 
@@ -904,8 +929,8 @@ __global__ void atmos_finish_kernel(const AtmosArgs a, int32_t n_boundaries) {
   const int t = threadIdx.x;
   if (t < a.nf) {
     R *out = reinterpret_cast<R *>(a.out[t]);
-    if (a.left >= 0) out[0] = (R)a.shared[(int64_t)a.left * a.stride + t];
-    if (a.right >= 0) out[tiled(a.n_atmos - 1, a.out_tpad)] = (R)a.shared[(int64_t)a.right * a.stride + t];
+    if (a.left >= 0) out[0] = (R)a.shared[(int64_t)a.left * a.stride + a.scol[t]];
+    if (a.right >= 0) out[tiled(a.n_atmos - 1, a.out_tpad)] = (R)a.shared[(int64_t)a.right * a.stride + a.scol[t]];
   }
   __syncthreads();
   for (int64_t i = t; i < (int64_t)n_boundaries * a.stride; i += blockDim.x) a.shared[i] = 0.0;

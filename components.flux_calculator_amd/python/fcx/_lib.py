@@ -21,6 +21,7 @@ FCX_CORR_CELL_MAJOR = 0
 FCX_CORR_MONTH_MAJOR = 1
 FCX_PRECISION_F64 = 0
 FCX_PRECISION_F32 = 1
+FCX_COMM_ID_BYTES = 128
 
 # every symbol declared in include/fcx.h: (name, restype, argtypes)
 _c = ctypes
@@ -65,6 +66,17 @@ SIGNATURES = [
     ("fcx_last_kernel_ms", _I, [_P, _c.POINTER(_c.c_float)]),
     ("fcx_pinned_bytes", _I, [_P, _P]),
     ("fcx_algorithmic_bytes", _I, [_P, _I, _c.POINTER(_I64)]),
+    ("fcx_handoff_recoveries", _I, [_P, _c.POINTER(_I64)]),
+    ("fcx_zero_copy_bytes", _I, [_P, _c.POINTER(_I64)]),
+    ("fcx_host_malloc", _I, [_c.c_size_t, _c.POINTER(_P)]),
+    ("fcx_set_atmos_boundaries", _I, [_P, _I32, _I32, _I32]),
+    ("fcx_comm_unique_id", _I, [_P]),
+    ("fcx_comm_create", _I, [_I, _I, _I, _P, _c.POINTER(_P)]),
+    ("fcx_comm_destroy", _I, [_P]),
+    ("fcx_comm_allreduce_sum", _I, [_P, _P, _c.c_size_t, _P]),
+    ("fcx_set_comm", _I, [_P, _P]),
+    ("fcx_atmos_allreduce", _I, [_P, _c.POINTER(_P), _I]),
+    ("fcx_host_free", _I, [_P]),
     ("fcx_add_remap", _I, [_P, _I64, _I64, _P, _P, _P, _P]),
     ("fcx_add_remap_field", _I, [_P, _I32, _I, _I, _I, _I, _P, _I]),
     ("fcx_set_option", _I, [_P, _I, _I64]),

@@ -24,6 +24,10 @@ class Engine:
              local   : fcx.parallel.LocalAtmos of this rank
              fields  : [(phase, surface_type, grid, name, out_array[n_atmos])]
              shared  : optional (device_buffer[n_boundaries * stride], stride)
+             own_boundaries : optional True: the engine allocates its boundary slots
+                       (fcx_set_atmos_boundaries) from local.n_boundaries/left/right
+             comm    : optional fcx.comm.Comm: the engine completes its boundary slots
+                       itself after every accumulation (fcx_set_comm)
         remaps: exchange -> model remaps, each {"n_dst", "src", "dst", "w" (0-based links),
                  "fields": [(phase, surface_type, grid, name, out_array[n_dst])]}
         options: {name: value} for fcx_set_option.
@@ -95,6 +99,11 @@ class Engine:
                     self._keep.append(buf)
                     _lib.check(self.lib.fcx_set_atmos_shared(h, ctypes.c_void_p(data_ptr(buf)), la.n_boundaries,
                                                              stride, la.left, la.right))
+                elif atmos.get("own_boundaries"):
+                    _lib.check(self.lib.fcx_set_atmos_boundaries(h, la.n_boundaries, la.left, la.right))
+                if atmos.get("comm") is not None:
+                    self._keep.append(atmos["comm"])
+                    _lib.check(self.lib.fcx_set_comm(h, atmos["comm"].h))
             for rm in remaps or ():
                 src = np.ascontiguousarray(rm["src"], dtype=np.int32)
                 dst = np.ascontiguousarray(rm["dst"], dtype=np.int32)
@@ -159,10 +168,25 @@ class Engine:
         _lib.check(self.lib.fcx_pinned_bytes(self.h, ctypes.byref(b)))
         return b.value
 
+    def zero_copy_bytes(self):
+        """bytes of host arrays the kernels use in place (fcx_zero_copy_bytes)"""
+        b = ctypes.c_int64()
+        _lib.check(self.lib.fcx_zero_copy_bytes(self.h, ctypes.byref(b)))
+        return b.value
+
+    def zero_copy_active(self):
+        return self.zero_copy_bytes() > 0
+
+    def handoff_recoveries(self):
+        """fused accumulations recomputed after a carry hand-off timeout"""
+        c = ctypes.c_int64()
+        _lib.check(self.lib.fcx_handoff_recoveries(self.h, ctypes.byref(c)))
+        return c.value
+
     OPTIONS = {"cells_per_thread": 1, "max_blocks": 2, "nontemporal": 3, "specialize": 4,
                "atmos_in_run": 5, "pin_host": 6, "pipeline_chunks": 7,
                "pipeline_min_chunk": 8, "zero_copy": 9,
-               "timing": 10, "tiled_layout": 11}
+               "timing": 10, "tiled_layout": 11, "test_handoff_timeout": 12}
 
     def run_atmos(self, phase=PHASE_ALL):
         _lib.check(self.lib.fcx_run_atmos(self.h, phase))

@@ -123,4 +123,32 @@ class LocalFields:
         return new
 
 
-__all__ = ["LocalFields", "data_ptr", "dtype_name", "is_device", "VARNAMES", "MAX_SURFACE_TYPES"]
+def rehome(lf, buf, offset, first_key=None):
+    """Move every distinct host array of lf into the flat numpy buffer `buf`, back to back
+    from byte `offset` (aliases stay one array); first_key = (s, g, name) goes first.
+    Returns the byte offset after the last array.  Tests use it to control which arrays
+    share memory pages (fcx page-lock registry)."""
+    if offset % 8:
+        raise ValueError("offset must be a multiple of 8 bytes")
+    order = list(lf.field)
+    if first_key is not None:
+        order.remove(first_key)
+        order.insert(0, first_key)
+    moved = {}
+    for key in order:
+        a = lf.field[key]
+        if id(a) not in moved:
+            if not isinstance(a, np.ndarray):
+                raise TypeError("rehome: host arrays only")
+            n = a.shape[0]
+            if offset + a.nbytes > buf.nbytes:
+                raise ValueError("rehome: buffer too small")
+            v = np.frombuffer(buf, dtype=a.dtype, count=n, offset=offset)
+            v[:] = a
+            moved[id(a)] = (a, v)
+            offset += a.nbytes
+        lf.field[key] = moved[id(a)][1]
+    return offset
+
+
+__all__ = ["LocalFields", "data_ptr", "dtype_name", "is_device", "rehome", "VARNAMES", "MAX_SURFACE_TYPES"]

@@ -243,6 +243,43 @@ def build_case(variant="CCLM", n=4096, T=1, bias=False, sep_grids=None, rsdr=Fal
                 outputs=outputs)
 
 
+def regrid_links(n_src, n_dst, seed, max_links=4):
+    """A sparse_regridding_matrix (basic:117-122) in COO file order: every destination gets
+    0..max_links links (empty rows included, repeated (src, dst) pairs possible), the links
+    shuffled so that a row's links are scattered through the list; 1-based indices."""
+    r = np.random.Generator(np.random.PCG64([seed, 97]))
+    per = r.integers(0, max_links + 1, n_dst)
+    dst = np.repeat(np.arange(1, n_dst + 1, dtype=np.int32), per)
+    src = r.integers(1, n_src + 1, dst.shape[0]).astype(np.int32)
+    w = r.uniform(0.0, 1.0, dst.shape[0])
+    order = r.permutation(dst.shape[0])
+    return (np.ascontiguousarray(src[order]), np.ascontiguousarray(dst[order]), np.ascontiguousarray(w[order]))
+
+
+def build_regrid_case(variant="CCLM", n=300, sep_grids=(310, 290), T=2, bias=False, seed=BASE_SEED):
+    """A case on separate t/u/v grids with all four regridding matrices in use
+    (flux_calculator.F90:330-337, do_regridding basic:463-522): QSUR computed on t and put to
+    the u and v grids (t->u, t->v; QSUR(u/v) methods 'none'), UMOM computed on u and put to t
+    (u->t), VMOM on v put to t (v->t)."""
+    case = build_case(variant, n=n, T=T, bias=bias, sep_grids=sep_grids, seed=seed)
+    nt, nu, nv = case.grid_size
+    case.regrid = {"matrices": {0: regrid_links(nu, nt, seed + 1), 1: regrid_links(nv, nt, seed + 2),
+                                2: regrid_links(nt, nu, seed + 3), 3: regrid_links(nt, nv, seed + 4)}}
+    lf = case.lf
+    for s in range(1, T + 1):
+        if case.methods["which_spec_vapor_surface_t"][s - 1] == "CCLM":
+            case.methods["which_spec_vapor_surface_u"][s - 1] = "none"
+            case.methods["which_spec_vapor_surface_v"][s - 1] = "none"
+            lf.put_to[(s, 1, "QSUR")] = 2 | 4
+        lf.put_to[(s, 2, "UMOM")] = 1
+        lf.put_to[(s, 3, "VMOM")] = 1
+        for name in ("UMOM", "VMOM"):
+            lf.allocate_localvar(name, s, 1, value=np.nan)
+            case.outputs.append((s, 1, name))
+    case.name = f"{case.name}_regrid"
+    return case
+
+
 def as_dtype(case, dtype):
     """The same case with every field array rounded once to dtype (aliases kept): the fp32
     variant of SURVEY.md 8d config 5, and (as_dtype(c32, 'float64')) the exactly widened

@@ -132,9 +132,11 @@ int fcx_run(fcx_engine *e, int phase, int32_t current_step_time); /* device comp
 int fcx_download(fcx_engine *e, int phase); /* D2H of host-bound outputs of the phase */
 /* the three above; with host-bound fields pipelined over cell chunks (FCX_OPT_PIPELINE_CHUNKS) */
 int fcx_step(fcx_engine *e, int phase, int32_t current_step_time);
-/* waits for the engine's stream.  Also reports (FCX_E_HIP) a fused accumulation whose
- * in-launch carry hand-off timed out since the last check -- never in a correct run, but
- * the atmosphere values of that run would be wrong; fcx_step checks the same. */
+/* waits for the engine's stream.  A fused accumulation whose in-launch carry hand-off timed
+ * out since the last check (a producer wave that was not resident, e.g. another process
+ * holding the GPU) is recomputed here by the separate accumulation kernel (bit-identical
+ * results, host copies refreshed) and counted (fcx_handoff_recoveries); fcx_step does the
+ * same. */
 int fcx_synchronize(fcx_engine *e);
 
 /* ---- per call: the reference subroutines one by one (exact drop-in semantics; each
@@ -163,6 +165,10 @@ int fcx_device_layout(fcx_engine *e, int64_t *tile, int64_t *tile_stride);
 int fcx_last_kernel_ms(fcx_engine *e, float *ms);
 /* bytes of caller host memory page-locked by this engine (FCX_OPT_PIN_HOST) */
 int fcx_pinned_bytes(fcx_engine *e, int64_t *bytes);
+/* fused accumulations recomputed after a carry hand-off timeout (fcx_synchronize) */
+int fcx_handoff_recoveries(fcx_engine *e, int64_t *count);
+/* bytes of host arrays the kernels use in place (FCX_OPT_ZERO_COPY) */
+int fcx_zero_copy_bytes(fcx_engine *e, int64_t *bytes);
 /* algorithmic HBM bytes of one fcx_run(phase) (each distinct array read once, written once) */
 int fcx_algorithmic_bytes(fcx_engine *e, int phase, int64_t *bytes);
 
@@ -184,10 +190,40 @@ int fcx_add_atmos_field(fcx_engine *e, int phase, int surface_type, int grid, in
  * boundary `right`; field f of the accumulation uses column f (f < stride) */
 int fcx_set_atmos_shared(fcx_engine *e, double *shared, int32_t n_boundaries, int32_t stride,
                          int32_t left, int32_t right);
+/* instead of fcx_set_atmos_shared: the engine allocates the [n_boundaries][fields] slots
+ * itself (device memory, zeroed; stride = number of fcx_add_atmos_field fields).  Before
+ * fcx_commit. */
+int fcx_set_atmos_boundaries(fcx_engine *e, int32_t n_boundaries, int32_t left, int32_t right);
 /* after the all-reduce of `shared`: boundary values -> out arrays, slots re-zeroed */
 int fcx_atmos_finish(fcx_engine *e);
 /* the accumulation of `phase` on its own (fcx_run runs it unless FCX_OPT_ATMOS_IN_RUN=0) */
 int fcx_run_atmos(fcx_engine *e, int phase);
+
+/* ---- the one collective: RCCL over xGMI ----
+ * The boundary slots of all ranks are summed by ONE ncclAllReduce(sum, ncclFloat64) per
+ * step, the exchange OASIS3-MCT performs on the oasis_put of the type-0 fields
+ * (flux_calculator.F90:1015, create_namcouple.F90:92-98).  One communicator per rank (one
+ * rank per GPU): rank 0 creates the unique id, the host broadcasts its
+ * FCX_COMM_ID_BYTES bytes (MPI_Bcast in the Fortran host) and every rank creates its
+ * communicator.  RCCL is loaded at run time (the process's own librccl.so if one is
+ * already loaded, e.g. PyTorch's, else /opt/rocm's). */
+#define FCX_COMM_ID_BYTES 128
+typedef struct fcx_comm fcx_comm;
+int fcx_comm_unique_id(void *id /* FCX_COMM_ID_BYTES */);
+int fcx_comm_create(int device, int nranks, int rank, const void *id, fcx_comm **out);
+int fcx_comm_destroy(fcx_comm *c);
+/* sum-all-reduce of count doubles in place on a HIP stream (generic) */
+int fcx_comm_allreduce_sum(fcx_comm *c, double *buf, size_t count, void *hip_stream);
+/* attach: from now on fcx_run / fcx_step / fcx_run_atmos of the engine complete its
+ * boundary slots themselves (all-reduce on the engine's stream, then fcx_atmos_finish);
+ * every rank's engine must then run the same steps.  NULL detaches. */
+int fcx_set_comm(fcx_engine *e, fcx_comm *c);
+/* several engines of this rank (e.g. one per bottom-model variant) in ONE all-reduce: the
+ * slots of engines whose regions are adjacent in one buffer go in one call (else one call
+ * per engine inside one RCCL group), on the first engine's stream; then fcx_atmos_finish of
+ * each.  Call after their accumulation (fcx_run, or fcx_run_atmos); engines already
+ * completed in this run (fcx_set_comm) are skipped. */
+int fcx_atmos_allreduce(fcx_comm *c, fcx_engine *const *engines, int n_engines);
 
 /* ---- exchange-grid -> model remaps ----
  * The SCRIP weight application OASIS3-MCT performs on the 'S' fields sent to a model
@@ -218,11 +254,19 @@ enum fcx_option {
                                    default 262144: smaller grids take the sequential step) */
   FCX_OPT_ZERO_COPY = 9,        /* host-bound fields read/written by the kernels in place
                                    through the host link (page-locked, mapped): no mirrors,
-                                   no copy calls.  0 off, 1 on, 2 auto (default): on when
-                                   every grid is below 2 x PIPELINE_MIN_CHUNK cells and
-                                   PIN_HOST is on */
+                                   no copy calls.  2 auto (default): arrays allocated by
+                                   fcx_host_malloc, when every grid is below
+                                   2 x PIPELINE_MIN_CHUNK cells; caller heap arrays take
+                                   device mirrors.  1 on: every host array, caller heap
+                                   arrays page-locked and mapped at fcx_commit (the caller
+                                   must not free or remap them while the engine lives).
+                                   0 off: device mirrors for everything */
   FCX_OPT_TIMING = 10,          /* record the events behind fcx_last_kernel_ms (default 0:
                                    two event records per run cost ~8 us on small grids) */
+  FCX_OPT_TEST_HANDOFF_TIMEOUT = 12, /* test hook (default 0): report every fused launch's
+                                   carry hand-off as timed out, so that the recovery of
+                                   fcx_synchronize (atmos_kernel recomputes the atmosphere
+                                   outputs) runs; the results must be unchanged            */
   FCX_OPT_TILED_LAYOUT = 11     /* engine-owned mirrors tile-blocked (default 1): tiles of
                                    4096 cells, the read-only arrays' tiles interleaved in
                                    one pool and the written arrays' in another, so a wave's
@@ -232,6 +276,14 @@ enum fcx_option {
                                    device memory or used in place (zero-copy) */
 };
 int fcx_set_option(fcx_engine *e, int option, int64_t value);
+
+/* page-locked host memory owned by the library, mapped for the device at allocation: a
+ * host that allocates its local_field arrays here (c_f_pointer in Fortran) gets the
+ * zero-copy step on small grids (FCX_OPT_ZERO_COPY auto) and direct DMA on large ones,
+ * without any registration of its own memory.  Free only after every engine using the
+ * memory is destroyed.  No GPU work; callable before any engine exists. */
+int fcx_host_malloc(size_t bytes, void **ptr);
+int fcx_host_free(void *ptr);
 
 /* device memory for hosts that keep fields resident in HBM (bind with FCX_MEM_DEVICE) */
 int fcx_device_malloc(int device, size_t bytes, void **ptr);

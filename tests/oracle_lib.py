@@ -16,6 +16,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORACLE_SO = os.path.join(ROOT, "oracle", "_build", "libfco.so")
 REF_SO = os.path.join(ROOT, "oracle", "_ref", "libfco_ref.so")
+REF_REGRID_SO = os.path.join(ROOT, "oracle", "_ref", "libfco_ref_regrid.so")
 
 NV, MT = 35, 10
 c_int32, c_void_p, c_uint8 = ctypes.c_int32, ctypes.c_void_p, ctypes.c_uint8
@@ -45,6 +46,16 @@ _libs = {}
 
 
 def load(kind="c"):
+    """kind "c": the C restatement; "ref": the reference flux_lib + ref_harness.F90;
+    "ref_regrid": the reference do_regridding (flux_calculator_basic.F90:463-522)."""
+    if kind == "ref_regrid":
+        if kind not in _libs:
+            if not os.path.exists(REF_REGRID_SO):
+                return None
+            lib = ctypes.CDLL(REF_REGRID_SO)
+            lib.ref_do_regridding.argtypes = [ctypes.POINTER(FcoState), ctypes.c_int, ctypes.c_int]
+            _libs[kind] = (lib, "ref_")
+        return _libs[kind]
     if kind not in _libs:
         path = ORACLE_SO if kind == "c" else REF_SO
         if not os.path.exists(path):
@@ -178,7 +189,12 @@ def run_state(o, kind="c", phases=(1, 2), regrid=False):
     lib, p = load(kind)
     sp = ctypes.byref(o.st)
     fn = lambda name: getattr(lib, p + name)  # noqa: E731
-    rg = (lambda v: lib.fco_do_regridding(sp, IDX0[v], 0)) if regrid else (lambda v: None)
+    if kind == "ref":  # the reference's own do_regridding next to its flux_lib (1-based varidx)
+        rlib, _ = load("ref_regrid")
+        rg1 = lambda v: rlib.ref_do_regridding(sp, IDX0[v] + 1, 0)  # noqa: E731
+    else:  # fco_do_regridding takes the 0-based variable index
+        rg1 = lambda v: load("c")[0].fco_do_regridding(sp, IDX0[v], 0)  # noqa: E731
+    rg = rg1 if regrid else (lambda v: None)
 
     def averages(phase):
         for ph, g, name in case.averages:

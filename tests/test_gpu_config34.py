@@ -1,0 +1,122 @@
+"""BASELINE.json configs 3 and 4 at their real sizes, through exactly the bench's path
+(fcx.workload.Workload: the three variants over one set of inputs, engine-owned
+tile-blocked mirrors uploaded once, the exchange -> atmosphere accumulation fused into the
+flux kernels, HBM-resident steps).
+
+* config 3: 10M cells, CCLM + MOM5 + RCO: every output on a 20k-cell sample against the
+  oracle (1e-10 mixed, tests/parity.py), every cell finite, and every atmosphere cell
+  bit-identical to the sequential SCRIP sum of the GPU's own fluxes.
+* config 4: the 40M-cell grid as 8 APPLE shards (decomp_def.F90:23-31) in one process, the
+  shards' boundary slots summed (what the RCCL all-reduce does) and finished: sampled
+  fluxes against the oracle; every atmosphere cell against the sequential sum over the
+  global grid -- interior cells bit-identical, the shared boundary cells (two partial sums)
+  within 1e-12 mixed.
+"""
+import numpy as np
+import pytest
+
+import oracle_lib
+from parity import assert_parity
+
+pytestmark = pytest.mark.gpu
+
+from fcx.workload import ATM_FIELDS, VARIANTS, Workload  # noqa: E402
+from fcx.synthetic import build_case  # noqa: E402
+
+T_STEP = 3600
+
+
+def sampled_case(case, idx):
+    """The case restricted to the cells idx (aliasing kept), for the oracle."""
+    small = build_case(case.name.split("_")[0], n=idx.size, T=case.num_surface_types)
+    remap = {}
+    for key, a in case.lf.field.items():
+        if id(a) not in remap:
+            remap[id(a)] = np.ascontiguousarray(np.asarray(a)[idx])
+        small.lf.field[key] = remap[id(a)]
+    return small
+
+
+def check_sampled(case, got, idx, label):
+    small = sampled_case(case, idx)
+    # the oracle recomputes the outputs from the sampled inputs
+    ref = oracle_lib.run_case(small, "c", current_step_time=T_STEP)
+    assert_parity({k: v[idx] for k, v in got.items()}, ref, label=label)
+
+
+def sample(n, rng):
+    return np.unique(np.concatenate([rng.integers(0, n, 20_000), [0, 1, n - 2, n - 1]]))
+
+
+@pytest.mark.timeout(300)
+def test_config3_bench_path_10M():
+    wl = Workload(10_000_000, variants=VARIANTS)
+    try:
+        wl.run(T_STEP)
+        wl.download()
+        rng = np.random.default_rng(11)
+        idx = sample(wl.n, rng)
+        for v, case, outs in zip(wl.variants, wl.cases, wl.atm_outs):
+            got = {k: np.array(case.lf.field[k], copy=True) for k in case.outputs}
+            for k, x in got.items():
+                assert np.isfinite(x).all(), (v, k)
+            check_sampled(case, got, idx, f"config3 {v}")
+            for name, g in ATM_FIELDS:
+                flux = got[(1, g, name)] if (1, g, name) in got else np.asarray(case.lf.field[(1, g, name)])
+                want = oracle_lib.atmos_accumulate(wl.la.atmos_index, wl.la.weight, flux, wl.la.n_atmos)
+                np.testing.assert_array_equal(outs[name][: wl.la.n_atmos], want, err_msg=f"{v} {name}")
+    finally:
+        wl.close()
+
+
+@pytest.mark.timeout(600)
+def test_config4_40M_eight_shards():
+    import torch
+    from fcx.parallel import PeriodicAtmosMap
+
+    n_global, world = 40_000_000, 8
+    shards = [Workload(n_global, r, world, variants=VARIANTS) for r in range(world)]
+    try:
+        for wl in shards:
+            wl.run(T_STEP)
+        total = sum(wl.shared for wl in shards)  # the all-reduce (sum) of the boundary slots
+        for wl in shards:
+            wl.shared.copy_(total)
+            wl.finish()
+            wl.download()
+        torch.cuda.synchronize()
+        for wl in shards:
+            assert float(wl.shared.abs().sum()) == 0.0
+        gmap = PeriodicAtmosMap().global_map(n_global)
+        rng = np.random.default_rng(12)
+        for i, v in enumerate(VARIANTS):
+            fluxes = {name: np.empty(n_global) for name, _ in ATM_FIELDS}
+            atm = {name: np.full(gmap.n_atmos, np.nan) for name, _ in ATM_FIELDS}
+            for r, wl in enumerate(shards):
+                case, la = wl.cases[i], wl.la
+                got = {k: np.asarray(case.lf.field[k]) for k in case.outputs}
+                if r in (0, world - 1):  # first and last shard: sampled parity with the oracle
+                    check_sampled(case, got, sample(wl.n, rng), f"config4 {v} shard {r}")
+                for name, g in ATM_FIELDS:
+                    fluxes[name][wl.offset: wl.offset + wl.n] = np.asarray(case.lf.field[(1, g, name)])
+                    part = wl.atm_outs[i][name][: la.n_atmos]
+                    seg = atm[name][la.atmos_offset: la.atmos_offset + la.n_atmos]
+                    both = ~np.isnan(seg)  # a boundary cell both neighbours hold: the same value
+                    np.testing.assert_array_equal(seg[both], part[both], err_msg=f"{v} {name} boundary r{r}")
+                    seg[:] = part
+            shared_cells = np.array(sorted({wl.la.atmos_offset for wl in shards if wl.la.left >= 0}))
+            for name, _ in ATM_FIELDS:
+                want = oracle_lib.atmos_accumulate(gmap.atmos_index, gmap.weight, fluxes[name], gmap.n_atmos)
+                got = atm[name]
+                assert np.isfinite(got).all(), (v, name)
+                interior = np.ones(gmap.n_atmos, bool)
+                interior[shared_cells] = False
+                np.testing.assert_array_equal(got[interior], want[interior], err_msg=f"{v} {name} interior")
+                if shared_cells.size:
+                    scale = max(np.abs(want).max(), 1e-300)
+                    err = np.abs(got[shared_cells] - want[shared_cells]) / np.maximum(
+                        np.abs(want[shared_cells]), 1e-6 * scale)
+                    assert err.max() <= 1e-12, (v, name, err.max())
+    finally:
+        for wl in shards:
+            wl.close()

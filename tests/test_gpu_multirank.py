@@ -46,13 +46,15 @@ def shard_case(full, lo, hi, variant, seed=911):
     return case
 
 
-def make_engine(case, la, shared, stride, device="cuda:0", fused=True, options=None):
+def make_engine(case, la, shared, stride, device="cuda:0", fused=True, options=None, fields=None):
+    """fields: [(phase, name, grid)] in registration order (default: FIELDS, normal phase)"""
     import torch
     from fcx.engine import Engine
 
+    fields = fields or [(2, name, g) for name, g in FIELDS]
     outs = {name: torch.full((max(la.n_atmos, 1),), float("nan"), dtype=torch.float64, device=device)
-            for name, _ in FIELDS}
-    atmos = {"local": la, "fields": [(2, 1, g, name, outs[name]) for name, g in FIELDS],
+            for _, name, _ in fields}
+    atmos = {"local": la, "fields": [(ph, 1, g, name, outs[name]) for ph, name, g in fields],
              "shared": (shared, stride) if shared is not None else None}
     # specialize=0 turns the T=1 kernels (and with them the fused accumulation) off
     opts = dict(options or {})
@@ -110,6 +112,40 @@ def test_fused_accumulation_long_segments(lengths, mode):
             gpu_flux = np.asarray(case.lf.field[(1, g, name)])
             want = oracle_lib.atmos_accumulate(amap.atmos_index, amap.weight, gpu_flux, amap.n_atmos)
             np.testing.assert_array_equal(outs[name].cpu().numpy(), want, err_msg=f"{name} step {step}")
+    eng.close()
+
+
+@pytest.mark.parametrize("host_outputs", [False, True])
+def test_handoff_timeout_recovery(host_outputs):
+    """A carry hand-off that gives up (forced by the FCX_OPT_TEST_HANDOFF_TIMEOUT hook) is
+    recovered at the synchronisation: atmos_kernel recomputes the atmosphere outputs from
+    the stored fluxes, bit-identical to the sequential sum; host outputs are refreshed."""
+    import torch
+    from fcx.engine import Engine
+
+    n = 70_001
+    case = build_case("MOM5", n=n, T=1, bias=True, seed=23)
+    amap = random_run_map(n, (1, 7), seed=3)
+    la = local_atmos(amap, 0, 1)
+    if host_outputs:
+        outs = {name: np.full(la.n_atmos, np.nan) for name, _ in FIELDS}
+    else:
+        outs = {name: torch.full((la.n_atmos,), float("nan"), dtype=torch.float64, device="cuda:0")
+                for name, _ in FIELDS}
+    atmos = {"local": la, "fields": [(2, 1, g, name, outs[name]) for name, g in FIELDS]}
+    eng = Engine(case.lf, 1, case.methods, corrections=case.corrections, atmos=atmos,
+                 options={"test_handoff_timeout": 1})
+    for step in range(2):
+        for o in outs.values():
+            o[:] = float("nan")
+        eng.step(PHASE_ALL, 3600 * step)
+        torch.cuda.synchronize()
+        assert eng.handoff_recoveries() == step + 1
+        for name, g in FIELDS:
+            gpu_flux = np.asarray(case.lf.field[(1, g, name)])
+            want = oracle_lib.atmos_accumulate(amap.atmos_index, amap.weight, gpu_flux, amap.n_atmos)
+            got = outs[name] if host_outputs else outs[name].cpu().numpy()
+            np.testing.assert_array_equal(got, want, err_msg=f"{name} step {step}")
     eng.close()
 
 
@@ -181,6 +217,43 @@ def test_sharded_engines_one_process(variant, world, fused):
             got[name][la.atmos_offset: la.atmos_offset + la.n_atmos] = outs[name].cpu().numpy()[: la.n_atmos]
         eng.close()
     assert_parity(got, ref, label=f"{variant} x{world}")
+
+
+@pytest.mark.parametrize("fused", [True, False])
+def test_sharded_engines_field_order_and_phases(fused):
+    """Fields registered out of the fused kernel's slot order, RBBR accumulated at the end of
+    the early phase and the rest at the end of the normal one: every path writes a field's
+    boundary partial sums into the column of its registration index, so the all-reduce and
+    fcx_atmos_finish complete the right cells."""
+    import torch
+
+    n, world, variant = 20_011, 3, "MOM5"
+    full, amap, ref = reference(n, variant)
+    fields = [(2, "VMOM", 3), (1, "RBBR", 1), (2, "HSEN", 1), (2, "MEVA", 1), (2, "UMOM", 2), (2, "HLAT", 1)]
+    stride = len(fields)
+    engines = []
+    for r in range(world):
+        la = local_atmos(amap, r, world)
+        shared = torch.zeros((world - 1) * stride, dtype=torch.float64, device="cuda:0")
+        case = shard_case(full, la.offset, la.offset + la.size, variant)
+        eng, outs = make_engine(case, la, shared, stride, fused=fused, fields=fields)
+        engines.append((la, shared, eng, outs))
+    for la, shared, eng, outs in engines:
+        eng.upload(PHASE_ALL)
+        eng.run(1, 7200)  # early phase: RBBR and its accumulation
+        eng.run(2, 7200)  # normal phase: the rest
+        eng.synchronize()
+    total = sum(sh for _, sh, _, _ in engines)
+    for la, shared, eng, outs in engines:
+        shared.copy_(total)
+        eng.atmos_finish()
+        eng.synchronize()
+    got = {name: np.full(amap.n_atmos, np.nan) for name, _ in FIELDS}
+    for la, shared, eng, outs in engines:
+        for name, _ in FIELDS:
+            got[name][la.atmos_offset: la.atmos_offset + la.n_atmos] = outs[name].cpu().numpy()[: la.n_atmos]
+        eng.close()
+    assert_parity(got, ref, label=f"field order, phases, fused={fused}")
 
 
 def _rank(rank, world, port, q):

@@ -106,9 +106,24 @@ def test_method_edges(per_type):
     assert_parity(fused(case), ref, label=str(per_type))
 
 
+@pytest.mark.parametrize("variant", ["CCLM", "MOM5", "RCO"])
+@pytest.mark.parametrize("T", [1, 3])
+def test_shortwave_distribution(variant, T):
+    """distribute_shortwave_radiation_flux (calc:347-364, flux_calculator.F90:991): with
+    RSDD/ALBA bound every surface type's RSDR is the type-0 RSDD (the albedo factors are
+    commented out in distribute_radiation_flux.F90:24), inside the fused step."""
+    case = build_case(variant, n=4099, T=T, bias=True, rsdr=True)
+    ref = oracle_lib.run_case(case, "c", current_step_time=STEP_T)
+    got = fused(case)
+    assert_parity(got, ref, label=case.name)
+    rsdd = np.asarray(case.lf.field[(0, 1, "RSDD")])
+    for s in range(1, T + 1):
+        np.testing.assert_array_equal(got[(s, 1, "RSDR")], rsdd, err_msg=f"RSDR({s})")
+
+
 def test_per_call_dropin_sequence():
     """The reference subroutines one by one (calc:25-385) through the C ABI."""
-    case = build_case("MOM5", n=2500, T=3, bias=True)
+    case = build_case("MOM5", n=2500, T=3, bias=True, rsdr=True)
     ref = oracle_lib.run_case(case, "c", current_step_time=STEP_T)
     fcc.prepare(case.lf, 1, case.num_surface_types, case.methods, corrections=case.corrections)
     m = fcc.methods_2d(case.methods)

@@ -1,0 +1,172 @@
+"""Zero-copy and page-lock hazards, each forced deterministically.
+
+Round 1 saw one non-finite MEVA in one full-suite run of test_fused_t1[4097-False-MOM5]
+(zero-copy on caller heap arrays), with HLAT -- computed from the same in-register MEVA --
+right.  Every mechanism that could lose a kernel store between the kernel and the host
+array is set up here on purpose, instead of hoping for the suite order to recreate it:
+
+  * an output whose page meets another live engine's registration (it stays pageable with a
+    device mirror inside a zero-copy engine), before and after that engine is closed;
+  * an engine dropped without close() and collected by the garbage collector between the
+    commit and the step of a new engine over fresh arrays;
+  * two live engines over the same arrays (a registration shared by reference count), one
+    closed before the other steps;
+  * non-temporal against plain stores to host-mapped memory;
+  * library-allocated page-locked arrays (fcx_host_malloc), the default zero-copy path.
+"""
+import gc
+
+import numpy as np
+import pytest
+
+import oracle_lib
+from parity import assert_parity
+
+pytestmark = pytest.mark.gpu
+
+fcx = pytest.importorskip("fcx")
+from fcx.basic import PHASE_ALL  # noqa: E402
+from fcx.engine import Engine  # noqa: E402
+from fcx.local_field import rehome  # noqa: E402
+from fcx.synthetic import build_case  # noqa: E402
+from fcx import host_alloc  # noqa: E402
+
+T_STEP = 3600
+PAGE = 4096
+
+
+def engine_for(case, **opts):
+    return Engine(case.lf, case.num_surface_types, case.methods, corrections=case.corrections,
+                  averages=case.averages, options=opts)
+
+
+def reset_outputs(case):
+    for k in case.outputs:
+        case.lf.field[k][:] = np.nan
+
+
+def check(case, label):
+    ref = oracle_lib.run_case(case, "c", current_step_time=T_STEP)
+    got = {k: np.array(case.lf.field[k], copy=True) for k in case.outputs}
+    assert_parity(got, ref, label=label)
+
+
+def carve(cases, first_key=None):
+    """Re-home the arrays of several cases back to back in ONE heap buffer, each case's
+    arrays contiguous, consecutive cases meeting inside one page (8-B apart), so that the
+    last array of case k and the first array of case k+1 share a page.  first_key puts that
+    (s, g, name) array first in every case."""
+    sizes = []
+    for c in cases:
+        seen = {}
+        for a in c.lf.field.values():
+            seen[id(a)] = a.nbytes
+        sizes.append(sum(seen.values()))
+    total = sum(sizes) + 8 * len(cases) + 2 * PAGE
+    buf = np.empty(total // 8 + 1, dtype=np.float64)
+    off = (-buf.ctypes.data) % PAGE + 8 * 17  # start mid-page
+    for c, sz in zip(cases, sizes):
+        rehome(c.lf, buf, off, first_key=first_key)
+        off += sz + 8
+    return buf
+
+
+@pytest.mark.parametrize("zero_copy", [1, 2])
+def test_output_page_shared_with_another_live_engine(zero_copy):
+    """Case B's MEVA begins on the page where case A's arrays end: in B it cannot be
+    page-locked exclusively, so it keeps a device mirror inside a zero-copy engine."""
+    a = build_case("MOM5", n=4097, T=1)
+    b = build_case("MOM5", n=4097, T=1)
+    keep = carve([a, b], first_key=(1, 1, "MEVA"))
+    ea = engine_for(a, zero_copy=zero_copy)
+    eb = engine_for(b, zero_copy=zero_copy)
+    eb.step(PHASE_ALL, T_STEP)
+    check(b, "B with A live")
+    ea.step(PHASE_ALL, T_STEP)
+    check(a, "A")
+    ea.close()
+    reset_outputs(b)
+    eb.step(PHASE_ALL, T_STEP)
+    check(b, "B after A closed")
+    eb.close()
+    del keep
+
+
+class _Cycle:
+    def __init__(self, eng, case):
+        self.eng, self.case, self.me = eng, case, self
+
+
+def test_engine_collected_between_commit_and_step():
+    """An engine only the cyclic garbage collector frees (never closed) is destroyed after a
+    new engine over fresh arrays has committed and before it steps."""
+    for n in (4097, 10_007):
+        a = build_case("MOM5", n=n, T=1)
+        _Cycle(engine_for(a, zero_copy=1), a)  # unreachable, alive until gc.collect()
+        del a
+        b = build_case("MOM5", n=n, T=1)
+        eb = engine_for(b, zero_copy=1)
+        gc.collect()  # the old engine's fcx_destroy runs here: its page locks are dropped
+        eb.step(PHASE_ALL, T_STEP)
+        check(b, f"n={n} after collecting the old engine")
+        eb.close()
+
+
+def test_registration_shared_by_two_engines():
+    """Two live engines over the same arrays share one registration (reference count);
+    closing the first leaves the second's mapping intact."""
+    c = build_case("CCLM", n=4097, T=1, bias=True)
+    e1 = engine_for(c, zero_copy=1)
+    e2 = engine_for(c, zero_copy=1)
+    e1.step(PHASE_ALL, T_STEP)
+    check(c, "first engine")
+    e1.close()
+    reset_outputs(c)
+    e2.step(PHASE_ALL, T_STEP)
+    check(c, "second engine after the first closed")
+    e2.close()
+
+
+@pytest.mark.parametrize("nontemporal", [0, 1])
+def test_host_mapped_stores(nontemporal):
+    """Stores to host-mapped arrays: the engine drops the non-temporal hint for mapped
+    fields whatever FCX_OPT_NONTEMPORAL says; the results are the same either way."""
+    for v in ("CCLM", "MOM5", "RCO"):
+        c = build_case(v, n=4097, T=1)
+        e = engine_for(c, zero_copy=1, nontemporal=nontemporal)
+        for _ in range(3):
+            reset_outputs(c)
+            e.step(PHASE_ALL, T_STEP)
+            check(c, f"{v} nt={nontemporal}")
+        e.close()
+
+
+@pytest.mark.parametrize("variant", ["CCLM", "MOM5", "RCO"])
+@pytest.mark.parametrize("n", [4097, 32_768])
+def test_library_pinned_arrays_zero_copy(variant, n):
+    """Arrays allocated by fcx_host_malloc are used in place by default (auto zero-copy:
+    page-locked and mapped by the library itself, no registration of caller memory)."""
+    c = build_case(variant, n=n, T=2, bias=True)
+    with host_alloc.Arena() as arena:
+        arena.adopt(c.lf)
+        e = engine_for(c)
+        assert e.zero_copy_active()
+        assert e.pinned_bytes() == 0  # nothing of the caller's was registered
+        for k in range(3):
+            reset_outputs(c)
+            e.step(PHASE_ALL, T_STEP)
+            check(c, f"{variant} step {k}")
+            for key in ("TSUR", "PSUR"):  # fresh inputs between steps reach the kernel
+                arr = c.lf.field[(1, 1, key)]
+                arr[:] = arr * (1.0 + 1e-4)
+        e.close()
+
+
+def test_heap_arrays_take_mirrors_by_default():
+    """Caller heap arrays are not used in place unless FCX_OPT_ZERO_COPY=1."""
+    c = build_case("CCLM", n=4097, T=1)
+    e = engine_for(c)
+    assert not e.zero_copy_active()
+    e.step(PHASE_ALL, T_STEP)
+    check(c, "mirrors")
+    e.close()
