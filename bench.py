@@ -326,7 +326,8 @@ def main():
             # the timed launch carries the accumulation only when it is fused (fp64)
             traffic = t.get(traffic_key(variants[dom], n, args.types, args.bias, fused, args.precision))
             if traffic is not None:
-                traffic_source = t.get("_source")
+                traffic_source = t.get("_sources", {}).get(
+                    traffic_key(variants[dom], n, args.types, args.bias, fused, args.precision))
         except Exception:
             traffic = None
 

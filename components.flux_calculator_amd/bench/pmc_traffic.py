@@ -56,6 +56,8 @@ def main():
     ap.add_argument("--cells", type=int, default=10_000_000)
     ap.add_argument("--types", type=int, default=1)
     ap.add_argument("--bias", type=int, default=0)
+    ap.add_argument("--source", default=None,
+                    help="where the PMC run's outputs are kept (e.g. profiles/r02/pmc_t1), stamped per key")
     ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.dirname(
         os.path.dirname(os.path.abspath(__file__)))), "profiles", "traffic.json"))
     a = ap.parse_args()
@@ -70,6 +72,9 @@ def main():
         w = sum(write[k]) / len(write[k]) * 1024
         key = traffic_key(v, a.cells, a.types, a.bias, atm, dt)
         out[key] = round(f + w)
+        out.setdefault("_sources", {})[key] = (
+            f"{a.source or a.dir}: rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE passes (separate runs), "
+            f"mean over {len(fetch[k])} launches, FETCH_SIZE x2 (gfx950) + WRITE_SIZE")
         print(key, "read", round(f / a.cells, 2), "B/cell", "write", round(w / a.cells, 2), "B/cell",
               "launches", len(fetch[k]))
     json.dump(out, open(a.out, "w"), indent=1, sort_keys=True)

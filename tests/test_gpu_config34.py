@@ -74,7 +74,10 @@ def test_config4_40M_eight_shards():
     import torch
     from fcx.parallel import PeriodicAtmosMap
 
-    n_global, world = 40_000_000, 8
+    # 40M + 40 cells: shards of 5,000,005 cells, so the shard ends fall inside atmosphere cells
+    # of the periodic map (16 exchange cells = 4 atmosphere cells) and the boundary exchange
+    # has work to do (with 5M-cell shards every boundary would coincide with a cell edge)
+    n_global, world = 40_000_040, 8
     shards = [Workload(n_global, r, world, variants=VARIANTS) for r in range(world)]
     try:
         for wl in shards:
@@ -104,7 +107,8 @@ def test_config4_40M_eight_shards():
                     both = ~np.isnan(seg)  # a boundary cell both neighbours hold: the same value
                     np.testing.assert_array_equal(seg[both], part[both], err_msg=f"{v} {name} boundary r{r}")
                     seg[:] = part
-            shared_cells = np.array(sorted({wl.la.atmos_offset for wl in shards if wl.la.left >= 0}))
+            shared_cells = np.array(sorted({wl.la.atmos_offset for wl in shards if wl.la.left >= 0}), dtype=np.int64)
+            assert shared_cells.size >= world // 2, "the shard boundaries must cut atmosphere cells"
             for name, _ in ATM_FIELDS:
                 want = oracle_lib.atmos_accumulate(gmap.atmos_index, gmap.weight, fluxes[name], gmap.n_atmos)
                 got = atm[name]
