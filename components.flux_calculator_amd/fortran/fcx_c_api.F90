@@ -19,6 +19,8 @@ MODULE fcx_c_api
                                FCX_FLUX_MOMENTUM = 6, FCX_FLUX_RADIATION_BLACKBODY = 7
   ! regridding matrices (enum fcx_regrid)
   INTEGER(c_int), PARAMETER :: FCX_U_TO_T = 0, FCX_V_TO_T = 1, FCX_T_TO_U = 2, FCX_T_TO_V = 3
+  ! the RCCL unique id travels between the ranks as these many bytes (MPI_Bcast)
+  INTEGER, PARAMETER :: FCX_COMM_ID_BYTES = 128
 
   INTERFACE
     FUNCTION fcx_last_error() BIND(C, name='fcx_last_error')
@@ -193,6 +195,90 @@ MODULE fcx_c_api
       TYPE(c_ptr), VALUE :: engine
       INTEGER(c_int), VALUE :: var, surface_type
       INTEGER(c_int) :: fcx_do_regridding
+    END FUNCTION
+    ! ---- exchange -> atmosphere accumulation and its one collective (SURVEY.md 8e)
+    FUNCTION fcx_set_atmos_map(engine, n_atmos, atmos_index, weight) BIND(C, name='fcx_set_atmos_map')
+      IMPORT :: c_int, c_int64_t, c_ptr
+      TYPE(c_ptr), VALUE :: engine, atmos_index, weight
+      INTEGER(c_int64_t), VALUE :: n_atmos
+      INTEGER(c_int) :: fcx_set_atmos_map
+    END FUNCTION
+    FUNCTION fcx_add_atmos_field(engine, phase, surface_type, grid, var, out, flags) &
+        BIND(C, name='fcx_add_atmos_field')
+      IMPORT :: c_int, c_ptr
+      TYPE(c_ptr), VALUE :: engine, out
+      INTEGER(c_int), VALUE :: phase, surface_type, grid, var, flags
+      INTEGER(c_int) :: fcx_add_atmos_field
+    END FUNCTION
+    FUNCTION fcx_set_atmos_boundaries(engine, n_boundaries, left, right) BIND(C, name='fcx_set_atmos_boundaries')
+      IMPORT :: c_int, c_int32_t, c_ptr
+      TYPE(c_ptr), VALUE :: engine
+      INTEGER(c_int32_t), VALUE :: n_boundaries, left, right
+      INTEGER(c_int) :: fcx_set_atmos_boundaries
+    END FUNCTION
+    FUNCTION fcx_atmos_finish(engine) BIND(C, name='fcx_atmos_finish')
+      IMPORT :: c_int, c_ptr
+      TYPE(c_ptr), VALUE :: engine
+      INTEGER(c_int) :: fcx_atmos_finish
+    END FUNCTION
+    FUNCTION fcx_run_atmos(engine, phase) BIND(C, name='fcx_run_atmos')
+      IMPORT :: c_int, c_ptr
+      TYPE(c_ptr), VALUE :: engine
+      INTEGER(c_int), VALUE :: phase
+      INTEGER(c_int) :: fcx_run_atmos
+    END FUNCTION
+    FUNCTION fcx_comm_unique_id(id) BIND(C, name='fcx_comm_unique_id')
+      IMPORT :: c_int, c_int8_t
+      INTEGER(c_int8_t), DIMENSION(*), INTENT(OUT) :: id
+      INTEGER(c_int) :: fcx_comm_unique_id
+    END FUNCTION
+    FUNCTION fcx_comm_create(device, nranks, rank, id, comm) BIND(C, name='fcx_comm_create')
+      IMPORT :: c_int, c_int8_t, c_ptr
+      INTEGER(c_int), VALUE :: device, nranks, rank
+      INTEGER(c_int8_t), DIMENSION(*), INTENT(IN) :: id
+      TYPE(c_ptr), INTENT(OUT) :: comm
+      INTEGER(c_int) :: fcx_comm_create
+    END FUNCTION
+    FUNCTION fcx_comm_destroy(comm) BIND(C, name='fcx_comm_destroy')
+      IMPORT :: c_int, c_ptr
+      TYPE(c_ptr), VALUE :: comm
+      INTEGER(c_int) :: fcx_comm_destroy
+    END FUNCTION
+    FUNCTION fcx_set_comm(engine, comm) BIND(C, name='fcx_set_comm')
+      IMPORT :: c_int, c_ptr
+      TYPE(c_ptr), VALUE :: engine, comm
+      INTEGER(c_int) :: fcx_set_comm
+    END FUNCTION
+    FUNCTION fcx_set_option(engine, option, value) BIND(C, name='fcx_set_option')
+      IMPORT :: c_int, c_int64_t, c_ptr
+      TYPE(c_ptr), VALUE :: engine
+      INTEGER(c_int), VALUE :: option
+      INTEGER(c_int64_t), VALUE :: value
+      INTEGER(c_int) :: fcx_set_option
+    END FUNCTION
+    FUNCTION fcx_handoff_recoveries(engine, count) BIND(C, name='fcx_handoff_recoveries')
+      IMPORT :: c_int, c_int64_t, c_ptr
+      TYPE(c_ptr), VALUE :: engine
+      INTEGER(c_int64_t), INTENT(OUT) :: count
+      INTEGER(c_int) :: fcx_handoff_recoveries
+    END FUNCTION
+    FUNCTION fcx_zero_copy_bytes(engine, bytes) BIND(C, name='fcx_zero_copy_bytes')
+      IMPORT :: c_int, c_int64_t, c_ptr
+      TYPE(c_ptr), VALUE :: engine
+      INTEGER(c_int64_t), INTENT(OUT) :: bytes
+      INTEGER(c_int) :: fcx_zero_copy_bytes
+    END FUNCTION
+    ! ---- library-owned page-locked host memory (c_f_pointer it onto local_field arrays)
+    FUNCTION fcx_host_malloc(bytes, ptr) BIND(C, name='fcx_host_malloc')
+      IMPORT :: c_int, c_size_t, c_ptr
+      INTEGER(c_size_t), VALUE :: bytes
+      TYPE(c_ptr), INTENT(OUT) :: ptr
+      INTEGER(c_int) :: fcx_host_malloc
+    END FUNCTION
+    FUNCTION fcx_host_free(ptr) BIND(C, name='fcx_host_free')
+      IMPORT :: c_int, c_ptr
+      TYPE(c_ptr), VALUE :: ptr
+      INTEGER(c_int) :: fcx_host_free
     END FUNCTION
   END INTERFACE
 

@@ -1,7 +1,11 @@
 ! fcx_selftest.F90 -- TEST INFRASTRUCTURE: a Fortran host driving libfcx through the
 ! iso_c_binding interfaces (fcx_c_api), checked against the REFERENCE flux_lib called
 ! directly from Fortran (compiled from /root/reference into oracle/_ref).  One CCLM and one
-! MOM5 coupling step, T=1, u/v grids aliased to the t grid, bias corrections on.
+! MOM5 coupling step, T=1, u/v grids aliased to the t grid, bias corrections on.  A third
+! step (CCLM) runs on arrays the library allocated (fcx_host_malloc + c_f_pointer: the
+! default zero-copy path), with the exchange -> atmosphere accumulation, engine-owned
+! boundary slots and an RCCL communicator of one rank attached (fcx_comm_*, fcx_set_comm);
+! its atmosphere outputs must equal the sequential sum of its own fluxes bit for bit.
 ! Prints "FCX_FORTRAN_SELFTEST OK <max mixed error>" and stops 0 when every field is
 ! within 1e-10 (SURVEY.md 8d metric), stops 1 otherwise.
 PROGRAM fcx_selftest
@@ -22,6 +26,17 @@ PROGRAM fcx_selftest
   INTEGER(c_int32_t) :: t_step, m32
   TYPE(c_ptr) :: eng
   CHARACTER(len=4) :: vname
+  ! part 3: library arrays, atmosphere accumulation, communicator
+  INTEGER, PARAMETER :: na = (n + 3) / 4, nfa = 4
+  TYPE(c_ptr) :: comm, blk(nfa + 7)
+  INTEGER(c_int8_t) :: uid(FCX_COMM_ID_BYTES)
+  INTEGER(c_int32_t), TARGET :: aidx(n)
+  REAL(dp), TARGET :: aw(n)
+  REAL(dp), POINTER :: lme(:), lhl(:), lhs(:), lrb(:), lqs(:), lum(:), lvm(:)
+  REAL(dp), POINTER :: ao(:, :)
+  REAL(dp) :: want(na)
+  INTEGER(c_int64_t) :: zc
+  INTEGER :: k, f
 
   DO j = 1, n   ! deterministic inputs in the ranges of SURVEY.md 8d
     fi(j) = MERGE(1.0_dp, 0.0_dp, MOD(j, 5) == 0)
@@ -91,6 +106,94 @@ PROGRAM fcx_selftest
                 err(um, r_um), err(vm, r_vm))
     WRITE (*, '(A,A,A,ES12.4)') 'variant ', vname, ' max mixed error ', worst
   END DO
+  ! ---- part 3 (CCLM again): outputs in library memory, accumulation, communicator
+  DO j = 1, n   ! 4 exchange cells per atmosphere cell, weights summing to 1
+    aidx(j) = INT((j - 1) / 4, c_int32_t)
+    aw(j) = 0.25_dp
+  END DO
+  CALL chk(fcx_host_malloc(INT(8 * n, c_size_t), blk(1)), 'host_malloc'); CALL c_f_pointer(blk(1), lme, [n])
+  CALL chk(fcx_host_malloc(INT(8 * n, c_size_t), blk(2)), 'host_malloc'); CALL c_f_pointer(blk(2), lhl, [n])
+  CALL chk(fcx_host_malloc(INT(8 * n, c_size_t), blk(3)), 'host_malloc'); CALL c_f_pointer(blk(3), lhs, [n])
+  CALL chk(fcx_host_malloc(INT(8 * n, c_size_t), blk(4)), 'host_malloc'); CALL c_f_pointer(blk(4), lrb, [n])
+  CALL chk(fcx_host_malloc(INT(8 * n, c_size_t), blk(5)), 'host_malloc'); CALL c_f_pointer(blk(5), lqs, [n])
+  CALL chk(fcx_host_malloc(INT(8 * n, c_size_t), blk(6)), 'host_malloc'); CALL c_f_pointer(blk(6), lum, [n])
+  CALL chk(fcx_host_malloc(INT(8 * n, c_size_t), blk(7)), 'host_malloc'); CALL c_f_pointer(blk(7), lvm, [n])
+  CALL chk(fcx_host_malloc(INT(8 * na * nfa, c_size_t), blk(8)), 'host_malloc'); CALL c_f_pointer(blk(8), ao, [na, nfa])
+  lme = -1.0_dp; lhl = -1.0_dp; lhs = -1.0_dp; lrb = -1.0_dp; lqs = -1.0_dp; lum = -1.0_dp; lvm = -1.0_dp
+  ao = -1.0_dp
+  CALL chk(fcx_comm_unique_id(uid), 'unique id')   ! rank 0; an MPI host broadcasts it
+  CALL chk(fcx_comm_create(0_c_int, 1_c_int, 0_c_int, uid, comm), 'comm create')
+  CALL chk(fcx_create(0_c_int, 1_c_int, [INT(n, c_int32_t), INT(n, c_int32_t), INT(n, c_int32_t)], eng), 'create')
+  CALL chk(fcx_set_method(eng, FCX_SPEC_VAPOR_SURFACE_T, 1_c_int, fcx_method_id('CCLM')), 'm')
+  CALL chk(fcx_set_method(eng, FCX_SPEC_VAPOR_SURFACE_U, 1_c_int, fcx_method_id('CCLM')), 'm')
+  CALL chk(fcx_set_method(eng, FCX_SPEC_VAPOR_SURFACE_V, 1_c_int, fcx_method_id('CCLM')), 'm')
+  CALL chk(fcx_set_method(eng, FCX_FLUX_MASS_EVAP, 1_c_int, fcx_method_id('CCLM')), 'm')
+  CALL chk(fcx_set_method(eng, FCX_FLUX_HEAT_LATENT, 1_c_int, fcx_method_id('water')), 'm')
+  CALL chk(fcx_set_method(eng, FCX_FLUX_HEAT_SENSIBLE, 1_c_int, fcx_method_id('CCLM')), 'm')
+  CALL chk(fcx_set_method(eng, FCX_FLUX_MOMENTUM, 1_c_int, fcx_method_id('CCLM')), 'm')
+  CALL chk(fcx_set_method(eng, FCX_FLUX_RADIATION_BLACKBODY, 1_c_int, fcx_method_id('StBo')), 'm')
+  CALL bind_inputs(1); CALL bind_inputs(2); CALL bind_inputs(3)
+  DO k = 1, 3   ! the u/v grids alias the t-grid arrays
+    CALL chk(fcx_bind_field(eng, 1_c_int, INT(k, c_int), QSUR, c_loc(lqs), INT(n, c_int64_t), FCX_ALLOCATED), 'b')
+  END DO
+  CALL chk(fcx_bind_field(eng, 1_c_int, 1_c_int, MEVA, c_loc(lme), INT(n, c_int64_t), FCX_ALLOCATED), 'b')
+  CALL chk(fcx_bind_field(eng, 1_c_int, 1_c_int, HLAT, c_loc(lhl), INT(n, c_int64_t), FCX_ALLOCATED), 'b')
+  CALL chk(fcx_bind_field(eng, 1_c_int, 1_c_int, HSEN, c_loc(lhs), INT(n, c_int64_t), FCX_ALLOCATED), 'b')
+  CALL chk(fcx_bind_field(eng, 1_c_int, 1_c_int, RBBR, c_loc(lrb), INT(n, c_int64_t), FCX_ALLOCATED), 'b')
+  CALL chk(fcx_bind_field(eng, 1_c_int, 2_c_int, UMOM, c_loc(lum), INT(n, c_int64_t), FCX_ALLOCATED), 'b')
+  CALL chk(fcx_bind_field(eng, 1_c_int, 3_c_int, VMOM, c_loc(lvm), INT(n, c_int64_t), FCX_ALLOCATED), 'b')
+  CALL chk(fcx_set_corrections(eng, 1_c_int, 19610101_c_int32_t, c_loc(corr), INT(n, c_int64_t), &
+                               FCX_CORR_CELL_MAJOR), 'corr')
+  CALL chk(fcx_set_atmos_map(eng, INT(na, c_int64_t), c_loc(aidx), c_loc(aw)), 'atmos map')
+  CALL chk(fcx_add_atmos_field(eng, FCX_PHASE_NORMAL, 1_c_int, 1_c_int, MEVA, c_loc(ao(1, 1)), FCX_MEM_HOST), 'af')
+  CALL chk(fcx_add_atmos_field(eng, FCX_PHASE_NORMAL, 1_c_int, 1_c_int, HLAT, c_loc(ao(1, 2)), FCX_MEM_HOST), 'af')
+  CALL chk(fcx_add_atmos_field(eng, FCX_PHASE_NORMAL, 1_c_int, 1_c_int, HSEN, c_loc(ao(1, 3)), FCX_MEM_HOST), 'af')
+  CALL chk(fcx_add_atmos_field(eng, FCX_PHASE_NORMAL, 1_c_int, 2_c_int, UMOM, c_loc(ao(1, 4)), FCX_MEM_HOST), 'af')
+  ! one boundary slot for the last atmosphere cell (with one rank the all-reduce is the
+  ! identity, so the completed value is the full sum)
+  CALL chk(fcx_set_atmos_boundaries(eng, 1_c_int32_t, -1_c_int32_t, 0_c_int32_t), 'boundaries')
+  CALL chk(fcx_set_comm(eng, comm), 'set comm')
+  CALL chk(fcx_commit(eng), 'commit')
+  CALL chk(fcx_zero_copy_bytes(eng, zc), 'zero copy bytes')
+  IF (zc <= 0) THEN
+    WRITE (*, *) 'library arrays were not used in place'
+    STOP 1
+  END IF
+  CALL chk(fcx_step(eng, FCX_PHASE_ALL, t_step), 'step')
+  CALL chk(fcx_destroy(eng), 'destroy')
+  CALL chk(fcx_comm_destroy(comm), 'comm destroy')
+  DO j = 1, n   ! CCLM reference again
+    CALL flux_radiation_blackbody_StBo(r_rb(j), ts(j))
+    CALL spec_vapor_surface_cclm(r_qs(j), fi(j), ps(j), ts(j))
+    CALL flux_mass_evap_cclm(r_me(j), ai(j), ps(j), qa(j), r_qs(j), ta(j), u(j), v(j))
+    r_me(j) = r_me(j) + corr(month, j)
+    CALL flux_heat_latent_water(r_hl(j), r_me(j))
+    CALL flux_heat_sensible_cclm(r_hs(j), ai(j), pa(j), ps(j), qa(j), ta(j), ts(j), u(j), v(j))
+    CALL flux_momentum_cclm(r_um(j), dummy, am(j), ps(j), r_qs(j), ts(j), u(j), v(j))
+    CALL flux_momentum_cclm(dummy, r_vm(j), am(j), ps(j), r_qs(j), ts(j), u(j), v(j))
+  END DO
+  worst = MAX(worst, err(lqs, r_qs), err(lme, r_me), err(lhl, r_hl), err(lhs, r_hs), err(lrb, r_rb), &
+              err(lum, r_um), err(lvm, r_vm))
+  WRITE (*, '(A,ES12.4)') 'library arrays + accumulation + comm, max mixed error ', worst
+  DO f = 1, nfa   ! sequential SCRIP sums of the engine's own fluxes, increasing exchange cell
+    want = 0.0_dp
+    DO j = 1, n
+      SELECT CASE (f)
+      CASE (1); want(aidx(j) + 1) = want(aidx(j) + 1) + aw(j) * lme(j)
+      CASE (2); want(aidx(j) + 1) = want(aidx(j) + 1) + aw(j) * lhl(j)
+      CASE (3); want(aidx(j) + 1) = want(aidx(j) + 1) + aw(j) * lhs(j)
+      CASE (4); want(aidx(j) + 1) = want(aidx(j) + 1) + aw(j) * lum(j)
+      END SELECT
+    END DO
+    IF (ANY(ao(:, f) /= want)) THEN
+      WRITE (*, *) 'atmosphere field ', f, ' differs from the sequential sum: ', COUNT(ao(:, f) /= want), ' cells'
+      STOP 1
+    END IF
+  END DO
+  DO k = 1, 8
+    CALL chk(fcx_host_free(blk(k)), 'host_free')
+  END DO
+
   IF (worst <= 1.0e-10_dp) THEN
     WRITE (*, '(A,ES12.4)') 'FCX_FORTRAN_SELFTEST OK ', worst
   ELSE
@@ -134,6 +237,23 @@ CONTAINS
       CALL chk(fcx_bind_field(eng, 1_c_int, gg, HSEN, c_loc(hs), nn, FCX_ALLOCATED), 'b')
       CALL chk(fcx_bind_field(eng, 1_c_int, gg, RBBR, c_loc(rb), nn, FCX_ALLOCATED), 'b')
     END IF
+  END SUBROUTINE
+
+  SUBROUTINE bind_inputs(g)   ! the t-grid inputs under every grid (aliases)
+    INTEGER, INTENT(IN) :: g
+    INTEGER(c_int) :: gg
+    INTEGER(c_int64_t) :: nn
+    gg = INT(g, c_int); nn = INT(n, c_int64_t)
+    CALL chk(fcx_bind_field(eng, 1_c_int, gg, FICE, c_loc(fi), nn, FCX_ALLOCATED), 'b')
+    CALL chk(fcx_bind_field(eng, 1_c_int, gg, PSUR, c_loc(ps), nn, FCX_ALLOCATED), 'b')
+    CALL chk(fcx_bind_field(eng, 1_c_int, gg, TSUR, c_loc(ts), nn, FCX_ALLOCATED), 'b')
+    CALL chk(fcx_bind_field(eng, 1_c_int, gg, PATM, c_loc(pa), nn, FCX_ALLOCATED), 'b')
+    CALL chk(fcx_bind_field(eng, 1_c_int, gg, QATM, c_loc(qa), nn, FCX_ALLOCATED), 'b')
+    CALL chk(fcx_bind_field(eng, 1_c_int, gg, TATM, c_loc(ta), nn, FCX_ALLOCATED), 'b')
+    CALL chk(fcx_bind_field(eng, 1_c_int, gg, UATM, c_loc(u), nn, FCX_ALLOCATED), 'b')
+    CALL chk(fcx_bind_field(eng, 1_c_int, gg, VATM, c_loc(v), nn, FCX_ALLOCATED), 'b')
+    CALL chk(fcx_bind_field(eng, 1_c_int, gg, AMOI, c_loc(ai), nn, FCX_ALLOCATED), 'b')
+    CALL chk(fcx_bind_field(eng, 1_c_int, gg, AMOM, c_loc(am), nn, FCX_ALLOCATED), 'b')
   END SUBROUTINE
 
   FUNCTION err(x, r) RESULT(e)   ! SURVEY.md 8d mixed metric
