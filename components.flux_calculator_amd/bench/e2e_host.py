@@ -62,7 +62,9 @@ SWEEP = [("pageable, sequential", {"pin_host": 0, "pipeline_chunks": 1}),
          ("pinned, 4 chunks", {"pin_host": 1, "pipeline_chunks": 4}),
          ("pinned, 8 chunks", {"pin_host": 1, "pipeline_chunks": 8}),
          ("pinned, 16 chunks", {"pin_host": 1, "pipeline_chunks": 16}),
-         ("zero-copy", {"zero_copy": 1})]
+         ("zero-copy", {"zero_copy": 1}),                       # arrays from fcx_host_malloc
+         ("library arrays, 8 chunks", {"zero_copy": 0, "pipeline_chunks": 8})]
+LIBRARY_ARRAYS = ("zero-copy", "library arrays, 8 chunks")
 N_IN = {"CCLM": 10, "MOM5": 11, "RCO": 5}
 N_OUT = {"CCLM": 7, "MOM5": 7, "RCO": 6}
 
@@ -79,6 +81,11 @@ def child(a):
         print(json.dumps(link_ceiling(N_IN[a.variants] * 8 * n, N_OUT[a.variants] * 8 * n)))
         return
     case = build_case(a.variants, n=n, T=1, data=inputs_for_bench(n))
+    if a.only in LIBRARY_ARRAYS:  # the host allocated its arrays with fcx_host_malloc
+        from fcx.host_alloc import Arena
+
+        arena = Arena()
+        arena.adopt(case.lf)
     opts = {**dict(SWEEP)[a.only], "timing": 1}  # device_timeline_ms / kernel_ms below
     eng = Engine(case.lf, 1, case.methods, options=opts)
     pinned = eng.pinned_bytes()

@@ -40,6 +40,12 @@ def main():
     ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--variants", default=",".join(VARIANTS))
     ap.add_argument("--atmos", type=int, default=1, help="0: flux pass only (no accumulation)")
+    ap.add_argument("--opts", action="append", default=[],
+                    help="NAME:key=val[,key=val] -- another engine set of the main build with these "
+                         "fcx_set_option values (e.g. split0:type_split=0)")
+    ap.add_argument("--host", action="store_true",
+                    help="bind host arrays: every build's engines own their (tile-blocked) device "
+                         "mirrors, uploaded once -- the bench's layout; builds then differ in placement")
     a = ap.parse_args()
 
     import torch
@@ -49,7 +55,11 @@ def main():
     from fcx.parallel import PeriodicAtmosMap
     from fcx.synthetic import build_case, inputs_for_bench
 
-    libs, no_atmos = {"ref": None}, set()
+    libs, no_atmos, extra_opts = {"ref": None}, set(), {}
+    for spec in a.opts:
+        name, kv = spec.split(":", 1)
+        libs[name] = None
+        extra_opts[name] = {k: int(v) for k, v in (x.split("=") for x in kv.split(","))}
     for spec in a.lib:
         name, path = spec.split("=", 1)
         if path.endswith(":atmos0"):
@@ -60,14 +70,18 @@ def main():
     n = a.cells
     dev = torch.device("cuda", 0)
     host = inputs_for_bench(n)
-    data = {k: torch.as_tensor(v).to(dev) for k, v in host.items()}
-    del host
+    if a.host:
+        data, cdev = host, None
+    else:
+        data, cdev = {k: torch.as_tensor(v).to(dev) for k, v in host.items()}, dev
+        del host
     stream = torch.cuda.current_stream(dev)
     la = PeriodicAtmosMap().local(0, n, 0, 1, n)
     cases, outs = [], []
     for v in variants:
-        cases.append(build_case(v, n=n, T=a.types, device=dev, data=data if a.types == 1 else None))
-        outs.append({name: torch.empty(max(la.n_atmos, 1), dtype=torch.float64, device=dev)
+        cases.append(build_case(v, n=n, T=a.types, device=cdev, data=data if a.types == 1 else None))
+        outs.append({name: (np.empty(max(la.n_atmos, 1)) if a.host else
+                            torch.empty(max(la.n_atmos, 1), dtype=torch.float64, device=dev))
                      for name, _ in FIELDS})
     s0 = 0 if a.types >= 2 else 1
     engines = {}
@@ -77,8 +91,11 @@ def main():
                    device=0, stream=stream.cuda_stream,
                    atmos=({"local": la, "fields": [(PHASE_NORMAL, s0, g, name, o[name]) for name, g in FIELDS]}
                           if a.atmos and lname not in no_atmos else None),
-                   options={"atmos_in_run": 0, "timing": 0}, lib=lib)
+                   options={"atmos_in_run": 0, "timing": 0, "pin_host": 0, **extra_opts.get(lname, {})}, lib=lib)
             for c, o in zip(cases, outs)]
+        if a.host:
+            for e in engines[lname]:
+                e.upload(PHASE_ALL)
     alg = {k: [es[i].algorithmic_bytes(PHASE_ALL) for i in range(len(variants))] for k, es in engines.items()}
 
     def step(es, t, ev=None):

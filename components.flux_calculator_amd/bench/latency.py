@@ -108,14 +108,14 @@ def main():
         e.close()
 
     # ---- host-bound: fcx_step per variant (upload, run, download, synchronise)
-    # host_mirrors: caller heap arrays, device mirrors (the default for heap arrays);
-    # host_zero_copy: caller heap arrays registered and used in place (FCX_OPT_ZERO_COPY=1);
-    # host_library_arrays: arrays from fcx_host_malloc, used in place by default (auto)
+    # host_mirrors: caller heap arrays, device mirrors (caller heap arrays always take them);
+    # host_library_arrays: arrays from fcx_host_malloc, used in place by default (auto
+    # zero-copy); host_library_mirrors: the same arrays through mirrors (FCX_OPT_ZERO_COPY=0)
     from fcx.host_alloc import Arena
 
-    for mode, opts, lib_arrays in (("host_mirrors", {"zero_copy": 0}, False),
-                                   ("host_zero_copy", {"zero_copy": 1}, False),
-                                   ("host_library_arrays", {}, True)):
+    for mode, opts, lib_arrays in (("host_mirrors", {}, False),
+                                   ("host_library_arrays", {}, True),
+                                   ("host_library_mirrors", {"zero_copy": 0}, True)):
         hb = {}
         for v in VARIANTS:
             c = build_case(v, n=n, T=1, bias=bool(a.bias), data=host)

@@ -175,7 +175,6 @@ struct fcx_engine {
   // is allowed)
   int zero_copy = 2;
   bool zc_active = false;        // some field array is used in place (host-mapped)
-  bool zc_mapped_flags = false;  // caller ranges registered mapped (FCX_OPT_ZERO_COPY = 1)
   int64_t zc_bytes = 0;          // bytes of host arrays used in place
   // ev0/ev1 around every run (fcx_last_kernel_ms).  Off by default: on the 32K-cell grid the
   // two event records per run made the 3-variant step 41 us instead of 16.5 us
@@ -1066,7 +1065,7 @@ static void pin_host_arrays(fcx_engine *e) {
     else
       m.push_back(x);
   }
-  const unsigned flags = e->zc_mapped_flags ? hipHostRegisterMapped : hipHostRegisterDefault;
+  const unsigned flags = hipHostRegisterDefault;
   for (auto &x : m)
     if (pin_range(x.first, x.second, flags))
       e->pinned.push_back({reinterpret_cast<char *>(x.first), x.second - x.first});
@@ -1077,30 +1076,15 @@ static void unpin_host_arrays(fcx_engine *e) {
   e->pinned.clear();
 }
 
-// Zero-copy (FCX_OPT_ZERO_COPY): a host array is used by the kernels in place through its
-// device-visible address -- no device mirror, no copy call; the cells kernel streams it over
-// the host link.  For the latency-bound small grids this replaces ~17 copy calls per step
-// by one launch.  Candidates: arrays inside fcx_host_malloc blocks (auto and on), and with
-// FCX_OPT_ZERO_COPY = 1 also caller arrays inside this engine's page-locked ranges.  Every
-// other array keeps a mirror.  Returns the number of arrays used in place.
-static int map_host_arrays(fcx_engine *e, bool caller_ranges) {
-  auto mapped = [&](void *host, size_t bytes) -> void * {
-    if (void *d = lib_block_device_ptr(host, bytes)) return d;
-    if (!caller_ranges) return nullptr;
-    const uintptr_t h = reinterpret_cast<uintptr_t>(host);
-    for (auto &r : e->pinned) {
-      const uintptr_t a = reinterpret_cast<uintptr_t>(r.first);
-      if (h >= a && h + bytes <= a + r.second) {
-        void *d = nullptr;
-        if (hipHostGetDevicePointer(&d, r.first, 0) != hipSuccess || !d) {
-          (void)hipGetLastError();
-          return nullptr;
-        }
-        return reinterpret_cast<char *>(d) + (h - a);
-      }
-    }
-    return nullptr;
-  };
+// Zero-copy (FCX_OPT_ZERO_COPY): a host array inside an fcx_host_malloc block is used by the
+// kernels in place through its device-visible address -- no device mirror, no copy call; the
+// cells kernel streams it over the host link.  For the latency-bound small grids this
+// replaces ~17 copy calls per step by one launch.  Caller heap arrays are never used in
+// place: GPU access to them goes through a hipHostRegister (userptr) mapping, and twice a
+// kernel access through such a mapping missed the page it addressed.
+// Every other array keeps a mirror.  Returns the number of arrays used in place.
+static int map_host_arrays(fcx_engine *e) {
+  auto mapped = [&](void *host, size_t bytes) -> void * { return lib_block_device_ptr(host, bytes); };
   int count = 0;
   for (auto &bf : e->bufs) {
     if (bf.external || !bf.host) continue;
@@ -1269,17 +1253,14 @@ extern "C" int fcx_commit(fcx_engine *e) {
   if (e->committed) return FCX_OK;
   if (int r = validate(e)) return r;
   if (int r = gpu_init(e)) return r;
-  // Zero-copy.  1: every host array in place (library blocks, and caller arrays page-locked
-  // and mapped here).  2 (auto, default): library blocks in place where the pipelined step
-  // would not apply (grids below two chunks, where the step is latency-bound and per-array
-  // copies dominate it); caller heap arrays always take mirrors (in-place
-  // use of registered caller memory is opt-in).  0: mirrors for everything.
+  // Zero-copy of fcx_host_malloc arrays.  2 (auto, default): where the pipelined step would
+  // not apply (grids below two chunks, where the step is latency-bound and per-array copies
+  // dominate it); 1: at any size; 0: never.  Caller heap arrays always take mirrors, fed by
+  // DMA from their page-locked ranges (FCX_OPT_PIN_HOST) or staged copies.
   const int64_t n_big = std::max(e->n[0], std::max(e->n[1], e->n[2]));
   const bool small = n_big < 2 * e->min_chunk;
-  const bool caller_zc = e->zero_copy == 1;
-  e->zc_mapped_flags = caller_zc;
-  if (e->pin_host || caller_zc) pin_host_arrays(e);
-  if (caller_zc || (e->zero_copy == 2 && small)) e->zc_active = map_host_arrays(e, caller_zc) > 0;
+  if (e->pin_host) pin_host_arrays(e);
+  if (e->zero_copy == 1 || (e->zero_copy == 2 && small)) e->zc_active = map_host_arrays(e) > 0;
   bool any_external = false;
   for (auto &bf : e->bufs) any_external = any_external || bf.external;
   if (e->tiled_opt && !any_external && !e->bufs.empty()) {
@@ -2038,6 +2019,9 @@ extern "C" int fcx_set_option(fcx_engine *e, int option, int64_t value) {
     case FCX_OPT_PIPELINE_CHUNKS:
       if (value < 1 || value > 1024) return fail(FCX_E_ARG, "pipeline chunks %lld outside 1..1024", (long long)value);
       e->chunks = (int)value;
+      return FCX_OK;
+    case FCX_OPT_TYPE_SPLIT:
+      e->launch.type_split = value != 0;
       return FCX_OK;
     case FCX_OPT_TEST_HANDOFF_TIMEOUT:
       e->test_handoff_timeout = value != 0;

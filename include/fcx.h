@@ -252,21 +252,21 @@ enum fcx_option {
                                    over this many cell chunks (default 8; 1 = sequential) */
   FCX_OPT_PIPELINE_MIN_CHUNK = 8, /* ... of at least this many cells (multiple of 1024;
                                    default 262144: smaller grids take the sequential step) */
-  FCX_OPT_ZERO_COPY = 9,        /* host-bound fields read/written by the kernels in place
-                                   through the host link (page-locked, mapped): no mirrors,
-                                   no copy calls.  2 auto (default): arrays allocated by
-                                   fcx_host_malloc, when every grid is below
-                                   2 x PIPELINE_MIN_CHUNK cells; caller heap arrays take
-                                   device mirrors.  1 on: every host array, caller heap
-                                   arrays page-locked and mapped at fcx_commit (the caller
-                                   must not free or remap them while the engine lives).
-                                   0 off: device mirrors for everything */
+  FCX_OPT_ZERO_COPY = 9,        /* fields in fcx_host_malloc memory read/written by the
+                                   kernels in place through the host link: no mirrors, no
+                                   copy calls.  2 auto (default): when every grid is below
+                                   2 x PIPELINE_MIN_CHUNK cells; 1: at any size; 0: never.
+                                   Caller heap arrays always take device mirrors */
   FCX_OPT_TIMING = 10,          /* record the events behind fcx_last_kernel_ms (default 0:
                                    two event records per run cost ~8 us on small grids) */
   FCX_OPT_TEST_HANDOFF_TIMEOUT = 12, /* test hook (default 0): report every fused launch's
                                    carry hand-off as timed out, so that the recovery of
                                    fcx_synchronize (atmos_kernel recomputes the atmosphere
                                    outputs) runs; the results must be unchanged            */
+  FCX_OPT_TYPE_SPLIT = 13,      /* several surface types with every type-0 average in
+                                   registers: one wave per surface type, the averages summed
+                                   from LDS in type order (default 1; 0 = one wave walks the
+                                   types of its cells in sequence)                          */
   FCX_OPT_TILED_LAYOUT = 11     /* engine-owned mirrors tile-blocked (default 1): tiles of
                                    4096 cells, the read-only arrays' tiles interleaved in
                                    one pool and the written arrays' in another, so a wave's

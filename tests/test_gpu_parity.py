@@ -52,14 +52,21 @@ def test_fused_t1(variant, bias, n):
 @pytest.mark.parametrize("variant", ["CCLM", "MOM5", "RCO"])
 @pytest.mark.parametrize("zero_copy", [0, 1])
 def test_fused_t1_host_modes(variant, zero_copy):
-    """Host-bound fields through device mirrors (copies, the default) and through zero-copy
-    mapping (FCX_OPT_ZERO_COPY=1): same oracle parity either way."""
+    """Host-bound fields through device mirrors (copies) and, for arrays allocated by
+    fcx_host_malloc, through zero-copy mapping (FCX_OPT_ZERO_COPY=1): same oracle parity."""
+    from fcx.host_alloc import Arena
+
     case = build_case(variant, n=10_007, T=1, bias=True)
     ref = oracle_lib.run_case(case, "c", current_step_time=STEP_T)
+    arena = Arena()
+    if zero_copy:
+        arena.adopt(case.lf)
     eng = engine_for(case, options={"zero_copy": zero_copy})
+    assert eng.zero_copy_active() == bool(zero_copy)
     eng.step(PHASE_ALL, STEP_T)
     got = outputs(case)
     eng.close()
+    arena.close()
     assert_parity(got, ref, label=f"{case.name} zero_copy={zero_copy}")
 
 

@@ -18,6 +18,16 @@ from fcx.synthetic import build_case  # noqa: E402
 STEP_T = 3600 * 24 * 40
 
 
+def library(case):
+    """The case's arrays moved into library-allocated page-locked memory (fcx_host_malloc),
+    which the kernels use in place (zero-copy); close the returned arena after the engines."""
+    from fcx.host_alloc import Arena
+
+    arena = Arena()
+    arena.adopt(case.lf)
+    return arena
+
+
 def run(case, options, atmos_n=None):
     """One fcx_step on fresh copies of the case's outputs; returns the outputs (and the
     atmosphere fields when atmos_n is given)."""
@@ -166,8 +176,10 @@ def steps_with_changing_inputs(case, options, steps=3):
 @pytest.mark.parametrize("variant", ["CCLM", "MOM5", "RCO"])
 def test_zero_copy_matches_mirrors_over_steps(variant):
     case = build_case(variant, n=40_001, T=1, bias=True)
+    arena = library(case)
     zc = steps_with_changing_inputs(case, {"zero_copy": 1})
     mir = steps_with_changing_inputs(case, {"zero_copy": 0, "pipeline_chunks": 1})
+    arena.close()
     for a, b in zip(zc, mir):
         same_bits(a, b)
     assert not any(np.isnan(v).any() for v in zc[-1].values())
@@ -175,24 +187,30 @@ def test_zero_copy_matches_mirrors_over_steps(variant):
 
 def test_zero_copy_generic_separate_grids_averages_and_atmosphere():
     case = build_case("CCLM", n=9_001, T=3, sep_grids=(8_999, 9_011), bias=True)
+    arena = library(case)
     same_bits(run(case, {"zero_copy": 1}), run(case, {"zero_copy": 0}))
     ref = oracle_lib.run_case(case, "c", current_step_time=STEP_T)
     assert_parity(run(case, {"zero_copy": 1}), ref, label="zero-copy T3 sep")
+    arena.close()
     c1 = build_case("MOM5", n=30_001, T=1, bias=True)
+    arena = library(c1)
     same_bits(run(c1, {"zero_copy": 1}, atmos_n=30_001), run(c1, {"zero_copy": 0}, atmos_n=30_001))
+    arena.close()
 
 
 def test_zero_copy_per_call_dropin():
-    """The per-call reference subroutines on a zero-copy engine (no copies at all)."""
+    """The per-call reference subroutines on a zero-copy engine over library arrays (no
+    copies at all; each kernel reads the previous call's outputs in host memory)."""
     from fcx.basic import IDX
 
     case = build_case("CCLM", n=5_003, T=2, bias=True)
     ref = oracle_lib.run_case(case, "c", current_step_time=STEP_T)
+    arena = library(case)
     for k in case.outputs:
         case.lf.field[k][:] = np.nan
     eng = Engine(case.lf, 2, case.methods, corrections=case.corrections, averages=case.averages,
                  options={"zero_copy": 1})
-    assert eng.pinned_bytes() > 0
+    assert eng.zero_copy_bytes() > 0 and eng.pinned_bytes() == 0
     lib, h = eng.lib, eng.h
     assert lib.fcx_calc_flux_radiation_blackbody(h) == 0
     for g in (1, 2, 3):
@@ -206,6 +224,7 @@ def test_zero_copy_per_call_dropin():
         assert lib.fcx_average_across_surface_types(h, g, IDX[name]) == 0
     got = {k: np.array(case.lf.field[k], copy=True) for k in case.outputs}
     eng.close()
+    arena.close()
     assert_parity(got, ref, label="zero-copy per call")
 
 

@@ -1,18 +1,23 @@
-"""Zero-copy and page-lock hazards, each forced deterministically.
+"""Host memory transports and the page-lock registry, each hazard forced deterministically
+(DESIGN.md section 5).
 
-Round 1 saw one non-finite MEVA in one full-suite run of test_fused_t1[4097-False-MOM5]
-(zero-copy on caller heap arrays), with HLAT -- computed from the same in-register MEVA --
-right.  Every mechanism that could lose a kernel store between the kernel and the host
-array is set up here on purpose, instead of hoping for the suite order to recreate it:
+Kernels used caller heap arrays in place (zero-copy through hipHostRegister mappings) until
+round 2; twice that lost data: round 1 a MEVA whose stores never reached the host array,
+round 2 an HLAT computed from MEVA read one 4 KiB page off (cells 2414.. got the values of
+cells 2926..).  Kernels now use only library-allocated memory (fcx_host_malloc) in place;
+caller heap arrays take device mirrors fed by DMA from their page-locked ranges.  Set up
+here on purpose:
 
-  * an output whose page meets another live engine's registration (it stays pageable with a
-    device mirror inside a zero-copy engine), before and after that engine is closed;
+  * an output whose page meets another live engine's registration (it stays pageable:
+    staged copies), before and after that engine is closed;
   * an engine dropped without close() and collected by the garbage collector between the
     commit and the step of a new engine over fresh arrays;
   * two live engines over the same arrays (a registration shared by reference count), one
     closed before the other steps;
-  * non-temporal against plain stores to host-mapped memory;
-  * library-allocated page-locked arrays (fcx_host_malloc), the default zero-copy path.
+  * library arrays in place with non-temporal and plain accesses, over several steps with
+    the host rewriting inputs, and a per-call chain where each kernel reads the previous
+    kernel's outputs in host memory;
+  * caller heap arrays are never used in place, whatever FCX_OPT_ZERO_COPY says.
 """
 import gc
 
@@ -71,15 +76,14 @@ def carve(cases, first_key=None):
     return buf
 
 
-@pytest.mark.parametrize("zero_copy", [1, 2])
-def test_output_page_shared_with_another_live_engine(zero_copy):
+def test_output_page_shared_with_another_live_engine():
     """Case B's MEVA begins on the page where case A's arrays end: in B it cannot be
-    page-locked exclusively, so it keeps a device mirror inside a zero-copy engine."""
+    page-locked exclusively, so its copies are staged."""
     a = build_case("MOM5", n=4097, T=1)
     b = build_case("MOM5", n=4097, T=1)
     keep = carve([a, b], first_key=(1, 1, "MEVA"))
-    ea = engine_for(a, zero_copy=zero_copy)
-    eb = engine_for(b, zero_copy=zero_copy)
+    ea = engine_for(a)
+    eb = engine_for(b)
     eb.step(PHASE_ALL, T_STEP)
     check(b, "B with A live")
     ea.step(PHASE_ALL, T_STEP)
@@ -102,10 +106,10 @@ def test_engine_collected_between_commit_and_step():
     new engine over fresh arrays has committed and before it steps."""
     for n in (4097, 10_007):
         a = build_case("MOM5", n=n, T=1)
-        _Cycle(engine_for(a, zero_copy=1), a)  # unreachable, alive until gc.collect()
+        _Cycle(engine_for(a), a)  # unreachable, alive until gc.collect()
         del a
         b = build_case("MOM5", n=n, T=1)
-        eb = engine_for(b, zero_copy=1)
+        eb = engine_for(b)
         gc.collect()  # the old engine's fcx_destroy runs here: its page locks are dropped
         eb.step(PHASE_ALL, T_STEP)
         check(b, f"n={n} after collecting the old engine")
@@ -116,8 +120,8 @@ def test_registration_shared_by_two_engines():
     """Two live engines over the same arrays share one registration (reference count);
     closing the first leaves the second's mapping intact."""
     c = build_case("CCLM", n=4097, T=1, bias=True)
-    e1 = engine_for(c, zero_copy=1)
-    e2 = engine_for(c, zero_copy=1)
+    e1 = engine_for(c)
+    e2 = engine_for(c)
     e1.step(PHASE_ALL, T_STEP)
     check(c, "first engine")
     e1.close()
@@ -129,16 +133,49 @@ def test_registration_shared_by_two_engines():
 
 @pytest.mark.parametrize("nontemporal", [0, 1])
 def test_host_mapped_stores(nontemporal):
-    """Stores to host-mapped arrays: the engine drops the non-temporal hint for mapped
-    fields whatever FCX_OPT_NONTEMPORAL says; the results are the same either way."""
+    """Library arrays in place: the engine drops the non-temporal hint for mapped fields
+    whatever FCX_OPT_NONTEMPORAL says; the results are the same either way."""
     for v in ("CCLM", "MOM5", "RCO"):
         c = build_case(v, n=4097, T=1)
-        e = engine_for(c, zero_copy=1, nontemporal=nontemporal)
-        for _ in range(3):
-            reset_outputs(c)
-            e.step(PHASE_ALL, T_STEP)
-            check(c, f"{v} nt={nontemporal}")
-        e.close()
+        with host_alloc.Arena() as arena:
+            arena.adopt(c.lf)
+            e = engine_for(c, zero_copy=1, nontemporal=nontemporal)
+            assert e.zero_copy_active()
+            for _ in range(3):
+                reset_outputs(c)
+                e.step(PHASE_ALL, T_STEP)
+                check(c, f"{v} nt={nontemporal}")
+            e.close()
+
+
+def test_library_arrays_per_call_chain():
+    """The per-call reference subroutines on library arrays in place: each kernel reads what
+    the previous call's kernel wrote to host memory (QSUR -> MEVA -> HLAT -> averages)."""
+    from fcx.basic import IDX
+
+    STEP = 3600 * 24 * 40
+    case = build_case("CCLM", n=5_003, T=2, bias=True)
+    ref = oracle_lib.run_case(case, "c", current_step_time=STEP)
+    with host_alloc.Arena() as arena:
+        arena.adopt(case.lf)
+        reset_outputs(case)
+        eng = Engine(case.lf, 2, case.methods, corrections=case.corrections, averages=case.averages,
+                     options={"zero_copy": 1})
+        assert eng.zero_copy_active()
+        lib, h = eng.lib, eng.h
+        assert lib.fcx_calc_flux_radiation_blackbody(h) == 0
+        for g in (1, 2, 3):
+            assert lib.fcx_calc_spec_vapor_surface(h, g) == 0
+        assert lib.fcx_calc_flux_mass_evap(h, STEP) == 0
+        assert lib.fcx_calc_flux_heat_latent(h) == 0
+        assert lib.fcx_calc_flux_heat_sensible(h) == 0
+        assert lib.fcx_calc_flux_momentum_east(h, 2) == 0
+        assert lib.fcx_calc_flux_momentum_north(h, 3) == 0
+        for ph, g, name in case.averages:
+            assert lib.fcx_average_across_surface_types(h, g, IDX[name]) == 0
+        got = {k: np.array(case.lf.field[k], copy=True) for k in case.outputs}
+        eng.close()
+    assert_parity(got, ref, label="library arrays per call")
 
 
 @pytest.mark.parametrize("variant", ["CCLM", "MOM5", "RCO"])
@@ -162,10 +199,11 @@ def test_library_pinned_arrays_zero_copy(variant, n):
         e.close()
 
 
-def test_heap_arrays_take_mirrors_by_default():
-    """Caller heap arrays are not used in place unless FCX_OPT_ZERO_COPY=1."""
+@pytest.mark.parametrize("zero_copy", [0, 1, 2])
+def test_heap_arrays_never_used_in_place(zero_copy):
+    """Caller heap arrays take device mirrors whatever FCX_OPT_ZERO_COPY says."""
     c = build_case("CCLM", n=4097, T=1)
-    e = engine_for(c)
+    e = engine_for(c, zero_copy=zero_copy)
     assert not e.zero_copy_active()
     e.step(PHASE_ALL, T_STEP)
     check(c, "mirrors")
