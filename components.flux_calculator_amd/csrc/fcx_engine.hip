@@ -2020,9 +2020,6 @@ extern "C" int fcx_set_option(fcx_engine *e, int option, int64_t value) {
       if (value < 1 || value > 1024) return fail(FCX_E_ARG, "pipeline chunks %lld outside 1..1024", (long long)value);
       e->chunks = (int)value;
       return FCX_OK;
-    case FCX_OPT_TYPE_SPLIT:
-      e->launch.type_split = value != 0;
-      return FCX_OK;
     case FCX_OPT_TEST_HANDOFF_TIMEOUT:
       e->test_handoff_timeout = value != 0;
       return FCX_OK;

@@ -102,7 +102,6 @@ struct LaunchConfig {
   int variant = 0;           // 0 generic, 1 CCLM, 2 MOM5, 3 RCO (T=1 specialisations)
   bool f32 = false;          // fp32 fields (FCX_PRECISION_F32): 4 cells per lane
   bool ravg = false;         // register averages in this plan (Params::ravg_on)
-  bool type_split = true;    // T >= 2 register-average plans: one wave per surface type
   int64_t lo = 0, hi = -1;   // cell range of this launch (lo a multiple of kChunkAlign;
                              // hi < 0: to n_max) -- the pipelined host-bound step
 };

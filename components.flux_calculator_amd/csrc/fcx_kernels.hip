@@ -194,34 +194,25 @@ struct AccLds {
   }
 };
 
-// Where a produced flux goes besides its own array.  RAVG 1: X_s * FARE_s is added to the
+// Where a produced flux goes besides its own array.  RAVG: X_s * FARE_s is added to the
 // type-0 accumulator of its slot (type order, from 0.0 -- calc:377-383) and the averages
-// go to the emitter (the fused atmosphere accumulation) once all types are done.  RAVG 2
-// (types on separate waves, types_atmos_kernel): the product X_s * FARE_s is parked in this
-// type's LDS row of the slot; the type-order sums are formed after a block barrier.
-// RAVG 0: the value of the single surface type goes to the emitter.
-template <int C, class R, int RAVG, class Emit>
+// go to the emitter (the fused atmosphere accumulation) once all types are done; without
+// RAVG the value of the single surface type goes to the emitter.
+template <int C, class R, bool RAVG, class Emit>
 struct Sink {
   const Emit &emit;
   const AvgRegs &ra;
   AccLds<C, R> acc;
   Vec<C, R> fare;
   __device__ __forceinline__ Sink(const Emit &e, const AvgRegs &r, AccLds<C, R> a) : emit(e), ra(r), acc(a) {
-    if constexpr (RAVG == 1) {
+    if constexpr (RAVG) {
 #pragma unroll
       for (int k = 0; k < kAvgSlots; ++k)
         if (ra.out[k]) acc.set(k, splat<C, R>(R(0)));
     }
   }
   __device__ __forceinline__ void operator()(int k, const Vec<C, R> &x) {
-    if constexpr (RAVG == 2) {
-      if (ra.out[k]) {
-        Vec<C, R> p;
-#pragma unroll
-        for (int i = 0; i < C; ++i) p.v[i] = x.v[i] * fare.v[i];
-        acc.set(k, p);
-      }
-    } else if constexpr (RAVG == 1) {
+    if constexpr (RAVG) {
       if (ra.out[k]) {
         Vec<C, R> a = acc.get(k);
 #pragma unroll
@@ -242,15 +233,13 @@ struct Sink {
 // differs from the previous type's (wave-uniform scalar compare).  Inputs are never written
 // by the pass, so a held value is the array's value.
 // TM: 1 = one surface type, fixed at compile time (the held inputs and the type loop
-// vanish): type s_first of the parameter block; 0 = T from the parameter block.  RAVG 1
-// (register averages) needs TM = 0; RAVG 2 (per-type products) processes one type (TM = 1).
-template <int C, bool MERGED, int VAR, bool NT, class R = double, int TM = 1, int RAVG = 0,
+// vanish); 0 = T from the parameter block.  RAVG (register averages) needs TM = 0.
+template <int C, bool MERGED, int VAR, bool NT, class R = double, int TM = 1, bool RAVG = false,
           class Emit = NoEmit>
 __device__ __forceinline__ void process(const Params *__restrict__ P, const double *__restrict__ corr_m,
                                         int64_t j0, const Emit &emit = Emit(),
-                                        AccLds<C, R> acc_lds = AccLds<C, R>{nullptr, 0}, int s_first = 0) {
-  static_assert(!(RAVG == 1 && TM), "register averages need more than one surface type");
-  static_assert(RAVG != 2 || TM, "per-type products: one type per call");
+                                        AccLds<C, R> acc_lds = AccLds<C, R>{nullptr, 0}) {
+  static_assert(!(RAVG && TM), "register averages need more than one surface type");
   const uint32_t stages = P->stages;
   const int T = TM ? 1 : P->num_types;
   const int64_t nt = P->n[0];
@@ -305,7 +294,7 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
     if constexpr (kReload) {  // nothing of the previous type stays live
       ts = fi = ps = pa = qa = ta = u = v = amoi = cmoi = chea = amom = cmom = vel = Vec<C, R>{};
     }
-    const TypeParams &tp = P->type[s + s_first];
+    const TypeParams &tp = P->type[s];
     const TGridPtrs &g = tp.t;
     constexpr int8_t kVarMethod = VAR == 1 ? FCX_CCLM : VAR == 2 ? FCX_MOM5 : FCX_RCO;
     const int8_t m_q = VAR ? (VAR == 3 ? FCX_NONE : FCX_CCLM) : tp.m_qsur[0];
@@ -336,8 +325,8 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
         HOLD(cmom, uv[0], cmom)
       }
       if (wind_new) FOR_C vel.v[i] = wind(u.v[i], v.v[i]);
-      if constexpr (RAVG != 0) {
-        if (P->ravg_on) sink.fare = LD(P->ravg.fare[s + s_first], j0, nt);
+      if constexpr (RAVG) {
+        if (P->ravg_on) sink.fare = LD(P->ravg.fare[s], j0, nt);
         sink(A_TSUR, ts);
       }
 
@@ -445,7 +434,7 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
 #undef HOLD
 
   // ---- average_across_surface_types (calc:376-383), summed in type order
-  if constexpr (RAVG == 1) {
+  if constexpr (RAVG) {
     if (do_t) {
 #pragma unroll
       for (int k = 0; k < kAvgSlots; ++k) {
@@ -795,126 +784,6 @@ __global__ __launch_bounds__(64 * atmos_waves<C>(), RAVG ? FCX_RAVG_ATMOS_BLOCKS
   }
 }
 
-// Several surface types (T >= 2) with every type-0 average in registers (RAVG plans),
-// one surface type per wave.  The multi-type cells_atmos_kernel walks the types of a tile
-// in sequence on one wave: the loads of type s+1 wait for the arithmetic of type s, and the
-// atmosphere inputs every type shares (basic:334-358) are fetched again per type.  Here the
-// T waves of a tile run its types side by side, each a T = 1-shaped wave (TM = 1: no type
-// loop, the T = 1 register budget), so every wave has one type's latency chain and the
-// shared inputs are read by T waves of one CU at about the same time.  Each wave parks
-// X_s * FARE_s of every register-average slot in its type's LDS rows (Sink mode 2); after
-// a block barrier the tile's first wave forms the averages in type order from 0.0
-// (calc:377-383: the same products added in the same order, bit-identical to the
-// sequential sum), stores them, turns them into the accumulation products w * X_0 in place
-// (ATM) and finishes the tile exactly as cells_atmos_kernel does.  Block: tpb tiles x T
-// waves (tpb = 4 / T for T <= 4, else 1), one tile per wave and trip; KW = waves per block
-// the kernel is compiled for.  LDS (dynamic): [tpb][T][kAvgSlots][row_len] doubles.
-template <int VAR, bool NT, bool ATM, int KW>
-__global__ __launch_bounds__(64 * KW, KW <= 4 ? FCX_RAVG_ATMOS_BLOCKS : 1) void types_atmos_kernel(
-    const Params *__restrict__ P, const double *__restrict__ corr_m, const AtmosFused af, int64_t lo, int64_t hi,
-    int T, int tpb) {
-  constexpr int C = 2;
-  using R = double;
-  constexpr int kT = tile_cells<C>();
-  constexpr int kR = row_len<C>();
-  extern __shared__ double s_prod[];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int tib = wv / T, sty = wv % T;  // tile in block, surface type of this wave
-  double *tbase = s_prod + (size_t)tib * T * kAvgSlots * kR;
-  const int sl = lds_slot(C * lane);
-  const int64_t n = P->n_max, nt = P->n[0];
-  const int64_t n_tiles = (hi + kT - 1) / kT;
-  const int64_t tile = lo / kT + (int64_t)xcd_block(blockIdx.x, gridDim.x) * tpb + tib;
-  const bool live = tile < n_tiles;  // wave-uniform
-  const int64_t t0 = tile * kT, j0 = t0 + C * lane;
-  if (live && j0 < n)
-    process<C, true, VAR, NT, R, 1, 2>(P, corr_m, j0, NoEmit(),
-                                       AccLds<C, R>{tbase + (size_t)sty * kAvgSlots * kR + sl, kR}, sty);
-  __syncthreads();  // every type's products of the tile are in LDS
-  if (!live || sty != 0) return;  // no block barrier follows
-  LdsEmitT<C> emit{tbase, {}, sl};  // type 0's rows double as the accumulation rows
-  int32_t a[C] = {-1, -1};
-  if constexpr (ATM) {
-    if (j0 + C <= n) {
-      const int2 ii = *reinterpret_cast<const int2 *>(af.idx + j0);
-      a[0] = ii.x;
-      a[1] = ii.y;
-      const d2 ww = __builtin_nontemporal_load(reinterpret_cast<const d2 *>(af.w + j0));
-      emit.w[0] = ww[0];
-      emit.w[1] = ww[1];
-    } else {
-#pragma unroll
-      for (int i = 0; i < C; ++i)
-        if (j0 + i < n) {
-          a[i] = af.idx[j0 + i];
-          emit.w[i] = af.w[j0 + i];
-        }
-    }
-  }
-  if (j0 < nt) {  // the averages, in type order from 0.0
-    const int64_t D_ = (j0 >> kLayoutShift) * P->tpad;
-#pragma unroll
-    for (int k = 0; k < kAvgSlots; ++k) {
-      if (!P->ravg.out[k]) continue;
-      Vec<C, R> acc = splat<C, R>(R(0));
-      for (int ss = 0; ss < T; ++ss) {
-        const d2 p = *reinterpret_cast<const d2 *>(tbase + ((size_t)ss * kAvgSlots + k) * kR + sl);
-        acc.v[0] = acc.v[0] + p[0];
-        acc.v[1] = acc.v[1] + p[1];
-      }
-      ST(P->ravg.out[k], j0, nt, acc);
-      if constexpr (ATM) {
-        if (k < kFusedFields) emit(k, acc);  // w * X_0 over type 0's row k (read above)
-      }
-    }
-  }
-  if constexpr (!ATM) return;
-  const uint64_t at_or_above = ~0ull << lane;
-  const uint64_t above = lane == 63 ? 0ull : (~0ull << (lane + 1));
-  double *wp = tbase;
-  const int32_t prev_tile = t0 > 0 ? af.idx[t0 - 1] : -2;
-  const int64_t tend = t0 + kT;
-  const int32_t next_a = (tend < n) ? af.idx[tend] : -3;
-  auto add_cell = [&](double *acc, int e) {
-    const double *q = wp + lds_slot(e);
-#pragma unroll
-    for (int k = 0; k < kFusedFields; ++k) acc[k] = acc[k] + q[k * kR];
-  };
-  int32_t prev = __shfl_up(a[C - 1], 1);
-  if (lane == 0) prev = prev_tile;
-  bool stt[C];
-  uint64_t m[C];
-#pragma unroll
-  for (int i = 0; i < C; ++i) {
-    stt[i] = a[i] != (i ? a[i - 1] : prev);
-    m[i] = __ballot(stt[i]);
-  }
-  wave_sync();
-#pragma unroll
-  for (int i = 0; i < C; ++i) {
-    if (!stt[i] || a[i] < 0) continue;
-    const int c = C * lane + i;
-    int e_end = kT;
-#pragma unroll
-    for (int q = 0; q < C; ++q) e_end = min(e_end, C * first_bit(m[q] & (q > i ? at_or_above : above)) + q);
-    const int end = min(e_end, kT);
-    double acc[kFusedFields];
-#pragma unroll
-    for (int k = 0; k < kFusedFields; ++k) acc[k] = 0.0;
-    for (int e = c; e < end; ++e) add_cell(acc, e);
-    segment_done<R>(af, tile, a[i], acc, end == kT && next_a == a[i]);
-  }
-  if (af.handoff && lane == 0 && a[0] >= 0 && a[0] == prev_tile) {
-    int end = kT;
-#pragma unroll
-    for (int q = 0; q < C; ++q) end = min(end, C * first_bit(m[q]) + q);
-    double acc[kFusedFields];
-    take_carry(af, tile - 1, acc);
-    for (int e = 0; e < end; ++e) add_cell(acc, e);
-    segment_done<R>(af, tile, a[0], acc, end == kT && next_a == a[0]);
-  }
-}
-
 // Segments that straddle a tile boundary: continue the carried prefix sum over the next
 // tile's cells (products recomputed from the stored fluxes, same operations, same order).
 __global__ __launch_bounds__(256) void atmos_fixup_kernel(const AtmosFused af, int64_t n) {
@@ -1134,55 +1003,6 @@ static void launch_atm(bool nt, int blocks, hipStream_t s, const Params *dp, con
                        s, dp, corr_m, af, lo, hi);
 }
 
-// several types, one per wave (types_atmos_kernel); atm: the fused accumulation (else af unused)
-template <int VAR>
-static int launch_types(const Params *hp, const LaunchConfig &lc, hipStream_t s, const Params *dp,
-                        const double *corr_m, const AtmosFused *atm, int64_t lo, int64_t hi) {
-  const int T = hp->num_types;
-  if (T < 2 || T > kMaxTypes) return (int)hipErrorInvalidValue;
-  const int tpb = T <= 4 ? 4 / T : 1;
-  const int64_t tiles = (hi - lo + tile_cells<2>() - 1) / tile_cells<2>();
-  const int blocks = (int)std::max<int64_t>(1, (tiles + tpb - 1) / tpb);
-  const dim3 threads(64 * T * tpb);
-  const size_t lds = (size_t)tpb * T * kAvgSlots * row_len<2>() * sizeof(double);
-  const AtmosFused af = atm ? *atm : AtmosFused{};
-#define FCX_LAUNCH_TYPES(NTV, ATMV, KWV)                                                                   \
-  hipLaunchKernelGGL((types_atmos_kernel<VAR, NTV, ATMV, KWV>), dim3(blocks), threads, lds, s, dp, corr_m, af, lo, \
-                     hi, T, tpb)
-  if (T * tpb <= 4) {
-    if (lc.nontemporal) {
-      if (atm) FCX_LAUNCH_TYPES(true, true, 4); else FCX_LAUNCH_TYPES(true, false, 4);
-    } else {
-      if (atm) FCX_LAUNCH_TYPES(false, true, 4); else FCX_LAUNCH_TYPES(false, false, 4);
-    }
-  } else {
-    if (lc.nontemporal) {
-      if (atm) FCX_LAUNCH_TYPES(true, true, kMaxTypes); else FCX_LAUNCH_TYPES(true, false, kMaxTypes);
-    } else {
-      if (atm) FCX_LAUNCH_TYPES(false, true, kMaxTypes); else FCX_LAUNCH_TYPES(false, false, kMaxTypes);
-    }
-  }
-#undef FCX_LAUNCH_TYPES
-  return 0;
-}
-
-static int launch_types_v(const Params *hp, const LaunchConfig &lc, hipStream_t s, const Params *dp,
-                          const double *corr_m, const AtmosFused *atm, int64_t lo, int64_t hi) {
-  switch (lc.variant) {
-    case 1: return launch_types<1>(hp, lc, s, dp, corr_m, atm, lo, hi);
-    case 2: return launch_types<2>(hp, lc, s, dp, corr_m, atm, lo, hi);
-    case 3: return launch_types<3>(hp, lc, s, dp, corr_m, atm, lo, hi);
-    default: return launch_types<0>(hp, lc, s, dp, corr_m, atm, lo, hi);
-  }
-}
-
-// one wave per surface type applies (types_atmos_kernel): register averages only, u/v grids
-// are the t grid, fp64, 16-B vectors, one trip per wave (no grid-stride cap)
-static bool types_split_ok(const Params *hp, const LaunchConfig &lc) {
-  return lc.type_split && lc.ravg && hp->num_types >= 2 && hp->num_avg == 0 && lc.merged && !lc.f32 &&
-         lc.cells_per_thread == 2 && lc.max_blocks <= 0;
-}
-
 // fused accumulation: one surface type (its fluxes), or several with the type-0 averages in
 // registers (what OASIS sends); several types without register averages are not fused
 template <int VAR>
@@ -1207,10 +1027,6 @@ int launch_cells(const Params *hp, const Params *dp, const double *corr_m, const
   const int64_t lo = lc.lo, hi = lc.hi < 0 ? hp->n_max : std::min<int64_t>(lc.hi, hp->n_max);
   if (lo % kChunkAlign || lo < 0) return (int)hipErrorInvalidValue;
   if (hi <= lo) return 0;
-  if (types_split_ok(hp, lc) && (!atm || lc.variant)) {  // several types, one per wave
-    if (int r = launch_types_v(hp, lc, s, dp, corr_m, atm, lo, hi)) return r;
-    return (int)hipGetLastError();
-  }
   if (atm) {  // fused accumulation: T=1 specialised merged kernel, 2 cells per lane
     // four waves per block (fp32: two), one 128-cell (fp32: 256-cell) tile per wave and trip.  Default: one trip (full
     // grid) -- +2 % per T=1 step over the 8192-block cap, equal at T=2 (profiles/r01/grid_ab)

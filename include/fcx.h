@@ -263,10 +263,6 @@ enum fcx_option {
                                    carry hand-off as timed out, so that the recovery of
                                    fcx_synchronize (atmos_kernel recomputes the atmosphere
                                    outputs) runs; the results must be unchanged            */
-  FCX_OPT_TYPE_SPLIT = 13,      /* several surface types with every type-0 average in
-                                   registers: one wave per surface type, the averages summed
-                                   from LDS in type order (default 1; 0 = one wave walks the
-                                   types of its cells in sequence)                          */
   FCX_OPT_TILED_LAYOUT = 11     /* engine-owned mirrors tile-blocked (default 1): tiles of
                                    4096 cells, the read-only arrays' tiles interleaved in
                                    one pool and the written arrays' in another, so a wave's
