@@ -31,8 +31,8 @@ FIELDS = (("MEVA", 1), ("HLAT", 1), ("HSEN", 1), ("RBBR", 1), ("UMOM", 2), ("VMO
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--lib", action="append", default=[],
-                    help="NAME=PATH[:atmos0] of another build (PATH 'ref': the main build; "
-                         ":atmos0 = that build's engines without the accumulation)")
+                    help="NAME=PATH[:atmos0][@key=val,...] of another build (PATH 'ref': the main build; "
+                         ":atmos0 = that build's engines without the accumulation; @: fcx_set_option values)")
     ap.add_argument("--cells", type=int, default=10_000_000)
     ap.add_argument("--types", type=int, default=1)
     ap.add_argument("--rounds", type=int, default=10)
@@ -62,6 +62,9 @@ def main():
         extra_opts[name] = {k: int(v) for k, v in (x.split("=") for x in kv.split(","))}
     for spec in a.lib:
         name, path = spec.split("=", 1)
+        if "@" in path:
+            path, kv = path.split("@", 1)
+            extra_opts[name] = {k: int(v) for k, v in (x.split("=") for x in kv.split(","))}
         if path.endswith(":atmos0"):
             path = path[: -len(":atmos0")]
             no_atmos.add(name)

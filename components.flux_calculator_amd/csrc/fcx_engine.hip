@@ -72,6 +72,7 @@ struct Plan {
   Params *dev = nullptr;
   std::vector<int> reads, writes;  // buffer ids
   int variant = 0;                 // T=1 specialisation (LaunchConfig::variant)
+  bool pair = false;               // T = 2 without memory-loop averages: cells_pair_kernel
   bool atm_fused = false;          // exchange -> atmosphere accumulation inside the launch
   AtmosFused af{};
   int atm_nf = 0;
@@ -116,6 +117,7 @@ struct fcx_engine {
   bool user_stream = false;
   LaunchConfig launch;      // fcx_set_option
   bool specialize = true;
+  bool type_pair = false;  // FCX_OPT_TYPE_PAIR
   // exchange -> atmosphere accumulation
   struct AtmosField {
     int phase, s, g, var;
@@ -886,6 +888,9 @@ static int build_plan(fcx_engine *e, uint32_t stages, int avg_phases, Plan &pl) 
     }
   }
   P.n_max = n_max;
+  // T = 2: one surface type per half-wave, when every type-0 average of the launch is a
+  // register slot (the memory-loop averages re-read X_s stored by the other half)
+  pl.pair = e->T == 2 && P.merged_uv && P.num_avg == 0;
   pl.reads.assign(reads.begin(), reads.end());
   pl.writes.assign(writes.begin(), writes.end());
   // buffers that are both read and written in the launch are produced there: not inputs
@@ -1320,7 +1325,8 @@ extern "C" int fcx_commit(fcx_engine *e) {
       HIP_TRY(hipMalloc(&e->d_atm_idx, e->atm_idx.size() * sizeof(int32_t)));
       HIP_TRY(hipMemcpy(e->d_atm_idx, e->atm_idx.data(), e->atm_idx.size() * sizeof(int32_t),
                         hipMemcpyHostToDevice));
-      const int64_t tiles = (e->n[0] + kTile - 1) / kTile;
+      // one carry and flag per wave tile: 128 cells (T = 1 fp64), 64 (cells_pair_kernel)
+      const int64_t tiles = (e->n[0] + kPairTileCells - 1) / kPairTileCells;
       HIP_TRY(hipMalloc(&e->d_atm_carry, (size_t)std::max<int64_t>(tiles, 1) * kFusedFields * sizeof(double)));
       HIP_TRY(hipMalloc(&e->d_atm_flag, (size_t)std::max<int64_t>(tiles, 1) * sizeof(uint32_t)));
       HIP_TRY(hipMemset(e->d_atm_flag, 0, (size_t)std::max<int64_t>(tiles, 1) * sizeof(uint32_t)));
@@ -1448,6 +1454,7 @@ static int launch_plan(fcx_engine *e, Plan *pl, const double *corr_m, int64_t lo
   lc.variant = (e->specialize && lc.merged) ? pl->variant : 0;
   lc.f32 = e->f32;
   lc.ravg = pl->host.ravg_on != 0;
+  lc.pair = e->type_pair && pl->pair;
   // the fp32 fused kernel has no fix-up kernel: it needs the in-launch hand-off (no grid cap)
   const bool fused = pl->atm_fused && lc.variant && lc.cells_per_thread == 2 &&
                      (!lc.f32 || (lc.max_blocks <= 0 && pl->af.err != nullptr));
@@ -2022,6 +2029,9 @@ extern "C" int fcx_set_option(fcx_engine *e, int option, int64_t value) {
       return FCX_OK;
     case FCX_OPT_TEST_HANDOFF_TIMEOUT:
       e->test_handoff_timeout = value != 0;
+      return FCX_OK;
+    case FCX_OPT_TYPE_PAIR:
+      e->type_pair = value != 0;
       return FCX_OK;
     case FCX_OPT_TILED_LAYOUT:
       if (e->committed) return fail(FCX_E_STATE, "tiled_layout is applied at fcx_commit");

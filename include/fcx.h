@@ -263,6 +263,10 @@ enum fcx_option {
                                    carry hand-off as timed out, so that the recovery of
                                    fcx_synchronize (atmos_kernel recomputes the atmosphere
                                    outputs) runs; the results must be unchanged            */
+  FCX_OPT_TYPE_PAIR = 13,       /* two surface types (water + ice): both computed side by
+                                   side, one per half-wave, so the atmosphere inputs they
+                                   share are read once and the type-0 averages formed in
+                                   registers (default 0: measured slower than the sequential types)  */
   FCX_OPT_TILED_LAYOUT = 11     /* engine-owned mirrors tile-blocked (default 1): tiles of
                                    4096 cells, the read-only arrays' tiles interleaved in
                                    one pool and the written arrays' in another, so a wave's
