@@ -72,7 +72,6 @@ struct Plan {
   Params *dev = nullptr;
   std::vector<int> reads, writes;  // buffer ids
   int variant = 0;                 // T=1 specialisation (LaunchConfig::variant)
-  bool pair = false;               // T = 2 without memory-loop averages: cells_pair_kernel
   bool atm_fused = false;          // exchange -> atmosphere accumulation inside the launch
   AtmosFused af{};
   int atm_nf = 0;
@@ -117,7 +116,6 @@ struct fcx_engine {
   bool user_stream = false;
   LaunchConfig launch;      // fcx_set_option
   bool specialize = true;
-  bool type_pair = false;  // FCX_OPT_TYPE_PAIR
   // exchange -> atmosphere accumulation
   struct AtmosField {
     int phase, s, g, var;
@@ -169,7 +167,7 @@ struct fcx_engine {
   };
   std::vector<Remap> remaps;
   // host-bound steps: page-locked caller arrays and the H2D / compute / D2H pipeline
-  bool pin_host = true;
+  bool pin_host = false;  // FCX_OPT_PIN_HOST: opt-in
   int chunks = 8;                                   // fcx_step pipeline depth (1 = off)
   int64_t min_chunk = 256 * 1024;                   // cells per chunk at least (~2 MB/array)
   // kernels use the host arrays in place: 0 off, 1 on, 2 auto (default: grids below two
@@ -888,9 +886,6 @@ static int build_plan(fcx_engine *e, uint32_t stages, int avg_phases, Plan &pl) 
     }
   }
   P.n_max = n_max;
-  // T = 2: one surface type per half-wave, when every type-0 average of the launch is a
-  // register slot (the memory-loop averages re-read X_s stored by the other half)
-  pl.pair = e->T == 2 && P.merged_uv && P.num_avg == 0;
   pl.reads.assign(reads.begin(), reads.end());
   pl.writes.assign(writes.begin(), writes.end());
   // buffers that are both read and written in the launch are produced there: not inputs
@@ -1325,8 +1320,7 @@ extern "C" int fcx_commit(fcx_engine *e) {
       HIP_TRY(hipMalloc(&e->d_atm_idx, e->atm_idx.size() * sizeof(int32_t)));
       HIP_TRY(hipMemcpy(e->d_atm_idx, e->atm_idx.data(), e->atm_idx.size() * sizeof(int32_t),
                         hipMemcpyHostToDevice));
-      // one carry and flag per wave tile: 128 cells (T = 1 fp64), 64 (cells_pair_kernel)
-      const int64_t tiles = (e->n[0] + kPairTileCells - 1) / kPairTileCells;
+      const int64_t tiles = (e->n[0] + kTile - 1) / kTile;
       HIP_TRY(hipMalloc(&e->d_atm_carry, (size_t)std::max<int64_t>(tiles, 1) * kFusedFields * sizeof(double)));
       HIP_TRY(hipMalloc(&e->d_atm_flag, (size_t)std::max<int64_t>(tiles, 1) * sizeof(uint32_t)));
       HIP_TRY(hipMemset(e->d_atm_flag, 0, (size_t)std::max<int64_t>(tiles, 1) * sizeof(uint32_t)));
@@ -1454,7 +1448,6 @@ static int launch_plan(fcx_engine *e, Plan *pl, const double *corr_m, int64_t lo
   lc.variant = (e->specialize && lc.merged) ? pl->variant : 0;
   lc.f32 = e->f32;
   lc.ravg = pl->host.ravg_on != 0;
-  lc.pair = e->type_pair && pl->pair;
   // the fp32 fused kernel has no fix-up kernel: it needs the in-launch hand-off (no grid cap)
   const bool fused = pl->atm_fused && lc.variant && lc.cells_per_thread == 2 &&
                      (!lc.f32 || (lc.max_blocks <= 0 && pl->af.err != nullptr));
@@ -2029,9 +2022,6 @@ extern "C" int fcx_set_option(fcx_engine *e, int option, int64_t value) {
       return FCX_OK;
     case FCX_OPT_TEST_HANDOFF_TIMEOUT:
       e->test_handoff_timeout = value != 0;
-      return FCX_OK;
-    case FCX_OPT_TYPE_PAIR:
-      e->type_pair = value != 0;
       return FCX_OK;
     case FCX_OPT_TILED_LAYOUT:
       if (e->committed) return fail(FCX_E_STATE, "tiled_layout is applied at fcx_commit");

@@ -102,7 +102,6 @@ struct LaunchConfig {
   int variant = 0;           // 0 generic, 1 CCLM, 2 MOM5, 3 RCO (T=1 specialisations)
   bool f32 = false;          // fp32 fields (FCX_PRECISION_F32): 4 cells per lane
   bool ravg = false;         // register averages in this plan (Params::ravg_on)
-  bool pair = false;         // T = 2: cells_pair_kernel (a surface type per half-wave)
   int64_t lo = 0, hi = -1;   // cell range of this launch (lo a multiple of kChunkAlign;
                              // hi < 0: to n_max) -- the pipelined host-bound step
 };
@@ -145,7 +144,6 @@ int launch_atmos(const AtmosArgs &a, void *stream);
 // atmos_fixup_kernel after the launch (launches with a grid-stride cap).
 constexpr int kFusedFields = 6;
 constexpr int kTile = 128;  // cells per wave iteration (64 lanes x 2)
-constexpr int kPairTileCells = 64;  // cells_pair_kernel (T = 2): 32 lanes x 2 per surface type
 struct AtmosFused {
   const int32_t *idx;  // local atmosphere cell of every exchange cell (non-decreasing)
   const double *w;

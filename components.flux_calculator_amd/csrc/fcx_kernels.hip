@@ -257,17 +257,19 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
   const double *h_ts = nullptr, *h_fi = nullptr, *h_ps = nullptr, *h_pa = nullptr, *h_qa = nullptr,
                *h_ta = nullptr, *h_u = nullptr, *h_v = nullptr, *h_amoi = nullptr, *h_cmoi = nullptr,
                *h_chea = nullptr, *h_amom = nullptr, *h_cmom = nullptr;
-  // With T from the parameter block (TM = 0) the inputs are reloaded for every type instead
-  // of held: holding kept 14 two-cell vectors (~56 VGPRs) live across the type loop and the
-  // kernels at 3 waves per SIMD; the shared atmosphere fields come back from L2 / the
-  // Infinity Cache.  FCX_HOLD_ACROSS_TYPES=1 restores the holding (A/B builds).
+  // With T from the parameter block (TM = 0) the bottom-side inputs (TSUR FICE CMOI CHEA
+  // CMOM) are reloaded for every type, and the atmosphere-side inputs (PSUR PATM QATM TATM
+  // UATM VATM AMOI AMOM, aliased into every surface type by distribute_input_field,
+  // basic:334-358) are held across the types and reloaded only when a type binds another
+  // array (FCX_HOLD_SHARED).  Measured at T = 2 (profiles/r02/t2_reload_ab): the per-type
+  // reloads of the shared fields cost 8 % of the step (a build that skips them, wrong results,
+  // is the floor); holding them costs 36 VGPRs, so the multi-type fused kernels run 3 instead
+  // of 4 waves per SIMD and still gain 6-7 % per step (RCO stays at 4 waves).  Holding every
+  // input (FCX_HOLD_ACROSS_TYPES=1, round 1) kept ~56 VGPRs live and lost; reloading the shared
+  // fields with temporal loads (FCX_TEMPORAL_SHARED=1) hits L2 but is slower still.
 #ifndef FCX_HOLD_ACROSS_TYPES
 #define FCX_HOLD_ACROSS_TYPES 0
 #endif
-// FCX_TEMPORAL_SHARED=1: load an input the next type binds too with a temporal load, so the
-// reload hits L2.  Measured (T=2/T=6 benches, 3 interleaved runs each): L2-miss reads fall to
-// the algorithmic bytes (CCLM T=2 186 -> 132 B/cell), but the step is 1.7 % / 0.6 % slower --
-// the non-temporal reloads were already served by the Infinity Cache.  Off by default.
 #ifndef FCX_TEMPORAL_SHARED
 #define FCX_TEMPORAL_SHARED 0
 #endif
@@ -278,12 +280,8 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
 #ifndef FCX_DBG_SKIP_SHARED
 #define FCX_DBG_SKIP_SHARED 0
 #endif
-// FCX_HOLD_SHARED=1: with TM = 0, the atmosphere-side inputs (PSUR PATM QATM TATM UATM VATM
-// AMOI AMOM, aliased into every surface type by distribute_input_field, basic:334-358) are
-// held across the types and reloaded only when a type binds another array; the bottom-side
-// inputs are reloaded per type as before.
 #ifndef FCX_HOLD_SHARED
-#define FCX_HOLD_SHARED 0
+#define FCX_HOLD_SHARED 1
 #endif
   // grp.member names the pointer in TypeParams (the next type's is compared when
   // FCX_TEMPORAL_SHARED is on).  ATM: an atmosphere-side input (FCX_HOLD_SHARED).
@@ -308,7 +306,7 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
   constexpr bool kHoldAtm = !kReload || (TM == 0 && FCX_HOLD_SHARED);
 
   for (int s = 0; s < T; ++s) {
-    if constexpr (kReload) {  // nothing of the previous type stays live
+    if constexpr (kReload) {  // no bottom-side input of the previous type stays live
       ts = fi = cmoi = chea = cmom = Vec<C, R>{};
       if constexpr (!kHoldAtm) ps = pa = qa = ta = u = v = amoi = amom = vel = Vec<C, R>{};
     }
@@ -669,9 +667,10 @@ __device__ __forceinline__ void take_carry(const AtmosFused &af, int64_t tile, d
                        : 0.0;
 }
 
-// blocks per CU the multi-type (RAVG) fused kernel is compiled for: 4 -> <= 128 VGPRs
+// blocks per CU the multi-type (RAVG) fused kernel is compiled for: 3 -> <= 168 VGPRs, room
+// for the held atmosphere-side inputs (4 -> <= 128 spilled them)
 #ifndef FCX_RAVG_ATMOS_BLOCKS
-#define FCX_RAVG_ATMOS_BLOCKS 4
+#define FCX_RAVG_ATMOS_BLOCKS 3
 #endif
 // blocks per CU the T=1 fused kernels are compiled for (1: no register cap)
 #ifndef FCX_T1_ATMOS_BLOCKS
@@ -801,296 +800,6 @@ __global__ __launch_bounds__(64 * atmos_waves<C>(), RAVG ? FCX_RAVG_ATMOS_BLOCKS
       segment_done<R>(af, tile, a[0], acc, end == kT && next_a == a[0]);
     }
     wave_sync();  // every lane is done reading before the next tile overwrites the region
-  }
-}
-
-// ---------------------------------------------------------------------------------------
-// T = 2 (water + ice, the IOW Baltic set-up) with the type-0 averages: the two surface types
-// side by side in the two half-waves.  Lane l works cells 2q, 2q+1 (q = l & 31) of a 64-cell
-// wave tile for surface type 1 + (l >> 5), so one instruction stream computes both types of
-// the same cells at once:
-//  * the atmosphere-side inputs, aliased into both types (distribute_input_field,
-//    basic:334-358), are read by both halves at the same addresses in the same instruction,
-//    so every byte is fetched once -- no per-type reload and nothing held across types;
-//  * the type-0 average of a flux is formed the moment both types have produced it: the
-//    lower half's X_1 * FARE_1 crosses to the upper half with v_permlane32_swap, and the
-//    upper lane adds (0.0 + X_1*FARE_1) + X_2*FARE_2 -- the type-order sum of calc:376-383,
-//    bit-identical to the accumulator of the sequential-types kernel, without LDS
-//    accumulators or a second pass;
-//  * the upper half stores the averages and parks w * average in the wave's LDS rows for the
-//    fused exchange -> atmosphere accumulation, which then runs one cell per lane over the
-//    64-cell tile (same segment sums, hand-off and link order as cells_atmos_kernel).
-// Used for the standard variants (VAR 1..3: QSUR/MEVA/HSEN/momentum methods compiled in; the
-// HLAT water/ice and RBBR methods per lane) when every average is a register slot.
-
-// the value of lane l - 32 on the upper lanes (lanes 0-31 keep their own)
-__device__ __forceinline__ double from_lower_half(double x) {
-  const int lo = __double2loint(x), hi = __double2hiint(x);
-  const auto a = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
-  const auto b = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
-  return __hiloint2double(b[0], a[0]);
-}
-
-constexpr int kPairTile = kPairTileCells;  // cells per wave tile (32 lanes x 2 cells)
-constexpr int kPairRow = kPairTile + 2 * (kPairTile / 16);  // lds_slot-padded row of products
-
-// Where a flux of the lane's type goes besides its own array: every call is made by both
-// half-waves together (the permlane needs both), under wave-uniform conditions only.
-struct PairSink {
-  const AvgRegs &ra;
-  double *rows;     // wave LDS [kFusedFields][kPairRow]: w * average (nullptr: not fused)
-  const double *const *atm_out;  // AtmosFused::out (which fields the accumulation takes)
-  Vec<2, double> fare;  // FARE of the lane's type at its two cells
-  double w[2];          // exchange -> atmosphere weights of the two cells
-  bool upper;
-  int s;                // lds_slot(2q)
-  int64_t j0, nt, D_;
-  template <bool NT>
-  __device__ __forceinline__ void put(int k, const Vec<2, double> &x) {
-    if (!ra.out[k]) return;  // wave-uniform
-    Vec<2, double> avg;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const double p = x.v[i] * fare.v[i];
-      avg.v[i] = (0.0 + from_lower_half(p)) + p;
-    }
-    if (upper) {
-      constexpr int C = 2;
-      using R = double;
-      ST(ra.out[k], j0, nt, avg);
-      if (rows && k < kFusedFields && atm_out[k])
-        *reinterpret_cast<d2 *>(rows + k * kPairRow + s) = d2{w[0] * avg.v[0], w[1] * avg.v[1]};
-    }
-  }
-};
-
-// The lane's value of a per-type parameter.  Both types' values are pinned to scalar
-// registers first: left alone, the compiler turns `h ? t1.x : t0.x` into a per-lane load
-// from the parameter block, a dependent vector-memory round trip in front of every field
-// access.
-template <class T>
-__device__ __forceinline__ T uniform(T x) {
-  if constexpr (sizeof(T) == 8) {
-    const uint64_t u = (uint64_t)x;
-    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)u), hi = __builtin_amdgcn_readfirstlane((uint32_t)(u >> 32));
-    return (T)(((uint64_t)hi << 32) | lo);
-  } else {
-    return (T)__builtin_amdgcn_readfirstlane((int)x);
-  }
-}
-template <class T>
-__device__ __forceinline__ T psel(bool h, T a, T b) {
-  return h ? uniform(b) : uniform(a);
-}
-
-// One surface type per half-wave; the stores of a type's outputs are per lane, the sink calls
-// wave-wide.  Mirrors process<2, true, VAR, NT, double, 1> (the single-type code) stage by
-// stage; the planner guarantees every sinked value is produced by both types (ravg_slot).
-template <int VAR, bool NT>
-__device__ __forceinline__ void process_pair(const Params *__restrict__ P, const double *__restrict__ corr_m,
-                                             int64_t j0, bool h, PairSink &sink) {
-  constexpr int C = 2;
-  using R = double;
-  static_assert(VAR >= 1 && VAR <= 3, "standard variants only");
-  const uint32_t stages = P->stages;
-  const int64_t nt = P->n[0];
-  const int64_t D_ = (j0 >> kLayoutShift) * P->tpad;
-  const TypeParams &t0 = P->type[0], &t1 = P->type[1];
-#define PSEL(m) psel(h, t0.m, t1.m)
-#define PLD(var, m)                       \
-  {                                       \
-    const double *p_ = PSEL(m);           \
-    if (p_) var = LD(p_, j0, nt);         \
-  }
-  Vec<C, R> corr = {}, rsdd = {};
-  if (corr_m && (stages & S_MEVA)) corr = ld<C, NT, R>(reinterpret_cast<const R *>(corr_m), j0, nt);
-  if (P->rsdd0 && (stages & S_RSDR)) rsdd = LD(P->rsdd0, j0, nt);
-  Vec<C, R> ts = {}, fi = {}, ps = {}, pa = {}, qa = {}, ta = {}, u = {}, v = {}, amoi = {}, cmoi = {}, chea = {},
-            amom = {}, cmom = {}, qs = {}, me = {}, vel = {};
-  PLD(ts, t.tsur)
-  PLD(fi, t.fice)
-  PLD(ps, t.psur)
-  PLD(pa, t.patm)
-  PLD(qa, t.qatm)
-  PLD(ta, t.tatm)
-  PLD(u, t.uatm)
-  PLD(v, t.vatm)
-  PLD(amoi, t.amoi)
-  PLD(cmoi, t.cmoi)
-  PLD(chea, t.chea)
-  PLD(qs, t.qsur_in)
-  PLD(me, t.meva_in)
-  PLD(amom, uv[0].amom)
-  PLD(cmom, uv[0].cmom)
-  if (PSEL(t.uatm) || PSEL(t.vatm)) FOR_C vel.v[i] = wind(u.v[i], v.v[i]);
-  if (P->ravg_on) {
-    const double *f = psel(h, P->ravg.fare[0], P->ravg.fare[1]);
-    sink.fare = LD(f, j0, nt);
-  }
-  sink.put<NT>(A_TSUR, ts);
-
-  constexpr int8_t kM = VAR == 1 ? FCX_CCLM : VAR == 2 ? FCX_MOM5 : FCX_RCO;
-  constexpr bool kQ = VAR != 3;  // QSUR method CCLM (VAR 1, 2) or none (RCO)
-  // ---- calc_flux_radiation_blackbody (calc:331-343)
-  if (stages & S_RBBR) {
-    const int8_t m = PSEL(m_rbbr);
-    double *o = PSEL(t.rbbr);
-    Vec<C, R> r;
-    FOR_C r.v[i] = m == FCX_STBO ? rbbr_stbo(ts.v[i]) : R(0);
-    if (o && (m == FCX_STBO || m == FCX_ZERO)) ST(o, j0, nt, r);
-    sink.put<NT>(A_RBBR, r);
-  }
-  // ---- calc_spec_vapor_surface(t) (calc:37-49)
-  if (kQ && (stages & S_QSUR_T)) {
-    FOR_C qs.v[i] = qsur_cclm(fi.v[i], ps.v[i], ts.v[i]);
-    if (double *o = PSEL(t.qsur)) ST(o, j0, nt, qs);
-  }
-  // ---- calc_flux_mass_evap (calc:75-118), P2: TATM in the T_s slot
-  if (stages & S_MEVA) {
-    if constexpr (kM == FCX_RCO) {
-      FOR_C me.v[i] = meva_rco(qa.v[i], ts.v[i], vel.v[i]);
-    } else {
-      const Vec<C, R> &a = kM == FCX_CCLM ? amoi : cmoi;
-      FOR_C me.v[i] = meva_cclm(a.v[i], ps.v[i], qa.v[i], qs.v[i], ta.v[i], vel.v[i]);
-    }
-    const int8_t adds = PSEL(bias_adds);
-    for (int b = 0; b < adds; ++b) FOR_C me.v[i] = me.v[i] + corr.v[i];
-    if (double *o = PSEL(t.meva)) ST(o, j0, nt, me);
-    sink.put<NT>(A_MEVA, me);
-  }
-  // ---- calc_flux_heat_latent (calc:135-152)
-  if (stages & S_HLAT) {
-    const int8_t m = PSEL(m_hlat);
-    double *o = PSEL(t.hlat);
-    const R f = m == FCX_WATER ? R(kLv) : R(kLs);
-    Vec<C, R> hl;
-    FOR_C hl.v[i] = m == FCX_ZERO ? R(0) : me.v[i] * f;
-    if (o && (m == FCX_WATER || m == FCX_ICE || m == FCX_ZERO)) ST(o, j0, nt, hl);
-    sink.put<NT>(A_HLAT, hl);
-  }
-  // ---- calc_flux_heat_sensible (calc:167-206), P3: QATM in the q_s slot
-  if (stages & S_HSEN) {
-    Vec<C, R> hs;
-    if constexpr (kM == FCX_RCO) {
-      FOR_C hs.v[i] = hsen_rco(ta.v[i], ts.v[i], vel.v[i]);
-    } else {
-      const Vec<C, R> &a = kM == FCX_CCLM ? amoi : chea;
-      FOR_C hs.v[i] = hsen_cclm(a.v[i], pa.v[i], ps.v[i], qa.v[i], ta.v[i], ts.v[i], vel.v[i]);
-    }
-    if (double *o = PSEL(t.hsen)) ST(o, j0, nt, hs);
-    sink.put<NT>(A_HSEN, hs);
-  }
-  // u and v grids ARE the t grid: QSUR(u/v) = QSUR(t), one exchange rate for both momenta
-  if constexpr (kQ) {
-    for (int k = 0; k < 2; ++k) {
-      const uint32_t s_qsur = k == 0 ? S_QSUR_U : S_QSUR_V;
-      if (!(stages & s_qsur)) continue;
-      if (double *o = PSEL(uv[k].qsur)) {
-        if (!(stages & S_QSUR_T)) FOR_C qs.v[i] = qsur_cclm(fi.v[i], ps.v[i], ts.v[i]);
-        ST(o, j0, nt, qs);
-      }
-    }
-  }
-  const bool do_u = stages & S_UMOM, do_v = stages & S_VMOM;
-  if (do_u || do_v) {
-    Vec<C, R> rate;
-    if constexpr (kM == FCX_RCO) {
-      FOR_C rate.v[i] = mom_rco_rate(vel.v[i]);
-    } else {
-      const Vec<C, R> &a = kM == FCX_MOM5 ? cmom : amom;
-      FOR_C rate.v[i] = mom_cclm_rate(a.v[i], ps.v[i], qs.v[i], ts.v[i], vel.v[i]);
-    }
-    if (do_u) {  // calc_flux_momentum_east (u grid)
-      Vec<C, R> o;
-      FOR_C o.v[i] = -(rate.v[i] * u.v[i]);
-      if (double *q = PSEL(uv[0].mom)) ST(q, j0, nt, o);
-      sink.put<NT>(A_UMOM, o);
-    }
-    if (do_v) {  // calc_flux_momentum_north (v grid)
-      Vec<C, R> o;
-      FOR_C o.v[i] = -(rate.v[i] * v.v[i]);
-      if (double *q = PSEL(uv[1].mom)) ST(q, j0, nt, o);
-      sink.put<NT>(A_VMOM, o);
-    }
-  }
-  // ---- distribute_shortwave_radiation_flux (calc:355-362): RSDR_s = RSDD_0
-  if (stages & S_RSDR)
-    if (double *o = PSEL(t.rsdr)) ST(o, j0, nt, rsdd);
-#undef PLD
-#undef PSEL
-}
-
-#ifndef FCX_PAIR_BLOCKS  // blocks per CU the pair kernel is compiled for
-#define FCX_PAIR_BLOCKS 3
-#endif
-// FUSED: with the exchange -> atmosphere accumulation (af); otherwise af is unused.
-template <int VAR, bool NT, bool FUSED>
-__global__ __launch_bounds__(256, FCX_PAIR_BLOCKS) void cells_pair_kernel(const Params *__restrict__ P,
-                                                                          const double *__restrict__ corr_m,
-                                                                          const AtmosFused af, int64_t lo,
-                                                                          int64_t hi) {
-  constexpr int kT = kPairTile;
-  __shared__ double s_p[FUSED ? 4 : 1][FUSED ? kFusedFields * kPairRow : 1];
-  const int64_t n = P->n_max;
-  const int64_t n_tiles = (hi + kT - 1) / kT;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int q = lane & 31;
-  const bool h = lane >= 32;
-  double *wp = s_p[FUSED ? wv : 0];
-  const int64_t waves = (int64_t)gridDim.x * (blockDim.x >> 6);
-  const int64_t wave0 = (int64_t)xcd_block(blockIdx.x, gridDim.x) * (blockDim.x >> 6) + wv;
-  for (int64_t tile = lo / kT + wave0; tile < n_tiles; tile += waves) {
-    const int64_t t0 = tile * kT;
-    const int64_t j0 = t0 + 2 * q;
-    PairSink sink{P->ravg, FUSED ? wp : nullptr, af.out, {}, {0.0, 0.0}, h, lds_slot(2 * q), j0, P->n[0], 0};
-    sink.D_ = (j0 >> kLayoutShift) * P->tpad;
-    if constexpr (FUSED) {
-      if (j0 + 2 <= n) {
-        const d2 ww = __builtin_nontemporal_load(reinterpret_cast<const d2 *>(af.w + j0));
-        sink.w[0] = ww[0];
-        sink.w[1] = ww[1];
-      } else if (j0 < n) {
-        sink.w[0] = af.w[j0];
-      }
-    }
-    if (j0 < n) process_pair<VAR, NT>(P, corr_m, j0, h, sink);
-    if constexpr (FUSED) {
-      if (j0 >= n && h) {  // dead cells: zero products (their segment sums are never stored)
-        *reinterpret_cast<d2 *>(wp + lds_slot(2 * q)) = d2{0.0, 0.0};
-      }
-      // the segment sums, one cell per lane over the 64-cell tile (cells_atmos_kernel, C = 1)
-      const int64_t jc = t0 + lane;
-      const int32_t a = jc < n ? af.idx[jc] : -1;  // -1: past the grid end
-      const int32_t prev_tile = t0 > 0 ? af.idx[t0 - 1] : -2;
-      const int32_t next_a = (t0 + kT < n) ? af.idx[t0 + kT] : -3;
-      int32_t prev = __shfl_up(a, 1);
-      if (lane == 0) prev = prev_tile;
-      const bool st = a != prev;
-      const uint64_t m = __ballot(st);
-      const uint64_t above = lane == 63 ? 0ull : (~0ull << (lane + 1));
-      auto add_cell = [&](double *acc, int e) {
-        const double *r = wp + lds_slot(e);
-#pragma unroll
-        for (int k = 0; k < kFusedFields; ++k) acc[k] = acc[k] + r[k * kPairRow];
-      };
-      wave_sync();  // the upper half's products are visible to every lane
-      if (st && a >= 0) {
-        const int end = min(first_bit(m & above), kT);
-        double acc[kFusedFields];
-#pragma unroll
-        for (int k = 0; k < kFusedFields; ++k) acc[k] = 0.0;
-        for (int e = lane; e < end; ++e) add_cell(acc, e);
-        segment_done<double>(af, tile, a, acc, end == kT && next_a == a);
-      }
-      if (af.handoff && lane == 0 && a >= 0 && a == prev_tile) {
-        const int end = min(first_bit(m), kT);
-        double acc[kFusedFields];
-        take_carry(af, tile - 1, acc);
-        for (int e = 0; e < end; ++e) add_cell(acc, e);
-        segment_done<double>(af, tile, a, acc, end == kT && next_a == a);
-      }
-      wave_sync();  // every lane is done reading before the next tile overwrites the rows
-    }
   }
 }
 
@@ -1313,40 +1022,6 @@ static void launch_atm(bool nt, int blocks, hipStream_t s, const Params *dp, con
                        s, dp, corr_m, af, lo, hi);
 }
 
-// T = 2, one type per half-wave (cells_pair_kernel): 64-cell wave tiles, four waves per
-// block, one trip; af == nullptr: no fused accumulation
-template <int VAR>
-static void launch_pair_v(bool nt, hipStream_t s, const Params *dp, const double *corr_m, const AtmosFused *af,
-                          int64_t lo, int64_t hi) {
-  const int64_t tiles = (hi - lo + kPairTile - 1) / kPairTile;
-  const int blocks = (int)std::max<int64_t>(1, (tiles + 3) / 4);
-  const AtmosFused none{};
-  const AtmosFused &a = af ? *af : none;
-  if (af) {
-    if (nt)
-      hipLaunchKernelGGL((cells_pair_kernel<VAR, true, true>), dim3(blocks), dim3(256), 0, s, dp, corr_m, a, lo, hi);
-    else
-      hipLaunchKernelGGL((cells_pair_kernel<VAR, false, true>), dim3(blocks), dim3(256), 0, s, dp, corr_m, a, lo, hi);
-  } else {
-    if (nt)
-      hipLaunchKernelGGL((cells_pair_kernel<VAR, true, false>), dim3(blocks), dim3(256), 0, s, dp, corr_m, a, lo, hi);
-    else
-      hipLaunchKernelGGL((cells_pair_kernel<VAR, false, false>), dim3(blocks), dim3(256), 0, s, dp, corr_m, a, lo,
-                         hi);
-  }
-}
-
-static int launch_pair(const LaunchConfig &lc, hipStream_t s, const Params *dp, const double *corr_m,
-                       const AtmosFused *af, int64_t lo, int64_t hi) {
-  switch (lc.variant) {
-    case 1: launch_pair_v<1>(lc.nontemporal, s, dp, corr_m, af, lo, hi); break;
-    case 2: launch_pair_v<2>(lc.nontemporal, s, dp, corr_m, af, lo, hi); break;
-    case 3: launch_pair_v<3>(lc.nontemporal, s, dp, corr_m, af, lo, hi); break;
-    default: return (int)hipErrorInvalidValue;
-  }
-  return (int)hipGetLastError();
-}
-
 // fused accumulation: one surface type (its fluxes), or several with the type-0 averages in
 // registers (what OASIS sends); several types without register averages are not fused
 template <int VAR>
@@ -1371,10 +1046,6 @@ int launch_cells(const Params *hp, const Params *dp, const double *corr_m, const
   const int64_t lo = lc.lo, hi = lc.hi < 0 ? hp->n_max : std::min<int64_t>(lc.hi, hp->n_max);
   if (lo % kChunkAlign || lo < 0) return (int)hipErrorInvalidValue;
   if (hi <= lo) return 0;
-  // T = 2, both types side by side in the half-waves (the engine's plan decides, lc.pair)
-  if (lc.pair && hp->num_types == 2 && lc.merged && lc.variant && !lc.f32 && lc.cells_per_thread == 2 &&
-      (!atm || atm->handoff))
-    return launch_pair(lc, s, dp, corr_m, atm, lo, hi);
   if (atm) {  // fused accumulation: T=1 specialised merged kernel, 2 cells per lane
     // four waves per block (fp32: two), one 128-cell (fp32: 256-cell) tile per wave and trip.  Default: one trip (full
     // grid) -- +2 % per T=1 step over the 8192-block cap, equal at T=2 (profiles/r01/grid_ab)

@@ -247,7 +247,12 @@ enum fcx_option {
   FCX_OPT_NONTEMPORAL = 3,      /* non-temporal hint on streamed loads/stores (default 1) */
   FCX_OPT_SPECIALIZE = 4,       /* T=1 CCLM/MOM5/RCO specialised kernels (default 1)      */
   FCX_OPT_ATMOS_IN_RUN = 5,     /* fcx_run also runs the atmosphere accumulation (def. 1) */
-  FCX_OPT_PIN_HOST = 6,         /* page-lock the bound host arrays at fcx_commit (def. 1)  */
+  FCX_OPT_PIN_HOST = 6,         /* hipHostRegister the caller's heap arrays at fcx_commit,
+                                   so their copies run as direct DMA (default 0: on ROCm
+                                   7.x, DMA and kernel access through registered heap ranges
+                                   faulted or read a neighbouring page in long test runs;
+                                   arrays from fcx_host_malloc are page-locked by the
+                                   library and need no registration)                      */
   FCX_OPT_PIPELINE_CHUNKS = 7,  /* fcx_step of host-bound fields: H2D/compute/D2H overlap
                                    over this many cell chunks (default 8; 1 = sequential) */
   FCX_OPT_PIPELINE_MIN_CHUNK = 8, /* ... of at least this many cells (multiple of 1024;
@@ -263,10 +268,6 @@ enum fcx_option {
                                    carry hand-off as timed out, so that the recovery of
                                    fcx_synchronize (atmos_kernel recomputes the atmosphere
                                    outputs) runs; the results must be unchanged            */
-  FCX_OPT_TYPE_PAIR = 13,       /* two surface types (water + ice): both computed side by
-                                   side, one per half-wave, so the atmosphere inputs they
-                                   share are read once and the type-0 averages formed in
-                                   registers (default 0: measured slower than the sequential types)  */
   FCX_OPT_TILED_LAYOUT = 11     /* engine-owned mirrors tile-blocked (default 1): tiles of
                                    4096 cells, the read-only arrays' tiles interleaved in
                                    one pool and the written arrays' in another, so a wave's
