@@ -45,6 +45,24 @@ def read_counter(d, name):
     return per
 
 
+def read_request_bytes(d):
+    """Read bytes per launch from the request-size counters (bench/pmc_bytes.sh):
+    32 x RDREQ_32B + 64 x RDREQ_64B + 128 x RDREQ_128B, exact on gfx950 (no calibration)."""
+    disp = defaultdict(lambda: defaultdict(float))
+    names = {}
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            disp[(f, r["Dispatch_Id"])][r["Counter_Name"]] += float(r["Counter_Value"])
+            names[(f, r["Dispatch_Id"])] = r["Kernel_Name"]
+    per = defaultdict(list)
+    for key, c in disp.items():
+        k = kernel_key(names[key])
+        if k is not None and "TCC_EA0_RDREQ_128B_sum" in c:
+            per[k].append(32 * c["TCC_EA0_RDREQ_32B_sum"] + 64 * c["TCC_EA0_RDREQ_64B_sum"]
+                          + 128 * c["TCC_EA0_RDREQ_128B_sum"])
+    return per
+
+
 def traffic_key(variant, cells, types, bias, atmos, dtype):
     """profiles/traffic.json key (bench.py looks the dominant kernel up by it)."""
     return f"{variant}:{cells}:T{types}:bias{int(bias)}:atmos{int(atmos)}:{dtype}"
@@ -61,20 +79,29 @@ def main():
     ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.dirname(
         os.path.dirname(os.path.abspath(__file__)))), "profiles", "traffic.json"))
     a = ap.parse_args()
-    fetch = read_counter(os.path.join(a.dir, "fetch"), "FETCH_SIZE")
+    rdreq = os.path.isdir(os.path.join(a.dir, "rdreq"))  # bench/pmc_bytes.sh layout
+    if rdreq:
+        fetch = read_request_bytes(os.path.join(a.dir, "rdreq"))
+    else:
+        fetch = read_counter(os.path.join(a.dir, "fetch"), "FETCH_SIZE")
     write = read_counter(os.path.join(a.dir, "write"), "WRITE_SIZE")
     out = json.load(open(a.out)) if os.path.exists(a.out) else {}
     for k in sorted(set(fetch) & set(write)):
         v, atm, dt = k
-        # KiB -> B, gfx950 x2 read correction (calibrated for 16 B/lane streaming reads; the
-        # fused kernel's 8 B/lane atmosphere-index reads are 4 of its ~150 B/cell)
-        f = sum(fetch[k]) / len(fetch[k]) * 1024 * 2
+        if rdreq:
+            f = sum(fetch[k]) / len(fetch[k])
+            how = ("rocprofv3 --pmc TCC_EA0_RDREQ_{32B,64B,128B}_sum and --pmc WRITE_SIZE passes "
+                   "(separate runs), read bytes = 32/64/128 x requests of each size + WRITE_SIZE")
+        else:
+            # KiB -> B, gfx950 x2 read correction (calibrated for 16 B/lane streaming reads; the
+            # fused kernel's 8 B/lane atmosphere-index reads are 4 of its ~150 B/cell)
+            f = sum(fetch[k]) / len(fetch[k]) * 1024 * 2
+            how = ("rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE passes (separate runs), "
+                   "FETCH_SIZE x2 (gfx950) + WRITE_SIZE")
         w = sum(write[k]) / len(write[k]) * 1024
         key = traffic_key(v, a.cells, a.types, a.bias, atm, dt)
         out[key] = round(f + w)
-        out.setdefault("_sources", {})[key] = (
-            f"{a.source or a.dir}: rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE passes (separate runs), "
-            f"mean over {len(fetch[k])} launches, FETCH_SIZE x2 (gfx950) + WRITE_SIZE")
+        out.setdefault("_sources", {})[key] = f"{a.source or a.dir}: {how}, mean over {len(fetch[k])} launches"
         print(key, "read", round(f / a.cells, 2), "B/cell", "write", round(w / a.cells, 2), "B/cell",
               "launches", len(fetch[k]))
     json.dump(out, open(a.out, "w"), indent=1, sort_keys=True)

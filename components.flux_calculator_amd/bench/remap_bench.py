@@ -37,6 +37,10 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--map", choices=("synthetic", "geometric"), default="synthetic")
     ap.add_argument("--side", type=int, default=1300, help="geometric: atmosphere cells per side")
+    ap.add_argument("--pack", default="0,2",
+                    help="FCX_OPT_REMAP_PACK values to compare (0: gather from the field arrays, "
+                         "2: packed records)")
+    ap.add_argument("--links", default="1,2", help="links per exchange cell (synthetic map)")
     a = ap.parse_args()
     import torch
 
@@ -55,15 +59,20 @@ def main():
     case = build_case("CCLM", n=n, T=1, device=dev, data=data)
     engines = {"none": Engine(case.lf, 1, case.methods, device=0, stream=stream.cuda_stream)}
     alg = {}
-    for links in ((1,) if geo is not None else (1, 2)):
+    packs = [int(x) for x in a.pack.split(",")]
+    for links in ((1,) if geo is not None else tuple(int(x) for x in a.links.split(","))):
         mm = geo if geo is not None else synthetic_model_map(n, m, links_per_cell=links)
-        outs = {k: torch.empty(m, dtype=torch.float64, device=dev) for k, _ in FIELDS}
-        rm = {"n_dst": m, "src": mm.src, "dst": mm.dst, "w": mm.weight,
-              "fields": [(2, 1, g, k, outs[k]) for k, g in FIELDS]}
-        engines[f"{links} link(s)/cell"] = Engine(case.lf, 1, case.methods, device=0,
-                                                  stream=stream.cuda_stream, remaps=[rm])
         nl, nf = mm.src.size, len(FIELDS)
-        alg[f"{links} link(s)/cell"] = {"links": int(nl), "bytes": int(nl * (4 + 8 + 8 * nf) + m * (4 + 8 * nf))}
+        for pack in packs:
+            outs = {k: torch.empty(m, dtype=torch.float64, device=dev) for k, _ in FIELDS}
+            rm = {"n_dst": m, "src": mm.src, "dst": mm.dst, "w": mm.weight,
+                  "fields": [(2, 1, g, k, outs[k]) for k, g in FIELDS]}
+            key = f"{links} link(s)/cell pack={pack}"
+            engines[key] = Engine(case.lf, 1, case.methods, device=0, stream=stream.cuda_stream, remaps=[rm],
+                                  options={"remap_pack": pack})
+            sc, packed = engines[key].remap_info(0)
+            alg[key] = {"links": int(nl), "bytes": int(nl * (4 + 8 + 8 * nf) + m * (4 + 8 * nf)),
+                        "scatter": round(sc, 3), "packed": packed}
     times = {k: [] for k in engines}
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     for r in range(a.rounds):

@@ -164,8 +164,15 @@ struct fcx_engine {
     double *d_w = nullptr;
     std::vector<RemapField> fields;
     void *pool = nullptr;
+    // gather scatter of the map: distinct 64-B segments of a field array (8 fp64 cells) the
+    // links of a 256-destination block touch, per link (sampled at commit).  About 0.3 on
+    // the geometric and the 1-link synthetic maps, 0.66 on the shuffled 2-link map.
+    double scatter = 0.0;
   };
   std::vector<Remap> remaps;
+  int remap_pack = 2;        // FCX_OPT_REMAP_PACK: 0 never, 1 always, 2 launches of >= 2 fields
+  void *d_rec = nullptr;     // remap records scratch (pack_records), shared by every remap launch
+  size_t rec_bytes = 0;
   // host-bound steps: page-locked caller arrays and the H2D / compute / D2H pipeline
   bool pin_host = false;  // FCX_OPT_PIN_HOST: opt-in
   int chunks = 8;                                   // fcx_step pipeline depth (1 = off)
@@ -294,6 +301,7 @@ extern "C" int fcx_destroy(fcx_engine *e) {
     (void)hipFree(r.d_w);
     (void)hipFree(r.pool);
   }
+  (void)hipFree(e->d_rec);
   (void)hipFree(e->pool);
   for (void *p : e->tiled_pools) (void)hipFree(p);
   if (e->ev0) (void)hipEventDestroy(e->ev0);
@@ -1248,6 +1256,48 @@ extern "C" int fcx_set_precision(fcx_engine *e, int precision) {
   return FCX_OK;
 }
 
+// a remap launch of nf fields gathers packed records (FCX_OPT_REMAP_PACK).  Auto: two
+// fields or more, on a scattered map.  Measured (components.flux_calculator_amd/bench/
+// remap_bench.py, 10M cells, 6 fields): the shuffled 2-link map (scatter 0.66) 1.46 ms from
+// the arrays, 0.68 ms packed; the 1-link synthetic (0.32) 0.356 / 0.405 ms and the
+// geometric map (0.31) 0.20 / 0.36 ms, where neighbouring links share their lines anyway.
+constexpr double kPackScatter = 0.5;
+static bool remap_packs(const fcx_engine *e, const fcx_engine::Remap &rm, int nf) {
+  if (nf <= 0 || rm.n_links <= 0) return false;
+  return e->remap_pack == 1 || (e->remap_pack == 2 && nf >= 2 && rm.scatter > kPackScatter);
+}
+
+// elements per packed record of nf fields: a whole number of 16-B vectors (A/B builds
+// with FCX_REC_POW2: a power of two, so that no record straddles a 64-B boundary)
+static int rec_width(const fcx_engine *e, int nf) {
+  const int v = (int)(16 / e->esize);
+#if defined(FCX_REC_POW2) && FCX_REC_POW2
+  int p = v;
+  while (p < nf) p *= 2;
+  return p;
+#else
+  return (nf + v - 1) / v * v;
+#endif
+}
+
+// distinct 64-B field segments per link over a sample of 256-destination blocks
+static double remap_scatter(const fcx_engine::Remap &rm) {
+  const int64_t nb = (rm.n_dst + 255) / 256;
+  if (nb == 0 || rm.n_links == 0) return 0.0;
+  const int64_t every = std::max<int64_t>(1, nb / 256);
+  int64_t links = 0, distinct = 0;
+  std::vector<int32_t> seg;
+  for (int64_t b = 0; b < nb; b += every) {
+    const int32_t k0 = rm.row[(size_t)(b * 256)], k1 = rm.row[(size_t)std::min<int64_t>(rm.n_dst, (b + 1) * 256)];
+    seg.clear();
+    for (int32_t k = k0; k < k1; ++k) seg.push_back(rm.col[(size_t)k] >> 3);
+    std::sort(seg.begin(), seg.end());
+    distinct += std::unique(seg.begin(), seg.end()) - seg.begin();
+    links += k1 - k0;
+  }
+  return links ? (double)distinct / (double)links : 0.0;
+}
+
 extern "C" int fcx_commit(fcx_engine *e) {
   if (!e) return fail(FCX_E_ARG, "NULL engine");
   if (e->committed) return FCX_OK;
@@ -1398,7 +1448,18 @@ extern "C" int fcx_commit(fcx_engine *e) {
           off += one;
         }
     }
+    // records scratch for the packed gather: the largest launch group of any phase
+    size_t nf_max = 0;
+    for (int ph = 1; ph <= 3; ++ph) {
+      size_t c = 0;
+      for (auto &f : rm.fields) c += (f.phase & ph) ? 1 : 0;
+      nf_max = std::max(nf_max, std::min<size_t>(c, kMaxAtmosFields));
+    }
+    rm.scatter = remap_scatter(rm);
+    if (remap_packs(e, rm, (int)nf_max))
+      e->rec_bytes = std::max(e->rec_bytes, (size_t)(rm.max_src + 1) * rec_width(e, (int)nf_max) * e->esize);
   }
+  if (e->rec_bytes) HIP_TRY(hipMalloc(&e->d_rec, e->rec_bytes));
   e->committed = true;
   return FCX_OK;
 }
@@ -1609,6 +1670,15 @@ static int run_remaps(fcx_engine *e, int phase) {
     a.tpad = e->tpad;
     auto flush = [&]() -> int {
       if (!a.nf) return FCX_OK;
+      a.rec = nullptr;
+      a.rec_p = 0;
+      if (e->d_rec && remap_packs(e, rm, a.nf)) {  // fields -> one record per cell, then the gather
+        a.rec_p = rec_width(e, a.nf);
+        const int r = launch_pack_records(a, (int64_t)rm.max_src + 1, e->aligned16, !e->zc_active && e->launch.nontemporal,
+                                          e->d_rec, e->stream);
+        if (r) return fail(FCX_E_HIP, "remap pack launch: %s", hipGetErrorString((hipError_t)r));
+        a.rec = e->d_rec;
+      }
       const int r = launch_atmos(a, e->stream);
       if (r) return fail(FCX_E_HIP, "remap launch: %s", hipGetErrorString((hipError_t)r));
       a.nf = 0;
@@ -2023,6 +2093,11 @@ extern "C" int fcx_set_option(fcx_engine *e, int option, int64_t value) {
     case FCX_OPT_TEST_HANDOFF_TIMEOUT:
       e->test_handoff_timeout = value != 0;
       return FCX_OK;
+    case FCX_OPT_REMAP_PACK:
+      if (e->committed) return fail(FCX_E_STATE, "remap_pack is applied at fcx_commit");
+      if (value < 0 || value > 2) return fail(FCX_E_ARG, "remap_pack: 0 never, 1 always, 2 auto");
+      e->remap_pack = (int)value;
+      return FCX_OK;
     case FCX_OPT_TILED_LAYOUT:
       if (e->committed) return fail(FCX_E_STATE, "tiled_layout is applied at fcx_commit");
       e->tiled_opt = value != 0;
@@ -2182,6 +2257,22 @@ extern "C" int fcx_add_remap_field(fcx_engine *e, int32_t remap_id, int phase, i
     f.out_host = out;
   }
   e->remaps[(size_t)remap_id].fields.push_back(f);
+  return FCX_OK;
+}
+
+extern "C" int fcx_remap_info(const fcx_engine *e, int32_t remap_id, double *scatter, int32_t *packed) {
+  if (!e || !scatter || !packed) return fail(FCX_E_ARG, "NULL argument");
+  if (!e->committed) return fail(FCX_E_STATE, "remap info is known after fcx_commit");
+  if (remap_id < 0 || remap_id >= (int32_t)e->remaps.size()) return fail(FCX_E_ARG, "remap %d unknown", remap_id);
+  const auto &rm = e->remaps[(size_t)remap_id];
+  int nf_max = 0;
+  for (int ph = 1; ph <= 3; ++ph) {
+    int c = 0;
+    for (auto &f : rm.fields) c += (f.phase & ph) ? 1 : 0;
+    nf_max = std::max(nf_max, std::min(c, kMaxAtmosFields));
+  }
+  *scatter = rm.scatter;
+  *packed = e->d_rec && remap_packs(e, rm, nf_max) ? 1 : 0;
   return FCX_OK;
 }
 

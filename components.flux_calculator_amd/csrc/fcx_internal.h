@@ -128,12 +128,18 @@ struct AtmosArgs {
   int64_t tpad;            // layout of the x fields (engine buffers)
   int64_t out_tpad;        // layout of out: the engine's tiled atmosphere pool, or 0
   int32_t vec;             // col == nullptr and every x 16-B aligned: vector staging loads
-  int32_t pad;
+  int32_t rec_p;           // elements per record of rec (nf rounded up to a 16-B multiple)
+  const void *rec;         // remap gather: the x fields packed cell-major (pack_records),
+                           // record of exchange cell j at rec + j * rec_p; nullptr = SoA gather
   int32_t scol[kMaxAtmosFields];  // column of field f in the shared boundary slots: the
                                   // field's registration index (fcx_add_atmos_field order),
                                   // the same for every phase and for the fused kernel
 };
 int launch_atmos(const AtmosArgs &a, void *stream);
+// remap records: rec[j * P + f] = x[f][tiled(j)] for f < nf, 0 for nf <= f < P, cells
+// j < n (P a multiple of the 16-B vector length); aligned16: every x is 16-B aligned;
+// nontemporal: streaming hint on the field loads (off for host-mapped fields)
+int launch_pack_records(const AtmosArgs &a, int64_t n, bool aligned16, bool nontemporal, void *rec, void *stream);
 
 // Exchange -> atmosphere accumulation fused into the T=1 cells kernel.  The six fluxes it
 // can take from registers, in this order: MEVA HLAT HSEN RBBR UMOM VMOM (out[k] nullptr =

@@ -913,6 +913,21 @@ __global__ __launch_bounds__(256) void atmos_kernel(const AtmosArgs a) {
             if (v + i >= C0 && v + i < hi_k) lds[f * kAtmChunk + (v + i - C0)] = wv[i] * (double)xv[i];
         }
       }
+    } else if (a.rec) {  // remap gather of packed records: nf values of a link in rec_p / V 16-B loads
+      for (int32_t i = threadIdx.x; i < len; i += blockDim.x) {
+        const int32_t k = C0 + i;
+        const int32_t xi = __builtin_nontemporal_load(a.col + k);
+        const double wk = __builtin_nontemporal_load(a.w + k);
+        const VecT *r = reinterpret_cast<const VecT *>(reinterpret_cast<const R *>(a.rec) + (int64_t)xi * a.rec_p);
+#pragma unroll
+        for (int q = 0; q < kMaxAtmosFields / V; ++q) {
+          if (q * V >= a.nf) break;
+          const VecT t = r[q];
+#pragma unroll
+          for (int h = 0; h < V; ++h)
+            if (q * V + h < a.nf) lds[(q * V + h) * kAtmChunk + i] = wk * (double)t[h];
+        }
+      }
     } else {
       for (int32_t i = threadIdx.x; i < len; i += blockDim.x) {
         const int32_t k = C0 + i;
@@ -938,6 +953,52 @@ __global__ __launch_bounds__(256) void atmos_kernel(const AtmosArgs a) {
     reinterpret_cast<R *>(a.out[f])[tiled(c, a.out_tpad)] = (R)acc[f];
     if (c == 0 && a.left >= 0) a.shared[(int64_t)a.left * a.stride + a.scol[f]] = acc[f];
     if (c == a.n_atmos - 1 && a.right >= 0) a.shared[(int64_t)a.right * a.stride + a.scol[f]] = acc[f];
+  }
+}
+
+// Remap records (row f3).  A remap link gathers the nf sent fields of one scattered exchange
+// cell; from nf separate arrays that is nf scattered 8-B reads, each of which costs the
+// memory a whole 32-B sector (PMC: 4x the algorithmic read bytes on a shuffled 2-link map).
+// Packed cell-major, the nf values of a cell are one record of P = nf rounded up to 16 B,
+// read by P / V 16-B loads that share its sectors.  One block packs 256 * V cells: the
+// fields are staged in LDS with coalesced 16-B loads (the block's cells lie in one layout
+// tile), then the block's contiguous record region is written with 16-B stores.
+template <class R>
+__global__ __launch_bounds__(256) void pack_records_kernel(const AtmosArgs a, int64_t n, int32_t flags, R *rec) {
+  constexpr int V = 16 / sizeof(R);
+  constexpr int CB = 256 * V;  // cells per block (divides kLayoutTile)
+  using VecT = typename std::conditional<sizeof(R) == 8, d2, f4>::type;
+  extern __shared__ unsigned char lds_raw[];
+  R *lds = reinterpret_cast<R *>(lds_raw);  // [nf][CB]
+  const int64_t c0 = (int64_t)blockIdx.x * CB;
+  const int64_t cn = min((int64_t)CB, n - c0);
+  const int t = threadIdx.x;
+  for (int f = 0; f < a.nf; ++f) {
+    const R *x = reinterpret_cast<const R *>(a.x[f]) + tiled(c0, a.tpad);
+    const int64_t j = (int64_t)t * V;
+    if ((flags & 1) && j + V <= cn) {  // 16-B aligned fields
+      const VecT *p = reinterpret_cast<const VecT *>(x + j);
+      const VecT v = (flags & 2) ? __builtin_nontemporal_load(p) : *p;  // not for host-mapped fields
+#pragma unroll
+      for (int h = 0; h < V; ++h) lds[f * CB + j + h] = v[h];
+    } else {
+#pragma unroll
+      for (int h = 0; h < V; ++h)
+        if (j + h < cn) lds[f * CB + j + h] = x[j + h];
+    }
+  }
+  __syncthreads();
+  const int P = a.rec_p;
+  const int64_t nvec = cn * P / V;  // P is a multiple of V: a vector never spans two records
+  VecT *out = reinterpret_cast<VecT *>(rec + c0 * P);
+  for (int64_t q = t; q < nvec; q += 256) {
+    const int64_t e = q * V;
+    const int64_t cell = e / P;
+    const int f0 = (int)(e - cell * P);
+    VecT v;
+#pragma unroll
+    for (int h = 0; h < V; ++h) v[h] = f0 + h < a.nf ? lds[(f0 + h) * CB + cell] : R(0);
+    __builtin_nontemporal_store(v, out + q);  // +1 % over plain stores (profiles/r02/remap/)
   }
 }
 
@@ -1104,6 +1165,24 @@ int launch_atmos(const AtmosArgs &a, void *stream) {
     hipLaunchKernelGGL(atmos_kernel<float>, dim3(blocks), dim3(256), lds, reinterpret_cast<hipStream_t>(stream), a);
   else
     hipLaunchKernelGGL(atmos_kernel<double>, dim3(blocks), dim3(256), lds, reinterpret_cast<hipStream_t>(stream), a);
+  return (int)hipGetLastError();
+}
+
+int launch_pack_records(const AtmosArgs &a, int64_t n, bool aligned16, bool nontemporal, void *rec, void *stream) {
+  if (n <= 0 || a.nf <= 0) return 0;
+  const int V = a.f32 ? 4 : 2;
+  if (a.rec_p < a.nf || a.rec_p % V || a.nf > kMaxAtmosFields) return (int)hipErrorInvalidValue;
+  const int64_t cb = 256 * V;
+  const int blocks = (int)((n + cb - 1) / cb);
+  const size_t lds = (size_t)a.nf * cb * (a.f32 ? 4 : 8);
+  const int32_t flags = (aligned16 ? 1 : 0) | (nontemporal ? 2 : 0);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (a.f32)
+    hipLaunchKernelGGL(pack_records_kernel<float>, dim3(blocks), dim3(256), lds, s, a, n, flags,
+                       reinterpret_cast<float *>(rec));
+  else
+    hipLaunchKernelGGL(pack_records_kernel<double>, dim3(blocks), dim3(256), lds, s, a, n, flags,
+                       reinterpret_cast<double *>(rec));
   return (int)hipGetLastError();
 }
 

@@ -79,6 +79,7 @@ SIGNATURES = [
     ("fcx_host_free", _I, [_P]),
     ("fcx_add_remap", _I, [_P, _I64, _I64, _P, _P, _P, _P]),
     ("fcx_add_remap_field", _I, [_P, _I32, _I, _I, _I, _I, _P, _I]),
+    ("fcx_remap_info", _I, [_P, _I32, _c.POINTER(_c.c_double), _c.POINTER(_I32)]),
     ("fcx_set_option", _I, [_P, _I, _I64]),
     ("fcx_set_atmos_map", _I, [_P, _I64, _P, _P]),
     ("fcx_add_atmos_field", _I, [_P, _I, _I, _I, _I, _P, _I]),

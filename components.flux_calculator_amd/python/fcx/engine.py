@@ -186,7 +186,7 @@ class Engine:
     OPTIONS = {"cells_per_thread": 1, "max_blocks": 2, "nontemporal": 3, "specialize": 4,
                "atmos_in_run": 5, "pin_host": 6, "pipeline_chunks": 7,
                "pipeline_min_chunk": 8, "zero_copy": 9,
-               "timing": 10, "tiled_layout": 11, "test_handoff_timeout": 12}
+               "timing": 10, "tiled_layout": 11, "test_handoff_timeout": 12, "remap_pack": 13}
 
     def run_atmos(self, phase=PHASE_ALL):
         _lib.check(self.lib.fcx_run_atmos(self.h, phase))
@@ -194,6 +194,12 @@ class Engine:
     def atmos_finish(self):
         """After the all-reduce of the shared boundary buffer (fcx_atmos_finish)."""
         _lib.check(self.lib.fcx_atmos_finish(self.h))
+
+    def remap_info(self, remap_id=0):
+        """(scatter, packed) of a remap (fcx_remap_info)."""
+        sc, pk = ctypes.c_double(), ctypes.c_int32()
+        _lib.check(self.lib.fcx_remap_info(self.h, remap_id, ctypes.byref(sc), ctypes.byref(pk)))
+        return sc.value, bool(pk.value)
 
     def set_option(self, name, value):
         _lib.check(self.lib.fcx_set_option(self.h, self.OPTIONS[name], int(value)))

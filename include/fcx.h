@@ -237,6 +237,10 @@ int fcx_add_remap(fcx_engine *e, int64_t n_dst, int64_t n_links, const int32_t *
                   const int32_t *dst_cell, const double *weight, int32_t *remap_id);
 int fcx_add_remap_field(fcx_engine *e, int32_t remap_id, int phase, int surface_type, int grid,
                         int var, double *out, int flags);
+/* after fcx_commit: the map's gather scatter (distinct 64-B field segments per link over a
+ * sample of 256-destination blocks) and whether its launches gather packed records
+ * (FCX_OPT_REMAP_PACK; 1 = the largest launch group of the remap does) */
+int fcx_remap_info(const fcx_engine *e, int32_t remap_id, double *scatter, int32_t *packed);
 
 /* launch tuning of the fused cells kernel (defaults are the measured best on MI355X) */
 enum fcx_option {
@@ -268,6 +272,12 @@ enum fcx_option {
                                    carry hand-off as timed out, so that the recovery of
                                    fcx_synchronize (atmos_kernel recomputes the atmosphere
                                    outputs) runs; the results must be unchanged            */
+  FCX_OPT_REMAP_PACK = 13,      /* exchange -> model remaps: the fields of a launch packed
+                                   cell-major into one record per exchange cell before the
+                                   gather, so a link reads one record instead of nf
+                                   scattered values.  2 auto (default): launches of >= 2
+                                   fields; 1: always; 0: never (gather from the arrays).
+                                   Applied at fcx_commit (scratch of cells x record)      */
   FCX_OPT_TILED_LAYOUT = 11     /* engine-owned mirrors tile-blocked (default 1): tiles of
                                    4096 cells, the read-only arrays' tiles interleaved in
                                    one pool and the written arrays' in another, so a wave's

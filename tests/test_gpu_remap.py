@@ -13,7 +13,7 @@ pytestmark = pytest.mark.gpu
 from fcx.basic import PHASE_ALL  # noqa: E402
 from fcx.engine import Engine  # noqa: E402
 from fcx.parallel import apple_range, local_links, synthetic_model_map  # noqa: E402
-from fcx.synthetic import build_case  # noqa: E402
+from fcx.synthetic import as_dtype, build_case  # noqa: E402
 
 STEP_T = 3600 * 24 * 40
 FIELDS = (("MEVA", 1), ("HSEN", 1), ("UMOM", 2), ("VMOM", 3))
@@ -27,7 +27,10 @@ def remap_spec(mmap, outs, s=1, src=None, dst=None, w=None):
 
 @pytest.mark.parametrize("links", [1, 2])
 @pytest.mark.parametrize("device_out", [False, True])
-def test_remap_bit_exact(links, device_out):
+@pytest.mark.parametrize("pack", [0, 1, 2])
+def test_remap_bit_exact(links, device_out, pack):
+    """pack: FCX_OPT_REMAP_PACK -- the gather from the field arrays (0), or from the packed
+    records (1, 2 = auto with these four fields); the same bits every way."""
     torch = pytest.importorskip("torch")
     n = 30_011
     case = build_case("CCLM", n=n, T=1, bias=True)
@@ -36,7 +39,8 @@ def test_remap_bit_exact(links, device_out):
         outs = {k: torch.full((mmap.n_model,), float("nan"), dtype=torch.float64, device="cuda:0") for k, _ in FIELDS}
     else:
         outs = {k: np.full(mmap.n_model, np.nan) for k, _ in FIELDS}
-    eng = Engine(case.lf, 1, case.methods, corrections=case.corrections, remaps=[remap_spec(mmap, outs)])
+    eng = Engine(case.lf, 1, case.methods, corrections=case.corrections, remaps=[remap_spec(mmap, outs)],
+                 options={"remap_pack": pack})
     eng.step(PHASE_ALL, STEP_T)
     eng.close()
     for name, g in FIELDS:
@@ -123,3 +127,69 @@ def test_geometric_grid_accumulation_and_remap(variant):
                                                                               am.n_atmos), err_msg=name)
         np.testing.assert_array_equal(rmo[name], oracle_lib.remap_apply(mm.src, mm.dst, mm.weight, flux,
                                                                          mm.n_model), err_msg=name)
+
+
+@pytest.mark.parametrize("nf", [1, 3, 5, 16, 17])
+@pytest.mark.parametrize("precision", ["f64", "f32"])
+def test_remap_pack_record_widths(nf, precision):
+    """Packed-record gather with record widths that are not a 16-B multiple (3, 5 fields: padded
+    records), a full launch group (16) and one more (17: two launches, the second of one field),
+    fp64 and fp32 engines, a grid whose size is not a multiple of the pack block; every output
+    equals the gather from the arrays (FCX_OPT_REMAP_PACK 0) bit for bit, and the sequential
+    application of the engine's own fluxes."""
+    n = 9_973
+    case = build_case("MOM5", n=n, T=1, bias=False, seed=5)
+    mmap = synthetic_model_map(n, 700, links_per_cell=2, seed=9)
+    dt = np.float32 if precision == "f32" else np.float64
+    names = [("MEVA", 1), ("HLAT", 1), ("HSEN", 1), ("RBBR", 1), ("UMOM", 2), ("VMOM", 3)]
+    fields = [names[i % len(names)] for i in range(nf)]
+    if precision == "f32":
+        case = as_dtype(case, "float32")
+    lf = case.lf
+    res = {}
+    for pack in (0, 1):
+        outs = [np.full(mmap.n_model, np.nan, dtype=dt) for _ in fields]
+        rm = {"n_dst": mmap.n_model, "src": mmap.src, "dst": mmap.dst, "w": mmap.weight,
+              "fields": [(2, 1, g, k, outs[i]) for i, (k, g) in enumerate(fields)]}
+        eng = Engine(lf, 1, case.methods, remaps=[rm], options={"remap_pack": pack})
+        eng.step(PHASE_ALL, 0)
+        eng.close()
+        res[pack] = outs
+        for i, (k, g) in enumerate(fields):
+            flux = np.asarray(lf.field[(1, g, k)], dtype=np.float64)
+            want = oracle_lib.remap_apply(mmap.src, mmap.dst, mmap.weight, flux, mmap.n_model)
+            np.testing.assert_array_equal(outs[i], want.astype(dt), err_msg=f"{k} pack={pack}")
+    for i in range(nf):
+        np.testing.assert_array_equal(res[0][i], res[1][i])
+
+
+def test_remap_pack_auto_follows_the_map_scatter():
+    """FCX_OPT_REMAP_PACK auto: the shuffled 2-link map (about 0.66 distinct field segments per
+    link) gathers packed records, the geometric intersection map (about 0.3: a model cell's
+    links come from neighbouring cells) gathers from the arrays; a one-field remap never packs.
+    Both give the sequential application's bits."""
+    from fcx.parallel import geometric_maps
+
+    _, geo = geometric_maps(200)
+    n = geo.src.size
+    case = build_case("CCLM", n=n, T=1, bias=False, seed=3)
+    shuf = synthetic_model_map(n, n // 4, links_per_cell=2, seed=4)
+    outs = [{k: np.full(mm.n_model, np.nan) for k, _ in FIELDS} for mm in (shuf, geo)]
+    one = np.full(shuf.n_model, np.nan)
+    remaps = [remap_spec(shuf, outs[0]), remap_spec(geo, outs[1]),
+              {"n_dst": shuf.n_model, "src": shuf.src, "dst": shuf.dst, "w": shuf.weight,
+               "fields": [(2, 1, 1, "HLAT", one)]}]
+    eng = Engine(case.lf, 1, case.methods, remaps=remaps)
+    info = [eng.remap_info(i) for i in range(3)]
+    eng.step(PHASE_ALL, 0)
+    eng.close()
+    assert info[0][1] and info[0][0] > 0.5, info
+    assert not info[1][1] and info[1][0] < 0.5, info
+    assert not info[2][1], info
+    for mm, oo in zip((shuf, geo), outs):
+        for name, g in FIELDS:
+            want = oracle_lib.remap_apply(mm.src, mm.dst, mm.weight, np.asarray(case.lf.field[(1, g, name)]),
+                                          mm.n_model)
+            np.testing.assert_array_equal(oo[name], want, err_msg=name)
+    np.testing.assert_array_equal(one, oracle_lib.remap_apply(shuf.src, shuf.dst, shuf.weight,
+                                                              np.asarray(case.lf.field[(1, 1, "HLAT")]), shuf.n_model))
