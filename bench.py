@@ -68,6 +68,9 @@ def parse():
                    help="rehearsal only: every rank on GPU 0 (with --backend gloo on a 1-GPU box)")
     p.add_argument("--max-blocks", type=int, default=None,
                    help="A/B only: FCX_OPT_MAX_BLOCKS of every engine (default: the engine's)")
+    p.add_argument("--atmos-map", choices=("periodic", "random"), default="periodic",
+                   help="exchange->atmosphere map: periodic runs of 3,4,5,4 cells, or runs of 3..5 at "
+                        "random (segments cross the kernel's wave tiles, as on a real intersection grid)")
     p.add_argument("--caller-device", action="store_true",
                    help="bind the caller's device arrays (contiguous torch tensors, the inputs shared "
                         "by the variants) instead of host arrays whose engine-owned device mirrors "
@@ -288,7 +291,7 @@ def main():
     # cells of a grid of world * cells) or a fixed global grid (--global-cells, strong)
     n_global = args.global_cells if args.global_cells else args.cells * world
     wl = Workload(n_global, rank, world, variants, types=args.types, bias=args.bias, precision=args.precision,
-                  atmos=bool(args.atmos), caller_device=args.caller_device, device=gpu,
+                  atmos=bool(args.atmos), caller_device=args.caller_device, device=gpu, atmos_map=args.atmos_map,
                   stream=torch.cuda.current_stream(dev), engine_options=engine_options)
     n, la = wl.n, wl.la
     torch.cuda.synchronize()
@@ -368,7 +371,8 @@ def main():
             "parallelism": f"dp{world} (APPLE contiguous cell ranges)"
                            + (f", REHEARSAL: all ranks on GPU 0 over {args.backend}" if args.same_device else ""),
             "atmos_accumulation": (f"6 fluxes -> {la.n_atmos} atmosphere cells per GPU (1 per ~4 "
-                                   "exchange cells), one all-reduce of the shared boundary cells per step"
+                                   f"exchange cells, {args.atmos_map} runs), one all-reduce of the shared "
+                                   "boundary cells per step"
                                    + (" (libfcx RCCL communicator)" if comm is not None else
                                       " (torch.distributed, rehearsal)" if world > 1 else " (none needed at N=1)")
                                    if la is not None else "off"),

@@ -41,6 +41,9 @@ def main():
                     help="FCX_OPT_REMAP_PACK values to compare (0: gather from the field arrays, "
                          "2: packed records)")
     ap.add_argument("--links", default="1,2", help="links per exchange cell (synthetic map)")
+    ap.add_argument("--atmos", action="store_true",
+                    help="every engine also accumulates the six fluxes to the atmosphere (fused), as "
+                         "in a coupled step")
     a = ap.parse_args()
     import torch
 
@@ -57,7 +60,16 @@ def main():
     stream = torch.cuda.current_stream(dev)
     data = {k: torch.as_tensor(v).to(dev) for k, v in inputs_for_bench(n).items()}
     case = build_case("CCLM", n=n, T=1, device=dev, data=data)
-    engines = {"none": Engine(case.lf, 1, case.methods, device=0, stream=stream.cuda_stream)}
+    if a.atmos:
+        from fcx.parallel import local_atmos, synthetic_atmos_map
+        amap = synthetic_atmos_map(n)
+        la = local_atmos(amap, 0, 1)
+
+        def atmos_spec():
+            outs = {k: torch.empty(la.n_atmos, dtype=torch.float64, device=dev) for k, _ in FIELDS}
+            return {"local": la, "fields": [(2, 1, g, k, outs[k]) for k, g in FIELDS]}
+    engines = {"none": Engine(case.lf, 1, case.methods, device=0, stream=stream.cuda_stream,
+                              **({"atmos": atmos_spec()} if a.atmos else {}))}
     alg = {}
     packs = [int(x) for x in a.pack.split(",")]
     for links in ((1,) if geo is not None else tuple(int(x) for x in a.links.split(","))):
@@ -69,7 +81,8 @@ def main():
                   "fields": [(2, 1, g, k, outs[k]) for k, g in FIELDS]}
             key = f"{links} link(s)/cell pack={pack}"
             engines[key] = Engine(case.lf, 1, case.methods, device=0, stream=stream.cuda_stream, remaps=[rm],
-                                  options={"remap_pack": pack})
+                                  options={"remap_pack": pack}, **({"atmos": atmos_spec()} if a.atmos else {}))
+            engines[key].run(PHASE_ALL, 0)
             sc, packed = engines[key].remap_info(0)
             alg[key] = {"links": int(nl), "bytes": int(nl * (4 + 8 + 8 * nf) + m * (4 + 8 * nf)),
                         "scatter": round(sc, 3), "packed": packed}
@@ -88,7 +101,7 @@ def main():
             e1.synchronize()
             times[k].append(e0.elapsed_time(e1) / a.reps)
     base = float(np.median(times["none"]))
-    out = {"map": a.map, "cells": n, "model_cells": m, "fields": len(FIELDS),
+    out = {"map": a.map, "cells": n, "model_cells": m, "fields": len(FIELDS), "atmos": a.atmos,
            "step_ms_without_remap": round(base, 4)}
     for k, v in alg.items():
         ms = float(np.median(times[k])) - base

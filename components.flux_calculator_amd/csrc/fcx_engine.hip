@@ -76,6 +76,9 @@ struct Plan {
   AtmosFused af{};
   int atm_nf = 0;
   int atm_phase = 0;               // the phase whose fields the fused accumulation writes
+  // remap records written by this launch (host.rec): the launch group `rec_group` of remap
+  // `rec_remap` gathers them (plan_fused_records); -1 = none
+  int rec_remap = -1, rec_group = -1;
 };
 
 int var0(int var) { return var - 1; }
@@ -173,6 +176,7 @@ struct fcx_engine {
   int remap_pack = 2;        // FCX_OPT_REMAP_PACK: 0 never, 1 always, 2 launches of >= 2 fields
   void *d_rec = nullptr;     // remap records scratch (pack_records), shared by every remap launch
   size_t rec_bytes = 0;
+  const Plan *rec_plan = nullptr;  // the whole-phase plan the current run launched (its records)
   // host-bound steps: page-locked caller arrays and the H2D / compute / D2H pipeline
   bool pin_host = false;  // FCX_OPT_PIN_HOST: opt-in
   int chunks = 8;                                   // fcx_step pipeline depth (1 = off)
@@ -279,7 +283,10 @@ extern "C" int fcx_destroy(fcx_engine *e) {
   }
   (void)hipSetDevice(e->device);
   if (e->stream) (void)hipStreamSynchronize(e->stream);
-  for (auto &kv : e->plans) (void)hipFree(kv.second.dev);
+  for (auto &kv : e->plans) {
+    (void)hipFree(kv.second.dev);
+    (void)hipFree(kv.second.host.rec);
+  }
   for (auto &r : e->rg) {
     (void)hipFree(r.d_row);
     (void)hipFree(r.d_col);
@@ -640,6 +647,78 @@ static void plan_fused_atmos(fcx_engine *e, Plan &pl, uint32_t stages, int phase
   pl.atm_fused = true;
 }
 
+static bool remap_packs(const fcx_engine *e, const fcx_engine::Remap &rm, int nf);
+static int rec_width(const fcx_engine *e, int nf);
+
+// Remap records written by the T=1 specialised launch itself (Params::rec).  A remap launch
+// group (the fields run_remaps hands one atmos_kernel launch) that would gather packed
+// records (remap_packs), and whose fields are all fluxes of surface type 1 the launch holds
+// in registers (the six AtmosFused slots), gets its records from the flux kernel: the
+// packing pass and its re-read of the fields disappear.  One group per plan.
+static int plan_fused_records(fcx_engine *e, Plan &pl, uint32_t stages, int phase) {
+  pl.rec_remap = pl.rec_group = -1;
+  Params &P = pl.host;
+  for (int k = 0; k < 6; ++k) P.rec_pos[k] = -1;
+#ifndef FCX_FUSE_RECORDS  // A/B builds: 0 = remap records only from the packing pass
+#define FCX_FUSE_RECORDS 1
+#endif
+  if (!FCX_FUSE_RECORDS || !pl.variant || e->T != 1 || e->f32 || !e->specialize || e->any_regrid || phase <= 0 || phase >= 1000 ||
+      e->remap_pack == 0 || e->launch.cells_per_thread != 2 || !e->aligned16 || !P.merged_uv || P.n_max <= 0)
+    return FCX_OK;
+  const TypeParams &tp = P.type[0];
+  auto slot_of = [&](const fcx_engine::RemapField &f) -> int {
+    const int b = e->buf(f.s, f.g, f.var);
+    if (f.s != 1 || b < 0) return -1;
+    if (f.var == FCX_MEVA && (stages & S_MEVA) && b == e->buf(1, 1, FCX_MEVA) && is_compute(tp.m_meva)) return 0;
+    if (f.var == FCX_HLAT && (stages & S_HLAT) && b == e->buf(1, 1, FCX_HLAT) && tp.t.hlat &&
+        (tp.m_hlat == FCX_WATER || tp.m_hlat == FCX_ICE || tp.m_hlat == FCX_ZERO))
+      return 1;
+    if (f.var == FCX_HSEN && (stages & S_HSEN) && b == e->buf(1, 1, FCX_HSEN) && tp.t.hsen && is_compute(tp.m_hsen))
+      return 2;
+    if (f.var == FCX_RBBR && (stages & S_RBBR) && b == e->buf(1, 1, FCX_RBBR) && tp.t.rbbr &&
+        (tp.m_rbbr == FCX_STBO || tp.m_rbbr == FCX_ZERO))
+      return 3;
+    if (f.var == FCX_UMOM && (stages & S_UMOM) && b == e->buf(1, 2, FCX_UMOM) && tp.uv[0].mom && is_compute(tp.m_mom))
+      return 4;
+    if (f.var == FCX_VMOM && (stages & S_VMOM) && b == e->buf(1, 3, FCX_VMOM) && tp.uv[1].mom && is_compute(tp.m_mom))
+      return 5;
+    return -1;
+  };
+  for (size_t ri = 0; ri < e->remaps.size(); ++ri) {
+    const auto &rm = e->remaps[ri];
+    std::vector<const fcx_engine::RemapField *> grp;
+    int gi = 0;
+    auto try_group = [&]() -> bool {
+      const int nf = (int)grp.size();
+      if (!remap_packs(e, rm, nf) || nf > 6) return false;
+      int8_t pos[6] = {-1, -1, -1, -1, -1, -1};
+      for (int i = 0; i < nf; ++i) {
+        const int k = slot_of(*grp[(size_t)i]);
+        if (k < 0 || pos[k] >= 0) return false;
+        pos[k] = (int8_t)i;
+      }
+      const int p = rec_width(e, nf);
+      HIP_TRY(hipMalloc(&P.rec, (size_t)P.n_max * p * sizeof(double)));
+      P.rec_p = p;
+      for (int k = 0; k < 6; ++k) P.rec_pos[k] = pos[k];
+      pl.rec_remap = (int)ri;
+      pl.rec_group = gi;
+      return true;
+    };
+    for (auto &f : rm.fields) {
+      if (!(f.phase & phase)) continue;
+      grp.push_back(&f);
+      if ((int)grp.size() == kMaxAtmosFields) {
+        if (try_group()) return FCX_OK;
+        grp.clear();
+        ++gi;
+      }
+    }
+    if (!grp.empty() && try_group()) return FCX_OK;
+  }
+  return FCX_OK;
+}
+
 // Register slot (AvgSlot) of the type-0 average of (g, var), or -1 when it has to be done
 // by re-reading X_s: every surface type must produce X_s in registers in this launch (a
 // computing method and a bound output -- not 'none'/'copy'), and one FARE array per type
@@ -902,6 +981,7 @@ static int build_plan(fcx_engine *e, uint32_t stages, int avg_phases, Plan &pl) 
     if (!writes.count(b)) pure.push_back(b);
   pl.reads.swap(pure);
   plan_fused_atmos(e, pl, stages, avg_phases);
+  if (int r = plan_fused_records(e, pl, stages, avg_phases)) return r;
   HIP_TRY(hipMalloc(&pl.dev, sizeof(Params)));
   HIP_TRY(hipMemcpy(pl.dev, &P, sizeof(Params), hipMemcpyHostToDevice));
   return FCX_OK;
@@ -1509,6 +1589,7 @@ static int launch_plan(fcx_engine *e, Plan *pl, const double *corr_m, int64_t lo
   lc.variant = (e->specialize && lc.merged) ? pl->variant : 0;
   lc.f32 = e->f32;
   lc.ravg = pl->host.ravg_on != 0;
+  lc.rec = pl->host.rec != nullptr;
   // the fp32 fused kernel has no fix-up kernel: it needs the in-launch hand-off (no grid cap)
   const bool fused = pl->atm_fused && lc.variant && lc.cells_per_thread == 2 &&
                      (!lc.f32 || (lc.max_blocks <= 0 && pl->af.err != nullptr));
@@ -1659,7 +1740,9 @@ static int run_atmos(fcx_engine *e, int phase) {
 // weight application OASIS performs on 'S' fields sent to a model; atmos_kernel with the
 // target's CSR (columns = exchange cells), up to kMaxAtmosFields fields per launch
 static int run_remaps(fcx_engine *e, int phase) {
-  for (auto &rm : e->remaps) {
+  for (size_t ri = 0; ri < e->remaps.size(); ++ri) {
+    auto &rm = e->remaps[ri];
+    int gi = 0;
     AtmosArgs a{};
     a.f32 = e->f32 ? 1 : 0;
     a.row_ptr = rm.d_row;
@@ -1672,7 +1755,11 @@ static int run_remaps(fcx_engine *e, int phase) {
       if (!a.nf) return FCX_OK;
       a.rec = nullptr;
       a.rec_p = 0;
-      if (e->d_rec && remap_packs(e, rm, a.nf)) {  // fields -> one record per cell, then the gather
+      const Plan *rp = e->rec_plan;
+      if (rp && rp->rec_remap == (int)ri && rp->rec_group == gi) {  // records written by the flux launch
+        a.rec = rp->host.rec;
+        a.rec_p = rp->host.rec_p;
+      } else if (e->d_rec && remap_packs(e, rm, a.nf)) {  // fields -> one record per cell, then the gather
         a.rec_p = rec_width(e, a.nf);
         const int r = launch_pack_records(a, (int64_t)rm.max_src + 1, e->aligned16, !e->zc_active && e->launch.nontemporal,
                                           e->d_rec, e->stream);
@@ -1682,6 +1769,7 @@ static int run_remaps(fcx_engine *e, int phase) {
       const int r = launch_atmos(a, e->stream);
       if (r) return fail(FCX_E_HIP, "remap launch: %s", hipGetErrorString((hipError_t)r));
       a.nf = 0;
+      ++gi;
       return FCX_OK;
     };
     for (auto &f : rm.fields) {
@@ -1714,10 +1802,12 @@ extern "C" int fcx_run(fcx_engine *e, int phase, int32_t t) {
   if (e->timing) HIP_TRY(hipEventRecord(e->ev0, e->stream));
   e->atm_done_fused = false;
   e->atm_done = e->exchanged = false;
+  e->rec_plan = nullptr;
   if (!e->any_regrid) {
     Plan *pl;
     if (int r = get_plan(e, phase_stages(phase), phase, &pl)) return r;
     if (int r = launch_plan(e, pl, corr_m)) return r;
+    e->rec_plan = pl;
   } else {
     std::vector<std::pair<uint32_t, int>> seq;
     staged_sequence(phase, seq);
@@ -1783,6 +1873,7 @@ static int step_pipelined(fcx_engine *e, int phase, int32_t t, Plan *pl) {
   if (e->timing) HIP_TRY(hipEventRecord(e->ev0, e->s_in));
   e->atm_done_fused = false;
   e->atm_done = e->exchanged = false;
+  e->rec_plan = pl;
   for (int k = 0; k < K; ++k) {
     const int64_t lo = k * per, hi = std::min(n, lo + per);
     const bool last = k == K - 1;
@@ -2273,6 +2364,7 @@ extern "C" int fcx_remap_info(const fcx_engine *e, int32_t remap_id, double *sca
   }
   *scatter = rm.scatter;
   *packed = e->d_rec && remap_packs(e, rm, nf_max) ? 1 : 0;
+  if (e->rec_plan && e->rec_plan->rec_remap == remap_id) *packed = 2;  // the last run's flux launch wrote them
   return FCX_OK;
 }
 

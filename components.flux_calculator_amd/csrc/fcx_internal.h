@@ -89,6 +89,13 @@ struct Params {
   int32_t ravg_on;        // any ravg.out set (selects the RAVG kernel instantiation)
   int32_t pad2;
   int64_t tpad;           // tile-blocked layout of every field pointer above (0: contiguous)
+  // remap records written by the T=1 specialised launch (the fields of one remap launch
+  // group, fcx_engine.hip plan_fused_records): cell j's record at rec + j * rec_p, the value
+  // of register slot k (AvgSlot 0..5) at position rec_pos[k] (-1 = not in the record)
+  double *rec;
+  int32_t rec_p;
+  int8_t rec_pos[6];
+  int8_t pad3[2];
 };
 
 // launchers (fcx_kernels.hip); return hipError_t as int
@@ -104,6 +111,8 @@ struct LaunchConfig {
   bool ravg = false;         // register averages in this plan (Params::ravg_on)
   int64_t lo = 0, hi = -1;   // cell range of this launch (lo a multiple of kChunkAlign;
                              // hi < 0: to n_max) -- the pipelined host-bound step
+  bool rec = false;          // Params::rec set: the launch also writes remap records
+                             // (T=1 specialised fp64 kernels, 2 cells per lane)
 };
 constexpr int64_t kChunkAlign = 1024;  // chunk boundaries: whole wave tiles and vectors
 

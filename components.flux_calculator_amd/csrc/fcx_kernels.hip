@@ -225,6 +225,62 @@ struct Sink {
   }
 };
 
+// Remap records (Params::rec): every flux of register slot k the T=1 launch produces is also
+// stored at position rec_pos[k] of its cell's record, so that a remap of those fields
+// gathers one record per link without a packing pass (fcx_engine.hip plan_fused_records).
+template <int C, class R, class Inner>
+struct RecEmit {
+  const Inner &inner;
+  R *rec;             // record of the lane's first cell
+  int P;              // elements per record
+  const int8_t *pos;  // Params::rec_pos (wave-uniform)
+  int nv;             // cells of the lane inside the grid
+#ifndef FCX_REC_VEC  // 1: the values stay in registers and each record goes out as 16-B stores
+#define FCX_REC_VEC 1
+#endif
+  mutable R vals[6][C];
+  template <int CC, class RR>
+  __device__ __forceinline__ void operator()(int k, const Vec<CC, RR> &x) const {
+    inner(k, x);
+    if (FCX_REC_VEC) {
+      if (k < 6) {
+#pragma unroll
+        for (int i = 0; i < CC; ++i) vals[k][i] = x.v[i];
+      }
+      return;
+    }
+    const int p = pos[k];
+    if (p >= 0) {
+#pragma unroll
+      for (int i = 0; i < CC; ++i)
+        if (i < nv) rec[i * P + p] = x.v[i];
+    }
+  }
+  __device__ __forceinline__ void flush() const {
+    if (!FCX_REC_VEC) return;
+    constexpr int V = 16 / sizeof(R);
+#pragma unroll
+    for (int i = 0; i < C; ++i) {
+      if (i >= nv) break;
+#pragma unroll
+      for (int q = 0; q < 6 / V; ++q) {
+        if (q * V >= P) break;
+        using VecT = typename std::conditional<sizeof(R) == 8, d2, f4>::type;
+        VecT t;
+#pragma unroll
+        for (int h = 0; h < V; ++h) {
+          R v = R(0);
+#pragma unroll
+          for (int k = 0; k < 6; ++k)
+            if (pos[k] == q * V + h) v = vals[k][i];
+          t[h] = v;
+        }
+        *reinterpret_cast<VecT *>(rec + i * P + q * V) = t;
+      }
+    }
+  }
+};
+
 // VAR: 0 = generic (methods read from the parameter block); 1/2/3 = the CCLM / MOM5 / RCO
 // variant with the QSUR/MEVA/HSEN/momentum methods of every surface type fixed at compile
 // time, so the other method paths vanish from the code and its register budget.  Any T.
@@ -235,21 +291,31 @@ struct Sink {
 // TM: 1 = one surface type, fixed at compile time (the held inputs and the type loop
 // vanish); 0 = T from the parameter block.  RAVG (register averages) needs TM = 0.
 template <int C, bool MERGED, int VAR, bool NT, class R = double, int TM = 1, bool RAVG = false,
-          class Emit = NoEmit>
+          class Emit = NoEmit, bool REC = false>
 __device__ __forceinline__ void process(const Params *__restrict__ P, const double *__restrict__ corr_m,
-                                        int64_t j0, const Emit &emit = Emit(),
+                                        int64_t j0, const Emit &emit_in = Emit(),
                                         AccLds<C, R> acc_lds = AccLds<C, R>{nullptr, 0}) {
   static_assert(!(RAVG && TM), "register averages need more than one surface type");
+  static_assert(!REC || (TM == 1 && !RAVG), "remap records: the T=1 launch");
   const uint32_t stages = P->stages;
   const int T = TM ? 1 : P->num_types;
   const int64_t nt = P->n[0];
   const bool do_t = j0 < nt;
+  using SinkEmit = typename std::conditional<REC, RecEmit<C, R, Emit>, const Emit &>::type;
+  SinkEmit emit = [&]() -> SinkEmit {
+    if constexpr (REC)
+      return RecEmit<C, R, Emit>{emit_in, reinterpret_cast<R *>(P->rec) + j0 * P->rec_p, P->rec_p, P->rec_pos,
+                                 (int)min((int64_t)C, nt - j0)};
+    else
+      return emit_in;
+  }();
   const int64_t D_ = (j0 >> kLayoutShift) * P->tpad;  // field layout shift of this lane's cells
   Vec<C, R> corr = {};  // the month slice is a plain contiguous array
   if (do_t && corr_m && (stages & S_MEVA)) corr = ld<C, NT, R>(reinterpret_cast<const R *>(corr_m), j0, nt);
   Vec<C, R> rsdd = {};
   if (do_t && P->rsdd0 && (stages & S_RSDR)) rsdd = LD(P->rsdd0, j0, nt);
-  Sink<C, R, RAVG, Emit> sink(emit, P->ravg, acc_lds);
+  Sink<C, R, RAVG, typename std::remove_cv<typename std::remove_reference<SinkEmit>::type>::type> sink(
+      emit, P->ravg, acc_lds);
 
   // inputs held across surface types, with the pointer they were loaded from
   Vec<C, R> ts = {}, fi = {}, ps = {}, pa = {}, qa = {}, ta = {}, u = {}, v = {}, amoi = {}, cmoi = {},
@@ -451,6 +517,7 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
 #undef HOLDA
 #undef HOLDX
 
+  if constexpr (REC) emit.flush();
   // ---- average_across_surface_types (calc:376-383), summed in type order
   if constexpr (RAVG) {
     if (do_t) {
@@ -480,7 +547,7 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
 }
 
 // cells [lo, hi) of the plan (lo a multiple of C), grid-stride over C-cell units
-template <int C, bool MERGED, int VAR, bool NT, class R, int TM, bool RAVG>
+template <int C, bool MERGED, int VAR, bool NT, class R, int TM, bool RAVG, bool REC = false>
 __global__ __launch_bounds__(256, RAVG ? 3 : 1) void cells_kernel(const Params *__restrict__ P,
                                                     const double *__restrict__ corr_m, int64_t lo,
                                                     int64_t hi) {
@@ -490,7 +557,7 @@ __global__ __launch_bounds__(256, RAVG ? 3 : 1) void cells_kernel(const Params *
   __shared__ R s_acc[RAVG ? kAvgSlots * 256 * C : 1];
   const AccLds<C, R> acc{s_acc + threadIdx.x * C, 256 * C};
   for (int64_t u = lo / C + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u < u_end; u += stride)
-    process<C, MERGED, VAR, NT, R, TM, RAVG>(P, corr_m, u * C, NoEmit(), acc);
+    process<C, MERGED, VAR, NT, R, TM, RAVG, NoEmit, REC>(P, corr_m, u * C, NoEmit(), acc);
 }
 
 // The T=1 hot path with the exchange -> atmosphere accumulation fused in (AtmosFused).
@@ -682,8 +749,9 @@ __device__ __forceinline__ void take_carry(const AtmosFused &af, int64_t tile, d
 #endif
 template <int C>
 constexpr int atmos_waves() { return C == 4 ? FCX_F32_ATMOS_WAVES : 4; }
-template <int C, class R, int VAR, bool NT, int TM, bool RAVG>
-__global__ __launch_bounds__(64 * atmos_waves<C>(), RAVG ? FCX_RAVG_ATMOS_BLOCKS : FCX_T1_ATMOS_BLOCKS) void cells_atmos_kernel(const Params *__restrict__ P,
+template <int C, class R, int VAR, bool NT, int TM, bool RAVG, bool REC = false>
+// (REC: the record stores took CCLM to 129 VGPRs and 3 waves per SIMD; capped at 4 blocks = 4 waves)
+__global__ __launch_bounds__(64 * atmos_waves<C>(), RAVG ? FCX_RAVG_ATMOS_BLOCKS : REC ? 4 : FCX_T1_ATMOS_BLOCKS) void cells_atmos_kernel(const Params *__restrict__ P,
                                                           const double *__restrict__ corr_m,
                                                           const AtmosFused af, int64_t lo, int64_t hi) {
   static_assert(!RAVG || (C == 2 && sizeof(R) == 8), "register averages: fp64 engine only");
@@ -740,7 +808,7 @@ __global__ __launch_bounds__(64 * atmos_waves<C>(), RAVG ? FCX_RAVG_ATMOS_BLOCKS
     const int64_t tend = t0 + kT;
     const int32_t next_a = (tend < n) ? af.idx[tend] : -3;
     if (j0 < n)
-      process<C, true, VAR, NT, R, TM, RAVG>(P, corr_m, j0, emit,
+      process<C, true, VAR, NT, R, TM, RAVG, LdsEmitT<C>, REC>(P, corr_m, j0, emit,
                                              AccLds<C, R>{reinterpret_cast<R *>(wp + emit.s), kR});
     if constexpr (kXF) {  // the weights row of the fp32 fluxes (dead cells: weight 0)
 #pragma unroll
@@ -1060,6 +1128,17 @@ static void launch_c(const LaunchConfig &lc, int blocks, hipStream_t s, const Pa
   }
 }
 
+template <int VAR>
+static void launch_rec(bool nt, int blocks, hipStream_t s, const Params *dp, const double *corr_m, int64_t lo,
+                       int64_t hi) {
+  if (nt)
+    hipLaunchKernelGGL((cells_kernel<2, true, VAR, true, double, 1, false, true>), dim3(blocks), dim3(256), 0, s, dp,
+                       corr_m, lo, hi);
+  else
+    hipLaunchKernelGGL((cells_kernel<2, true, VAR, false, double, 1, false, true>), dim3(blocks), dim3(256), 0, s, dp,
+                       corr_m, lo, hi);
+}
+
 // type mode: one surface type (compile-time), several, several with register averages
 template <int C, class R>
 static void launch_r(const Params *hp, const LaunchConfig &lc, int blocks, hipStream_t s, const Params *dp,
@@ -1072,15 +1151,15 @@ static void launch_r(const Params *hp, const LaunchConfig &lc, int blocks, hipSt
     launch_c<C, R, 0, false>(lc, blocks, s, dp, corr_m, lo, hi);
 }
 
-template <int C, class R, int VAR, int TM, bool RAVG>
+template <int C, class R, int VAR, int TM, bool RAVG, bool REC = false>
 static void launch_atm(bool nt, int blocks, hipStream_t s, const Params *dp, const double *corr_m,
                        const AtmosFused &af, int64_t lo, int64_t hi) {
   if (nt)
-    hipLaunchKernelGGL((cells_atmos_kernel<C, R, VAR, true, TM, RAVG>), dim3(blocks), dim3(64 * atmos_waves<C>()), 0,
-                       s, dp, corr_m, af, lo, hi);
+    hipLaunchKernelGGL((cells_atmos_kernel<C, R, VAR, true, TM, RAVG, REC>), dim3(blocks), dim3(64 * atmos_waves<C>()),
+                       0, s, dp, corr_m, af, lo, hi);
   else
-    hipLaunchKernelGGL((cells_atmos_kernel<C, R, VAR, false, TM, RAVG>), dim3(blocks), dim3(64 * atmos_waves<C>()), 0,
-                       s, dp, corr_m, af, lo, hi);
+    hipLaunchKernelGGL((cells_atmos_kernel<C, R, VAR, false, TM, RAVG, REC>), dim3(blocks), dim3(64 * atmos_waves<C>()),
+                       0, s, dp, corr_m, af, lo, hi);
 }
 
 // fused accumulation: one surface type (its fluxes), or several with the type-0 averages in
@@ -1092,6 +1171,8 @@ static int launch_atm_r(const Params *hp, const LaunchConfig &lc, int blocks, hi
     launch_atm<4, float, VAR, 1, false>(lc.nontemporal, blocks, s, dp, corr_m, af, lo, hi);
   else if (lc.f32)
     return (int)hipErrorInvalidValue;
+  else if (hp->num_types == 1 && lc.rec)
+    launch_atm<2, double, VAR, 1, false, true>(lc.nontemporal, blocks, s, dp, corr_m, af, lo, hi);
   else if (hp->num_types == 1)
     launch_atm<2, double, VAR, 1, false>(lc.nontemporal, blocks, s, dp, corr_m, af, lo, hi);
   else if (lc.ravg)
@@ -1130,6 +1211,16 @@ int launch_cells(const Params *hp, const Params *dp, const double *corr_m, const
   const int c = lc.cells_per_thread == 1 ? 1 : lc.f32 ? 4 : 2;
   const int64_t units = (hi - lo + c - 1) / c;
   const int blocks = grid_for(units, lc.max_blocks < 0 ? 8192 : lc.max_blocks);
+  if (lc.rec) {  // remap records: the T=1 specialised fp64 kernels only (the planner's rule)
+    if (lc.f32 || c != 2 || hp->num_types != 1 || !lc.merged || lc.variant < 1 || lc.variant > 3)
+      return (int)hipErrorInvalidValue;
+    switch (lc.variant) {
+      case 1: launch_rec<1>(lc.nontemporal, blocks, s, dp, corr_m, lo, hi); break;
+      case 2: launch_rec<2>(lc.nontemporal, blocks, s, dp, corr_m, lo, hi); break;
+      default: launch_rec<3>(lc.nontemporal, blocks, s, dp, corr_m, lo, hi); break;
+    }
+    return (int)hipGetLastError();
+  }
   if (lc.f32) {
     if (c == 4)
       launch_r<4, float>(hp, lc, blocks, s, dp, corr_m, lo, hi);

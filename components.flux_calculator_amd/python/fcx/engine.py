@@ -196,10 +196,11 @@ class Engine:
         _lib.check(self.lib.fcx_atmos_finish(self.h))
 
     def remap_info(self, remap_id=0):
-        """(scatter, packed) of a remap (fcx_remap_info)."""
+        """(scatter, packed) of a remap (fcx_remap_info): packed 0 = gather from the arrays,
+        1 = packing pass, 2 = records written by the last run's flux launch."""
         sc, pk = ctypes.c_double(), ctypes.c_int32()
         _lib.check(self.lib.fcx_remap_info(self.h, remap_id, ctypes.byref(sc), ctypes.byref(pk)))
-        return sc.value, bool(pk.value)
+        return sc.value, pk.value
 
     def set_option(self, name, value):
         _lib.check(self.lib.fcx_set_option(self.h, self.OPTIONS[name], int(value)))

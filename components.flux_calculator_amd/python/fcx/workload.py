@@ -14,7 +14,7 @@ import numpy as np
 
 from .basic import PHASE_ALL, PHASE_NORMAL
 from .engine import Engine
-from .parallel import PeriodicAtmosMap, apple_range
+from .parallel import PeriodicAtmosMap, apple_range, local_atmos, synthetic_atmos_map
 from .synthetic import BASE_SEED, as_dtype, build_case, inputs_for_bench
 
 VARIANTS = ("CCLM", "MOM5", "RCO")
@@ -31,7 +31,7 @@ class Workload:
 
     def __init__(self, n_global, rank=0, world=1, variants=VARIANTS, types=1, bias=False,
                  precision="f64", atmos=True, caller_device=False, device=0, stream=None,
-                 engine_options=None):
+                 engine_options=None, atmos_map="periodic"):
         import torch
 
         self.n_global, self.rank, self.world = int(n_global), int(rank), int(world)
@@ -52,7 +52,16 @@ class Workload:
         else:
             data, case_dev = host, None
         self.caller_device = caller_device
-        self.la = PeriodicAtmosMap().local(self.offset, self.n, self.rank, self.world, self.n_global) if atmos else None
+        # periodic: runs of 3, 4, 5, 4 cells that never cross a 16-cell period (nor a wave
+        # tile); random: runs of 3..5 cells at random, so that segments cross wave tiles and
+        # the fused kernel hands carries on as on a real intersection grid
+        if not atmos:
+            self.la = None
+        elif atmos_map == "random":
+            self.la = local_atmos(synthetic_atmos_map(self.n_global), self.rank, self.world)
+        else:
+            self.la = PeriodicAtmosMap().local(self.offset, self.n, self.rank, self.world, self.n_global)
+        self.atmos_map = atmos_map
         nb, stride = max(self.world - 1, 0), len(ATM_FIELDS)
         self.n_boundaries, self.stride = nb, stride
         # [variant][boundary][field]: the shared slots of every variant in one buffer

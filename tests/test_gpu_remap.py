@@ -183,9 +183,9 @@ def test_remap_pack_auto_follows_the_map_scatter():
     info = [eng.remap_info(i) for i in range(3)]
     eng.step(PHASE_ALL, 0)
     eng.close()
-    assert info[0][1] and info[0][0] > 0.5, info
-    assert not info[1][1] and info[1][0] < 0.5, info
-    assert not info[2][1], info
+    assert info[0][1] == 1 and info[0][0] > 0.5, info
+    assert info[1][1] == 0 and info[1][0] < 0.5, info
+    assert info[2][1] == 0, info
     for mm, oo in zip((shuf, geo), outs):
         for name, g in FIELDS:
             want = oracle_lib.remap_apply(mm.src, mm.dst, mm.weight, np.asarray(case.lf.field[(1, g, name)]),
@@ -193,3 +193,55 @@ def test_remap_pack_auto_follows_the_map_scatter():
             np.testing.assert_array_equal(oo[name], want, err_msg=name)
     np.testing.assert_array_equal(one, oracle_lib.remap_apply(shuf.src, shuf.dst, shuf.weight,
                                                               np.asarray(case.lf.field[(1, 1, "HLAT")]), shuf.n_model))
+
+
+@pytest.mark.parametrize("variant", ["CCLM", "MOM5", "RCO"])
+@pytest.mark.parametrize("atmos", [False, True])
+@pytest.mark.parametrize("host", ["device", "pipelined"])
+def test_remap_records_from_the_flux_launch(variant, atmos, host):
+    """T=1: the records of a remap of type-1 fluxes are written by the flux kernel itself
+    (fcx_remap_info packed == 2, no packing pass), alone or beside the fused atmosphere
+    accumulation, HBM-resident or in the pipelined host step; a second remap of the same fields
+    (one record buffer per plan) and a remap with a field the kernel does not hold (TSUR) take
+    the packing pass.  Every output equals the sequential application of the engine's own
+    fluxes, bit for bit."""
+    torch = pytest.importorskip("torch")
+    from fcx.parallel import local_atmos, synthetic_atmos_map
+
+    n = 70_001
+    dev = torch.device("cuda", 0)
+    case = build_case(variant, n=n, T=1, bias=True, seed=11, device=dev if host == "device" else None)
+    shuf = synthetic_model_map(n, n // 4, links_per_cell=2, seed=12)
+    names = [k for k in FIELDS if not (variant == "RCO" and k[0] == "QSUR")]
+    outs = [{k: np.full(shuf.n_model, np.nan) for k, _ in names} for _ in range(2)]
+    ts_out = {"HSEN": np.full(shuf.n_model, np.nan), "TSUR": np.full(shuf.n_model, np.nan)}
+    remaps = [remap_spec(shuf, outs[0]), remap_spec(shuf, outs[1]),
+              {"n_dst": shuf.n_model, "src": shuf.src, "dst": shuf.dst, "w": shuf.weight,
+               "fields": [(2, 1, 1, "HSEN", ts_out["HSEN"]), (2, 1, 1, "TSUR", ts_out["TSUR"])]}]
+    kw = {}
+    if atmos:
+        amap = synthetic_atmos_map(n)
+        atm = {k: np.full(amap.n_atmos, np.nan) for k, _ in names}
+        kw["atmos"] = {"local": local_atmos(amap, 0, 1), "fields": [(2, 1, g, k, atm[k]) for k, g in names]}
+    opts = {"pipeline_min_chunk": 8192} if host == "pipelined" else {}
+    eng = Engine(case.lf, 1, case.methods, corrections=case.corrections, remaps=remaps, options=opts, **kw)
+    eng.step(PHASE_ALL, STEP_T)
+    info = [eng.remap_info(i)[1] for i in range(3)]
+    eng.close()
+    assert info == [2, 1, 1], info
+
+    def flux(k, g):
+        a = case.lf.field[(1, g, k)]
+        return a.cpu().numpy() if hasattr(a, "cpu") else np.asarray(a)
+
+    for oo in outs:
+        for name, g in names:
+            want = oracle_lib.remap_apply(shuf.src, shuf.dst, shuf.weight, flux(name, g), shuf.n_model)
+            np.testing.assert_array_equal(oo[name], want, err_msg=name)
+    for name in ("HSEN", "TSUR"):
+        want = oracle_lib.remap_apply(shuf.src, shuf.dst, shuf.weight, flux(name, 1), shuf.n_model)
+        np.testing.assert_array_equal(ts_out[name], want, err_msg=name)
+    if atmos:
+        for name, g in names:
+            want = oracle_lib.atmos_accumulate(amap.atmos_index, amap.weight, flux(name, g), amap.n_atmos)
+            np.testing.assert_array_equal(atm[name], want, err_msg=f"atmos {name}")
