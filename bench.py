@@ -68,15 +68,21 @@ def parse():
                    help="rehearsal only: every rank on GPU 0 (with --backend gloo on a 1-GPU box)")
     p.add_argument("--max-blocks", type=int, default=None,
                    help="A/B only: FCX_OPT_MAX_BLOCKS of every engine (default: the engine's)")
-    p.add_argument("--atmos-map", choices=("periodic", "random"), default="periodic",
-                   help="exchange->atmosphere map: periodic runs of 3,4,5,4 cells, or runs of 3..5 at "
-                        "random (segments cross the kernel's wave tiles, as on a real intersection grid)")
+    p.add_argument("--atmos-map", choices=("periodic", "random"), default="random",
+                   help="exchange->atmosphere map: runs of 3..5 cells at random (default: segments cross "
+                        "the kernel's 128-cell wave tiles, as on a real intersection grid), or periodic runs "
+                        "of 3,4,5,4 cells (no segment crosses a tile; the round-1 bench map)")
+    p.add_argument("--other-map", type=int, default=1,
+                   help="also time the same workload on the other atmosphere map (an 'other_map' sub-object)")
     p.add_argument("--caller-device", action="store_true",
                    help="bind the caller's device arrays (contiguous torch tensors, the inputs shared "
                         "by the variants) instead of host arrays whose engine-owned device mirrors "
                         "(tile-blocked, FCX_OPT_TILED_LAYOUT) are uploaded once before the timed region")
     p.add_argument("--tiled", type=int, default=1, help="FCX_OPT_TILED_LAYOUT of the engines (A/B)")
     p.add_argument("--nontemporal", type=int, default=1, help="FCX_OPT_NONTEMPORAL of the engines (A/B)")
+    p.add_argument("--carry-handoff", type=int, default=0,
+                   help="FCX_OPT_CARRY_HANDOFF of the engines (A/B): 1 = carries across wave tiles handed "
+                        "over inside the launch instead of the fix-up kernel")
     p.add_argument("--precision", choices=("f64", "f32"), default="f64",
                    help="f32: the fp32 variant (config 5): fp32 cell pass with the accumulation fused in "
                         "(fp32 fluxes, fp64 weights, products and sums, fp32 outputs)")
@@ -284,7 +290,8 @@ def main():
 
     coll = comm if comm is not None else (TorchCollective() if world > 1 else None)
 
-    engine_options = {"tiled_layout": args.tiled, "nontemporal": args.nontemporal}
+    engine_options = {"tiled_layout": args.tiled, "nontemporal": args.nontemporal,
+                      "carry_handoff": args.carry_handoff}
     if args.max_blocks is not None:
         engine_options["max_blocks"] = args.max_blocks
     # this rank's APPLE range (decomp_def.F90:23-31): weak scaling (every rank owns args.cells
@@ -395,18 +402,41 @@ def main():
     del wl
     torch.cuda.synchronize()
 
+    # the same workload on the other atmosphere map (periodic: no carried segment, no fix-up)
+    if args.other_map and args.atmos:
+        other = "periodic" if args.atmos_map == "random" else "random"
+        wo = Workload(n_global, rank, world, variants, types=args.types, bias=args.bias, precision=args.precision,
+                      atmos=True, caller_device=args.caller_device, device=gpu, atmos_map=other,
+                      stream=torch.cuda.current_stream(dev), engine_options=engine_options)
+        wl = wo
+        mo = measure(wo, args, world, dist, coll if comm is None else comm, args.steps, args.warmup)
+        ko = mo["kern_ms"].mean(axis=0)
+        do = int(np.argmax(ko))
+        out["other_map"] = {
+            "atmos_map": other,
+            "value": round(n_global * len(variants) * args.steps / mo["t_max"] / 1e6, 1),
+            "unit": "Mcells/s",
+            "ms_per_step": round(mo["t_max"] / args.steps * 1e3, 4),
+            "dominant_kernel_ms": round(float(ko[do]), 4),
+            "frac": round(wo.alg_bytes[do] / (ko[do] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+        }
+        wo.close()
+        del wo, wl
+        torch.cuda.synchronize()
+
     # config 4 at this N: the fixed 40M-cell grid over the same ranks (strong scaling)
     if args.config4 and not args.global_cells:
         w4 = Workload(args.config4, rank, world, variants, types=1, precision=args.precision,
                       atmos=bool(args.atmos), device=gpu, stream=torch.cuda.current_stream(dev),
-                      engine_options=engine_options)
+                      engine_options=engine_options, atmos_map=args.atmos_map)
         wl = w4
         m4 = measure(w4, args, world, dist, coll if comm is None else comm, args.steps, args.warmup)
         k4 = m4["kern_ms"].mean(axis=0)
         d4 = int(np.argmax(k4))
         out["config4"] = {
             "workload": "config 4: fixed synthetic grid sharded by APPLE ranges over the ranks (strong scaling), "
-                        "CCLM+MOM5+RCO fused kernels + accumulation, one all-reduce of the boundary slots per step",
+                        "CCLM+MOM5+RCO fused kernels + accumulation, one all-reduce of the boundary slots per step, "
+                        f"{args.atmos_map} atmosphere map",
             "cells_global": args.config4,
             "cells_per_gpu": w4.n,
             "value": round(args.config4 * len(variants) * args.steps / m4["t_max"] / 1e6, 1),

@@ -134,6 +134,10 @@ struct fcx_engine {
   int32_t atm_maxseg = 0;
   double *d_atm_carry = nullptr;
   uint32_t *d_atm_flag = nullptr;  // [tiles] hand-off flags (epoch tags)
+  int32_t *d_atm_head = nullptr;   // [tiles] head cells of every tile (fix-up kernel)
+  double *d_atm_headp = nullptr;   // [tiles][kHeadCells][kFusedFields] their products
+  int64_t atm_crossings = 0;       // 128-cell tile boundaries inside a segment of the map
+  bool carry_handoff = false;      // FCX_OPT_CARRY_HANDOFF: carries handed over inside the launch
   uint32_t *h_atm_err = nullptr;   // mapped host word: a hand-off wait gave up
   uint32_t atm_epoch = 0;          // tag of the current run's hand-offs
   double *d_atm_w = nullptr;
@@ -297,6 +301,8 @@ extern "C" int fcx_destroy(fcx_engine *e) {
   (void)hipFree(e->d_atm_idx);
   (void)hipFree(e->d_atm_carry);
   (void)hipFree(e->d_atm_flag);
+  (void)hipFree(e->d_atm_head);
+  (void)hipFree(e->d_atm_headp);
   if (e->h_atm_err) (void)hipHostFree(e->h_atm_err);
   (void)hipFree(e->d_atm_col);
   (void)hipFree(e->d_atm_w);
@@ -633,6 +639,8 @@ static void plan_fused_atmos(fcx_engine *e, Plan &pl, uint32_t stages, int phase
   af.w = e->d_atm_w;
   af.carry = e->d_atm_carry;
   af.flag = e->d_atm_flag;
+  af.head = e->d_atm_head;
+  af.headp = e->d_atm_headp;
   if (e->h_atm_err && hipHostGetDevicePointer((void **)&af.err, e->h_atm_err, 0) != hipSuccess) af.err = nullptr;
   af.n_atmos = e->n_atmos;
   af.shared = e->atm_shared;
@@ -1454,6 +1462,12 @@ extern "C" int fcx_commit(fcx_engine *e) {
       HIP_TRY(hipMalloc(&e->d_atm_carry, (size_t)std::max<int64_t>(tiles, 1) * kFusedFields * sizeof(double)));
       HIP_TRY(hipMalloc(&e->d_atm_flag, (size_t)std::max<int64_t>(tiles, 1) * sizeof(uint32_t)));
       HIP_TRY(hipMemset(e->d_atm_flag, 0, (size_t)std::max<int64_t>(tiles, 1) * sizeof(uint32_t)));
+      HIP_TRY(hipMalloc(&e->d_atm_head, (size_t)std::max<int64_t>(tiles, 1) * sizeof(int32_t)));
+      HIP_TRY(hipMalloc(&e->d_atm_headp, (size_t)std::max<int64_t>(tiles, 1) * kHeadCells * kFusedFields * sizeof(double)));
+      // tile boundaries a segment runs across: none (a map whose runs never cross a wave
+      // tile) means no fix-up launch at all
+      e->atm_crossings = 0;
+      for (size_t b = kTile; b < e->atm_idx.size(); b += kTile) e->atm_crossings += e->atm_idx[b - 1] == e->atm_idx[b];
       if (!e->h_atm_err) {
         HIP_TRY(hipHostMalloc((void **)&e->h_atm_err, sizeof(uint32_t), hipHostMallocMapped));
         *e->h_atm_err = 0;
@@ -1590,9 +1604,7 @@ static int launch_plan(fcx_engine *e, Plan *pl, const double *corr_m, int64_t lo
   lc.f32 = e->f32;
   lc.ravg = pl->host.ravg_on != 0;
   lc.rec = pl->host.rec != nullptr;
-  // the fp32 fused kernel has no fix-up kernel: it needs the in-launch hand-off (no grid cap)
-  const bool fused = pl->atm_fused && lc.variant && lc.cells_per_thread == 2 &&
-                     (!lc.f32 || (lc.max_blocks <= 0 && pl->af.err != nullptr));
+  const bool fused = pl->atm_fused && lc.variant && lc.cells_per_thread == 2;
   if (fused) {  // the shared-slot pointers may have been set after the plan was built
     pl->af.shared = e->atm_shared;
     pl->af.stride = e->atm_stride;
@@ -1601,14 +1613,15 @@ static int launch_plan(fcx_engine *e, Plan *pl, const double *corr_m, int64_t lo
     // carries handed to the next tile's wave inside the launch: only when every wave makes
     // one trip (no grid-stride cap), so a wave only ever waits on an earlier-dispatched one;
     // a run's chunk launches share its epoch (lo == 0 starts a run)
-    pl->af.handoff = lc.max_blocks <= 0 && pl->af.err != nullptr;
+    // (FCX_OPT_CARRY_HANDOFF; the default leaves the carries to atmos_fixup_kernel)
+    pl->af.handoff = e->carry_handoff && lc.max_blocks <= 0 && pl->af.err != nullptr;
     if (lo == 0 && ++e->atm_epoch == 0) e->atm_epoch = 1;
     pl->af.epoch = e->atm_epoch;
   }
   const int r = launch_cells(&pl->host, pl->dev, corr_m, lc, e->stream, fused ? &pl->af : nullptr);
   if (r) return fail(FCX_E_HIP, "cells_kernel launch: %s", hipGetErrorString((hipError_t)r));
-  if (fused && fixup && !pl->af.handoff) {
-    const int r2 = launch_atmos_fixup(pl->af, pl->host.n_max, e->stream);
+  if (fused && fixup && !pl->af.handoff && e->atm_crossings > 0) {
+    const int r2 = launch_atmos_fixup(pl->af, pl->host.n_max, lc.f32, e->stream);
     if (r2) return fail(FCX_E_HIP, "atmos_fixup launch: %s", hipGetErrorString((hipError_t)r2));
   }
   if (fused) {
@@ -2183,6 +2196,9 @@ extern "C" int fcx_set_option(fcx_engine *e, int option, int64_t value) {
       return FCX_OK;
     case FCX_OPT_TEST_HANDOFF_TIMEOUT:
       e->test_handoff_timeout = value != 0;
+      return FCX_OK;
+    case FCX_OPT_CARRY_HANDOFF:
+      e->carry_handoff = value != 0;
       return FCX_OK;
     case FCX_OPT_REMAP_PACK:
       if (e->committed) return fail(FCX_E_STATE, "remap_pack is applied at fcx_commit");

@@ -158,6 +158,7 @@ int launch_pack_records(const AtmosArgs &a, int64_t n, bool aligned16, bool nont
 // launch: the carry is published with write-through stores and flag[tile] = epoch) or by
 // atmos_fixup_kernel after the launch (launches with a grid-stride cap).
 constexpr int kFusedFields = 6;
+constexpr int kHeadCells = 16;  // head products kept per tile for the fix-up (longer heads re-read)
 constexpr int kTile = 128;  // cells per wave iteration (64 lanes x 2)
 struct AtmosFused {
   const int32_t *idx;  // local atmosphere cell of every exchange cell (non-decreasing)
@@ -167,6 +168,10 @@ struct AtmosFused {
   double *carry;       // [n_tiles][kFusedFields]
   uint32_t *flag;      // [n_tiles]: epoch of the run whose carry[tile] is published
   uint32_t *err;       // set when a hand-off wait gave up (never in a correct run)
+  int32_t *head;       // [n_tiles]: cells at the start of the tile that continue the previous
+                       // tile's segment (written when handoff == 0; atmos_fixup_kernel)
+  double *headp;       // [n_tiles][kHeadCells][kFusedFields]: the products w * x of those
+                       // cells (the first kHeadCells of them), as the launch formed them
   uint32_t epoch;      // this run's tag (never 0); the flags start at 0
   int32_t handoff;     // 1: carries handed to the next tile's wave inside the launch
   int64_t n_atmos;
@@ -176,7 +181,9 @@ struct AtmosFused {
   int64_t out_tpad;    // layout of out (tiled atmosphere pool, or 0)
   int32_t scol[kFusedFields];  // shared-slot column of fused field k (AtmosArgs::scol)
 };
-int launch_atmos_fixup(const AtmosFused &af, int64_t n_cells, void *stream);
+// the segments carried over a tile boundary: carry of tile t-1 + the head cells of tile t,
+// for every tile of a launch of n_cells (fp32: 256-cell tiles of float fields)
+int launch_atmos_fixup(const AtmosFused &af, int64_t n_cells, bool f32, void *stream);
 int launch_atmos_finish(const AtmosArgs &a, int32_t n_boundaries, void *stream);
 
 // f32: w, src and dst are float arrays (the reference's single-precision build, where the

@@ -856,6 +856,27 @@ __global__ __launch_bounds__(64 * atmos_waves<C>(), RAVG ? FCX_RAVG_ATMOS_BLOCKS
       for (int e = c; e < end; ++e) add_cell(acc, e);
       segment_done<R>(af, tile, a[i], acc, end == kT && next_a == a[i]);
     }
+    // without the hand-off: the number of head cells (continuing the previous tile's
+    // segment) for atmos_fixup_kernel; 0 when the tile starts a segment
+    if (!af.handoff) {
+      int head = kT;
+#pragma unroll
+      for (int q = 0; q < C; ++q) head = min(head, C * first_bit(m[q]) + q);
+      if (lane == 0) af.head[tile] = head;
+      // the products of the first kHeadCells head cells, one lane per cell, for the fix-up
+      if (lane < min(head, kHeadCells)) {
+        double *hp = af.headp + (tile * kHeadCells + lane) * kFusedFields;
+        if constexpr (kXF) {
+          const float *xr = reinterpret_cast<const float *>(wp);
+          const double we = wp[xrows_doubles<C>() + lds_slot(lane)];
+#pragma unroll
+          for (int k = 0; k < kFusedFields; ++k) hp[k] = we * (double)xr[k * kT + lane];
+        } else {
+#pragma unroll
+          for (int k = 0; k < kFusedFields; ++k) hp[k] = wp[k * kR + lds_slot(lane)];
+        }
+      }
+    }
     // hand-off: the segment the previous tile carried into this one is continued here, from
     // its carry over this tile's products of the segment's cells, in link order
     if (af.handoff && lane == 0 && a[0] >= 0 && a[0] == prev_tile) {
@@ -871,31 +892,41 @@ __global__ __launch_bounds__(64 * atmos_waves<C>(), RAVG ? FCX_RAVG_ATMOS_BLOCKS
   }
 }
 
-// Segments that straddle a tile boundary: continue the carried prefix sum over the next
-// tile's cells (products recomputed from the stored fluxes, same operations, same order).
-__global__ __launch_bounds__(256) void atmos_fixup_kernel(const AtmosFused af, int64_t n) {
-  const int64_t n_tiles = (n + kTile - 1) / kTile;
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= n_tiles - 1) return;
-  const int64_t end = (t + 1) * kTile;
-  const int32_t a = af.idx[end - 1];
-  if (af.idx[end] != a) return;
-  double acc[kFusedFields];
+// Segments that straddle a tile boundary (the default, FCX_OPT_CARRY_HANDOFF = 0): the
+// launch leaves the prefix sum of a tile's last segment in carry[tile] and the number of
+// head cells of every tile (cells that continue the previous tile's segment) in head[tile];
+// this kernel continues each carry over the next tile's head cells, one thread per (tile,
+// field), in link order: the same bits as the in-launch sum.  The launch also leaves the
+// products of the first kHeadCells head cells of every tile (headp, a few dense bytes per
+// tile); the cells of a longer head are recomputed from the stored fluxes with the kernel's
+// own operation (w * x, fp32 fluxes widened).
+// Segments are at most half a tile (the fused path's rule), so a carry never spans a tile.
+template <class R, int kT>
+__global__ __launch_bounds__(256) void atmos_fixup_kernel(const AtmosFused af, int64_t n_tiles) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t t = 1 + i / kFusedFields;
+  const int k = (int)(i % kFusedFields);
+  if (t >= n_tiles || !af.out[k]) return;
+  // every load of the common case (heads of up to 4 cells) issued before the head count is
+  // known: one memory round trip instead of one per cell
+  const int64_t x0 = t * kT;
+  const double *hp = af.headp + t * kHeadCells * kFusedFields + k;
+  const int h = af.head[t];
+  const int32_t a = af.idx[x0];
+  double acc = af.carry[(t - 1) * kFusedFields + k];
+  double p[4];
 #pragma unroll
-  for (int k = 0; k < kFusedFields; ++k) acc[k] = af.out[k] ? af.carry[t * kFusedFields + k] : 0.0;
-  for (int64_t x = end; x < n && af.idx[x] == a; ++x) {
-    const double wx = af.w[x];
+  for (int e = 0; e < 4; ++e) p[e] = hp[e * kFusedFields];
+  if (h == 0) return;
 #pragma unroll
-    for (int k = 0; k < kFusedFields; ++k)
-      if (af.out[k]) acc[k] = acc[k] + wx * af.x[k][tiled(x, af.tpad)];
-  }
-#pragma unroll
-  for (int k = 0; k < kFusedFields; ++k) {
-    if (!af.out[k]) continue;
-    af.out[k][tiled(a, af.out_tpad)] = acc[k];
-    if (a == 0 && af.left >= 0) af.shared[(int64_t)af.left * af.stride + af.scol[k]] = acc[k];
-    if (a == af.n_atmos - 1 && af.right >= 0) af.shared[(int64_t)af.right * af.stride + af.scol[k]] = acc[k];
-  }
+  for (int e = 0; e < 4; ++e)
+    if (e < h) acc = acc + p[e];
+  for (int e = 4; e < min(h, kHeadCells); ++e) acc = acc + hp[e * kFusedFields];
+  const R *xk = reinterpret_cast<const R *>(af.x[k]);
+  for (int e = kHeadCells; e < h; ++e) acc = acc + af.w[x0 + e] * (double)xk[tiled(x0 + e, af.tpad)];
+  reinterpret_cast<R *>(af.out[k])[tiled(a, af.out_tpad)] = (R)acc;
+  if (a == 0 && af.left >= 0) af.shared[(int64_t)af.left * af.stride + af.scol[k]] = acc;
+  if (a == af.n_atmos - 1 && af.right >= 0) af.shared[(int64_t)af.right * af.stride + af.scol[k]] = acc;
 }
 
 // do_regridding (basic:463-522) as CSR-by-destination: row d holds the links with
@@ -1288,12 +1319,16 @@ int launch_atmos_finish(const AtmosArgs &a, int32_t n_boundaries, void *stream) 
   return (int)hipGetLastError();
 }
 
-int launch_atmos_fixup(const AtmosFused &af, int64_t n, void *stream) {
-  const int64_t tiles = (n + kTile - 1) / kTile;
+int launch_atmos_fixup(const AtmosFused &af, int64_t n, bool f32, void *stream) {
+  const int64_t kt = f32 ? tile_cells<4>() : tile_cells<2>();
+  const int64_t tiles = (n + kt - 1) / kt;
   if (tiles < 2) return 0;
-  const int blocks = (int)((tiles - 1 + 255) / 256);
-  hipLaunchKernelGGL(atmos_fixup_kernel, dim3(blocks), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
-                     af, n);
+  const int blocks = (int)(((tiles - 1) * kFusedFields + 255) / 256);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (f32)
+    hipLaunchKernelGGL((atmos_fixup_kernel<float, tile_cells<4>()>), dim3(blocks), dim3(256), 0, s, af, tiles);
+  else
+    hipLaunchKernelGGL((atmos_fixup_kernel<double, tile_cells<2>()>), dim3(blocks), dim3(256), 0, s, af, tiles);
   return (int)hipGetLastError();
 }
 

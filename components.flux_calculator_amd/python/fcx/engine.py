@@ -186,7 +186,7 @@ class Engine:
     OPTIONS = {"cells_per_thread": 1, "max_blocks": 2, "nontemporal": 3, "specialize": 4,
                "atmos_in_run": 5, "pin_host": 6, "pipeline_chunks": 7,
                "pipeline_min_chunk": 8, "zero_copy": 9,
-               "timing": 10, "tiled_layout": 11, "test_handoff_timeout": 12, "remap_pack": 13}
+               "timing": 10, "tiled_layout": 11, "test_handoff_timeout": 12, "remap_pack": 13, "carry_handoff": 14}
 
     def run_atmos(self, phase=PHASE_ALL):
         _lib.check(self.lib.fcx_run_atmos(self.h, phase))

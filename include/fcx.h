@@ -273,6 +273,13 @@ enum fcx_option {
                                    carry hand-off as timed out, so that the recovery of
                                    fcx_synchronize (atmos_kernel recomputes the atmosphere
                                    outputs) runs; the results must be unchanged            */
+  FCX_OPT_CARRY_HANDOFF = 14,   /* fused accumulation, segments crossing a 128-cell wave
+                                   tile: 0 (default) the launch leaves each carry and tile
+                                   head count, atmos_fixup_kernel completes them after it
+                                   (one small launch, none when no segment crosses a tile);
+                                   1: the next tile's wave waits for the carry inside the
+                                   launch (spin-wait on a flag; measured 1.5x slower per
+                                   step on a map whose segments cross tiles)               */
   FCX_OPT_REMAP_PACK = 13,      /* exchange -> model remaps: the fields of a launch packed
                                    cell-major into one record per exchange cell before the
                                    gather, so a link reads one record instead of nf

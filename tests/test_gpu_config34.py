@@ -49,8 +49,11 @@ def sample(n, rng):
 
 
 @pytest.mark.timeout(300)
-def test_config3_bench_path_10M():
-    wl = Workload(10_000_000, variants=VARIANTS)
+@pytest.mark.parametrize("atmos_map", ["random", "periodic"])
+def test_config3_bench_path_10M(atmos_map):
+    """The bench's exact path at config 3's size: the random-run atmosphere map (segments
+    cross the wave tiles: the fix-up kernel completes them) and the periodic one (none do)."""
+    wl = Workload(10_000_000, variants=VARIANTS, atmos_map=atmos_map)
     try:
         wl.run(T_STEP)
         wl.download()
@@ -70,15 +73,16 @@ def test_config3_bench_path_10M():
 
 
 @pytest.mark.timeout(600)
-def test_config4_40M_eight_shards():
+@pytest.mark.parametrize("atmos_map", ["random", "periodic"])
+def test_config4_40M_eight_shards(atmos_map):
     import torch
-    from fcx.parallel import PeriodicAtmosMap
+    from fcx.parallel import PeriodicAtmosMap, synthetic_atmos_map
 
     # 40M + 40 cells: shards of 5,000,005 cells, so the shard ends fall inside atmosphere cells
     # of the periodic map (16 exchange cells = 4 atmosphere cells) and the boundary exchange
     # has work to do (with 5M-cell shards every boundary would coincide with a cell edge)
     n_global, world = 40_000_040, 8
-    shards = [Workload(n_global, r, world, variants=VARIANTS) for r in range(world)]
+    shards = [Workload(n_global, r, world, variants=VARIANTS, atmos_map=atmos_map) for r in range(world)]
     try:
         for wl in shards:
             wl.run(T_STEP)
@@ -90,7 +94,7 @@ def test_config4_40M_eight_shards():
         torch.cuda.synchronize()
         for wl in shards:
             assert float(wl.shared.abs().sum()) == 0.0
-        gmap = PeriodicAtmosMap().global_map(n_global)
+        gmap = PeriodicAtmosMap().global_map(n_global) if atmos_map == "periodic" else synthetic_atmos_map(n_global)
         rng = np.random.default_rng(12)
         for i, v in enumerate(VARIANTS):
             fluxes = {name: np.empty(n_global) for name, _ in ATM_FIELDS}

@@ -198,7 +198,7 @@ def test_fp32_engine_rejects_fp64_outputs():
 # run lengths: 1..7 and 40..64 (the fp32 fused kernel, 256-cell wave tiles: segments within
 # a tile or crossing one boundary), 1..400 (longer than half a 128-cell tile: atmos_kernel)
 @pytest.mark.parametrize("lengths", [(1, 7), (40, 64), (1, 400)])
-@pytest.mark.parametrize("mode", ["handoff", "capped", "pipelined"])
+@pytest.mark.parametrize("mode", ["handoff", "fixup", "capped", "pipelined"])
 @pytest.mark.parametrize("variant", ["CCLM", "MOM5", "RCO"])
 def test_fp32_fused_accumulation(variant, mode, lengths):
     """The fp32 engine's flux kernel with the accumulation fused in (4 cells per lane,
@@ -215,7 +215,7 @@ def test_fp32_fused_accumulation(variant, mode, lengths):
     amap = random_run_map(n, lengths, seed=lengths[1] + 5)
     la = local_atmos(amap, 0, 1)
     outs = {k: np.full(la.n_atmos, np.nan, np.float32) for k, _ in ATM_FIELDS}
-    opts = {"handoff": {}, "capped": {"max_blocks": 64},
+    opts = {"handoff": {"carry_handoff": 1}, "fixup": {}, "capped": {"max_blocks": 64},
             "pipelined": {"pipeline_chunks": 4, "pipeline_min_chunk": 65536, "zero_copy": 0}}[mode]
     eng = Engine(c32.lf, 1, c32.methods, corrections=c32.corrections,
                  atmos={"local": la, "fields": [(2, 1, g, k, outs[k]) for k, g in ATM_FIELDS]}, options=opts)

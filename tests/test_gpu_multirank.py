@@ -79,10 +79,11 @@ def random_run_map(n, lengths, seed):
     return AtmosMap(np.ascontiguousarray(idx, dtype=np.int32), np.ascontiguousarray(w), n_atmos)
 
 
-# run lengths: 1..7 (the fused kernel: segments within a tile or crossing one boundary);
+# run lengths: 1..7 and 20..64 (the fused kernel: segments within a tile or crossing one
+# boundary; heads longer than the fix-up's kHeadCells = 16 kept products are recomputed);
 # 130..140 and 1..400 (longer than half a tile: the engine runs atmos_kernel instead)
-@pytest.mark.parametrize("lengths", [(1, 7), (130, 140), (1, 400)])
-@pytest.mark.parametrize("mode", ["handoff", "capped", "pipelined"])
+@pytest.mark.parametrize("lengths", [(1, 7), (20, 64), (130, 140), (1, 400)])
+@pytest.mark.parametrize("mode", ["handoff", "fixup", "capped", "pipelined"])
 def test_fused_accumulation_long_segments(lengths, mode):
     """The accumulation with segments crossing 128-cell wave tiles: carries handed to the next
     tile's wave inside the launch (default one-trip grid), left to the fix-up kernel (a
@@ -100,7 +101,7 @@ def test_fused_accumulation_long_segments(lengths, mode):
     outs = {name: torch.full((la.n_atmos,), float("nan"), dtype=torch.float64, device="cuda:0")
             for name, _ in FIELDS}
     atmos = {"local": la, "fields": [(2, 1, g, name, outs[name]) for name, g in FIELDS]}
-    opts = {"handoff": {}, "capped": {"max_blocks": 64},
+    opts = {"handoff": {"carry_handoff": 1}, "fixup": {}, "capped": {"max_blocks": 64},
             "pipelined": {"pipeline_chunks": 4, "pipeline_min_chunk": 65536, "zero_copy": 0}}[mode]
     eng = Engine(case.lf, 1, case.methods, corrections=case.corrections, atmos=atmos, options=opts)
     for step in range(3):  # the epochs of later runs must not see stale flags
@@ -134,7 +135,7 @@ def test_handoff_timeout_recovery(host_outputs):
                 for name, _ in FIELDS}
     atmos = {"local": la, "fields": [(2, 1, g, name, outs[name]) for name, g in FIELDS]}
     eng = Engine(case.lf, 1, case.methods, corrections=case.corrections, atmos=atmos,
-                 options={"test_handoff_timeout": 1})
+                 options={"test_handoff_timeout": 1, "carry_handoff": 1})
     for step in range(2):
         for o in outs.values():
             o[:] = float("nan")
