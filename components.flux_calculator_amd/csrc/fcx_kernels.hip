@@ -862,7 +862,12 @@ __global__ __launch_bounds__(64 * atmos_waves<C>(), RAVG ? FCX_RAVG_ATMOS_BLOCKS
       int head = kT;
 #pragma unroll
       for (int q = 0; q < C; ++q) head = min(head, C * first_bit(m[q]) + q);
-      if (lane == 0) af.head[tile] = head;
+#ifndef FCX_DBG_NO_HEAD  // A/B measurement builds only (WRONG atmosphere values): no head stores
+#define FCX_DBG_NO_HEAD 0
+#endif
+      if (FCX_DBG_NO_HEAD >= 2) head = 0;
+      if (lane == 0 && FCX_DBG_NO_HEAD < 2) af.head[tile] = head;
+      if (FCX_DBG_NO_HEAD) head = 0;
       // the products of the first kHeadCells head cells, one lane per cell, for the fix-up
       if (lane < min(head, kHeadCells)) {
         double *hp = af.headp + (tile * kHeadCells + lane) * kFusedFields;
