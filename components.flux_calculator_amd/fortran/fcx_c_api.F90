@@ -19,6 +19,10 @@ MODULE fcx_c_api
                                FCX_FLUX_MOMENTUM = 6, FCX_FLUX_RADIATION_BLACKBODY = 7
   ! regridding matrices (enum fcx_regrid)
   INTEGER(c_int), PARAMETER :: FCX_U_TO_T = 0, FCX_V_TO_T = 1, FCX_T_TO_U = 2, FCX_T_TO_V = 3
+  ! fcx_set_option (enum fcx_option)
+  INTEGER(c_int), PARAMETER :: FCX_OPT_NONTEMPORAL = 3, FCX_OPT_ATMOS_IN_RUN = 5, FCX_OPT_PIN_HOST = 6, &
+                               FCX_OPT_PIPELINE_CHUNKS = 7, FCX_OPT_ZERO_COPY = 9, FCX_OPT_TIMING = 10, &
+                               FCX_OPT_TILED_LAYOUT = 11, FCX_OPT_REMAP_PACK = 13, FCX_OPT_CARRY_HANDOFF = 14
   ! the RCCL unique id travels between the ranks as these many bytes (MPI_Bcast)
   INTEGER, PARAMETER :: FCX_COMM_ID_BYTES = 128
 
@@ -267,6 +271,32 @@ MODULE fcx_c_api
       TYPE(c_ptr), VALUE :: engine
       INTEGER(c_int64_t), INTENT(OUT) :: bytes
       INTEGER(c_int) :: fcx_zero_copy_bytes
+    END FUNCTION
+    ! ---- exchange -> model remaps (the OASIS 'S' maps to a bottom model, SURVEY.md 8f rank 3):
+    ! src/dst 0-based cells, links in file order; outputs REAL(wp) arrays of n_dst cells
+    FUNCTION fcx_add_remap(engine, n_dst, n_links, src_cell, dst_cell, weight, remap_id) &
+        BIND(C, name='fcx_add_remap')
+      IMPORT :: c_int, c_int32_t, c_int64_t, c_ptr
+      TYPE(c_ptr), VALUE :: engine, src_cell, dst_cell, weight
+      INTEGER(c_int64_t), VALUE :: n_dst, n_links
+      INTEGER(c_int32_t), INTENT(OUT) :: remap_id
+      INTEGER(c_int) :: fcx_add_remap
+    END FUNCTION
+    FUNCTION fcx_add_remap_field(engine, remap_id, phase, surface_type, grid, var, out, flags) &
+        BIND(C, name='fcx_add_remap_field')
+      IMPORT :: c_int, c_int32_t, c_ptr
+      TYPE(c_ptr), VALUE :: engine, out
+      INTEGER(c_int32_t), VALUE :: remap_id
+      INTEGER(c_int), VALUE :: phase, surface_type, grid, var, flags
+      INTEGER(c_int) :: fcx_add_remap_field
+    END FUNCTION
+    FUNCTION fcx_remap_info(engine, remap_id, scatter, packed) BIND(C, name='fcx_remap_info')
+      IMPORT :: c_int, c_int32_t, c_double, c_ptr
+      TYPE(c_ptr), VALUE :: engine
+      INTEGER(c_int32_t), VALUE :: remap_id
+      REAL(c_double), INTENT(OUT) :: scatter
+      INTEGER(c_int32_t), INTENT(OUT) :: packed
+      INTEGER(c_int) :: fcx_remap_info
     END FUNCTION
     ! ---- library-owned page-locked host memory (c_f_pointer it onto local_field arrays)
     FUNCTION fcx_host_malloc(bytes, ptr) BIND(C, name='fcx_host_malloc')
