@@ -169,6 +169,61 @@ class PeriodicAtmosMap:
                         int(idx[-1]) + 1 if n_global else 0)
 
 
+class BlockedRandomAtmosMap:
+    """Runs of 3, 4 or 5 exchange cells per atmosphere cell in random order, so that the
+    segments cross the fused kernel's 128-cell wave tiles at random places, as on an
+    intersection grid: every block of 4096 exchange cells holds 1024 atmosphere cells (341
+    runs of 3, 342 of 4 and 341 of 5, shuffled by a generator seeded with the block index).
+    Any rank builds its own range in O(size) without the global arrays (a global random-run
+    map is O(n_global) per rank: 80M cells at 8 x 10M).  Areas as PeriodicAtmosMap, weights =
+    area / sum of the atmosphere cell's areas (the last block truncated at n_global)."""
+    BLOCK = 4096
+    RUNS = 1024
+    COUNTS = (341, 342, 341)  # runs of 3, 4, 5 cells: 1024 runs, 4096 cells
+
+    def __init__(self, seed=20231015):
+        self.seed = seed
+        self._base = np.repeat(np.array([3, 4, 5]), self.COUNTS)
+
+    def _runs(self, b):
+        lengths = self._base.copy()
+        np.random.default_rng([self.seed, 11, int(b)]).shuffle(lengths)
+        return np.repeat(np.arange(self.RUNS, dtype=np.int64), lengths)  # run of every cell of the block
+
+    def _cells(self, lo, hi, n_global):
+        """global atmosphere index and weight of cells [lo, hi)"""
+        if hi <= lo:
+            return np.zeros(0, np.int64), np.zeros(0)
+        b0, b1 = lo // self.BLOCK, (hi - 1) // self.BLOCK
+        idx = np.concatenate([self._runs(b) + b * self.RUNS for b in range(b0, b1 + 1)])
+        x = np.arange(b0 * self.BLOCK, min((b1 + 1) * self.BLOCK, n_global), dtype=np.int64)
+        idx = idx[: x.size]
+        area = PeriodicAtmosMap.area(x)
+        first = idx[0]
+        tot = np.bincount(idx - first, weights=area)
+        w = area / tot[idx - first]
+        s = lo - b0 * self.BLOCK
+        return idx[s: s + (hi - lo)], w[s: s + (hi - lo)]
+
+    def local(self, offset, size, rank, nranks, n_global):
+        if size == 0:
+            return LocalAtmos(offset, 0, 0, 0, np.zeros(0, np.int32), np.zeros(0), -1, -1, max(nranks - 1, 0))
+        lo, hi = max(offset - 1, 0), min(offset + size + 1, n_global)  # one neighbour cell each side
+        gi, w = self._cells(lo, hi, n_global)
+        mine = slice(offset - lo, offset - lo + size)
+        g, wm = gi[mine], w[mine]
+        a0, a1 = int(g[0]), int(g[-1])
+        left = rank - 1 if (offset > 0 and int(gi[0]) == a0) else -1
+        right = rank if (offset + size < n_global and int(gi[-1]) == a1) else -1
+        return LocalAtmos(offset, size, a0, a1 - a0 + 1, np.ascontiguousarray(g - a0, dtype=np.int32),
+                          np.ascontiguousarray(wm), left, right, max(nranks - 1, 0))
+
+    def global_map(self, n_global):
+        idx, w = self._cells(0, n_global, n_global)
+        return AtmosMap(np.ascontiguousarray(idx, dtype=np.int32), np.ascontiguousarray(w),
+                        int(idx[-1]) + 1 if n_global else 0)
+
+
 @dataclass
 class ModelMap:
     """Exchange -> model (e.g. ocean) remap links, SCRIP style: 0-based src (exchange cell),

@@ -14,7 +14,7 @@ import numpy as np
 
 from .basic import PHASE_ALL, PHASE_NORMAL
 from .engine import Engine
-from .parallel import PeriodicAtmosMap, apple_range, local_atmos, synthetic_atmos_map
+from .parallel import BlockedRandomAtmosMap, PeriodicAtmosMap, apple_range
 from .synthetic import BASE_SEED, as_dtype, build_case, inputs_for_bench
 
 VARIANTS = ("CCLM", "MOM5", "RCO")
@@ -53,12 +53,12 @@ class Workload:
             data, case_dev = host, None
         self.caller_device = caller_device
         # periodic: runs of 3, 4, 5, 4 cells that never cross a 16-cell period (nor a wave
-        # tile); random: runs of 3..5 cells at random, so that segments cross wave tiles and
-        # the fused kernel hands carries on as on a real intersection grid
+        # tile); random: runs of 3..5 cells in random order (BlockedRandomAtmosMap), so that
+        # segments cross wave tiles as on a real intersection grid
         if not atmos:
             self.la = None
         elif atmos_map == "random":
-            self.la = local_atmos(synthetic_atmos_map(self.n_global), self.rank, self.world)
+            self.la = BlockedRandomAtmosMap().local(self.offset, self.n, self.rank, self.world, self.n_global)
         else:
             self.la = PeriodicAtmosMap().local(self.offset, self.n, self.rank, self.world, self.n_global)
         self.atmos_map = atmos_map

@@ -76,7 +76,7 @@ def test_config3_bench_path_10M(atmos_map):
 @pytest.mark.parametrize("atmos_map", ["random", "periodic"])
 def test_config4_40M_eight_shards(atmos_map):
     import torch
-    from fcx.parallel import PeriodicAtmosMap, synthetic_atmos_map
+    from fcx.parallel import BlockedRandomAtmosMap, PeriodicAtmosMap
 
     # 40M + 40 cells: shards of 5,000,005 cells, so the shard ends fall inside atmosphere cells
     # of the periodic map (16 exchange cells = 4 atmosphere cells) and the boundary exchange
@@ -94,7 +94,7 @@ def test_config4_40M_eight_shards(atmos_map):
         torch.cuda.synchronize()
         for wl in shards:
             assert float(wl.shared.abs().sum()) == 0.0
-        gmap = PeriodicAtmosMap().global_map(n_global) if atmos_map == "periodic" else synthetic_atmos_map(n_global)
+        gmap = (PeriodicAtmosMap() if atmos_map == "periodic" else BlockedRandomAtmosMap()).global_map(n_global)
         rng = np.random.default_rng(12)
         for i, v in enumerate(VARIANTS):
             fluxes = {name: np.empty(n_global) for name, _ in ATM_FIELDS}

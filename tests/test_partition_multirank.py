@@ -59,6 +59,33 @@ def test_local_views_agree_on_shared_boundaries(p):
     assert sum(v.size for v in views) == 50_001
 
 
+@pytest.mark.parametrize("cls", ["periodic", "blocked_random"])
+@pytest.mark.parametrize("p", [1, 2, 3, 8])
+def test_local_structured_maps_match_their_global_map(cls, p):
+    """The bench's locally built maps (PeriodicAtmosMap, BlockedRandomAtmosMap): every rank's
+    view built from its own range equals the slice of the global map (indices, weights,
+    boundary slots as local_atmos gives them); weights conservative; runs of 3..5 cells."""
+    from fcx.parallel import BlockedRandomAtmosMap, PeriodicAtmosMap
+
+    n = 50_003  # not a multiple of the 4096-cell blocks: a truncated last block
+    mk = PeriodicAtmosMap() if cls == "periodic" else BlockedRandomAtmosMap(seed=5)
+    g = mk.global_map(n)
+    assert np.all(np.diff(g.atmos_index) >= 0) and g.atmos_index[0] == 0
+    np.testing.assert_allclose(np.bincount(g.atmos_index, weights=g.weight), 1.0, rtol=1e-12)
+    lengths = np.bincount(g.atmos_index)
+    assert lengths[:-1].min() >= 3 and lengths.max() <= 5
+    for r in range(p):
+        off, size = apple_range(n, r, p)
+        v, w = mk.local(off, size, r, p, n), local_atmos(g, r, p)
+        assert (v.atmos_offset, v.n_atmos, v.left, v.right) == (w.atmos_offset, w.n_atmos, w.left, w.right)
+        np.testing.assert_array_equal(v.atmos_index, w.atmos_index)
+        np.testing.assert_array_equal(v.weight, w.weight)
+    if cls == "blocked_random":  # segments cross the kernel's 128-cell wave tiles
+        b = np.arange(128, n, 128)
+        cross = np.mean(g.atmos_index[b - 1] == g.atmos_index[b])
+        assert 0.6 < cross < 0.85, cross
+
+
 def _global_reference(n, amap):
     case = build_case("CCLM", n=n, T=1, bias=True, seed=777)
     out = oracle_lib.run_case(case, "c", current_step_time=3600)
