@@ -841,20 +841,54 @@ __global__ __launch_bounds__(64 * atmos_waves<C>(), RAVG ? FCX_RAVG_ATMOS_BLOCKS
       m[i] = __ballot(st[i]);
     }
     wave_sync();  // the wave's LDS products are visible to all its lanes
+#ifndef FCX_SEG_ROUNDS  // A/B: 0 = one pass per cell position i (the round-1 loop)
+#define FCX_SEG_ROUNDS 1
+#endif
+    if (FCX_SEG_ROUNDS) {
+      // Rounds of one segment start per lane: every lane with a start sums its segment and
+      // stores the six values in the same round, so a tile's atmosphere stores are six
+      // store instructions per round (one round when every run is >= C cells long, as on an
+      // intersection grid), not six per cell position of the lane.
+      uint32_t rem = 0;  // bit i: cell C*lane+i starts a segment not summed yet
 #pragma unroll
-    for (int i = 0; i < C; ++i) {
-      if (!st[i] || a[i] < 0) continue;
-      const int c = C * lane + i;
-      // next start after cell c: cell C*j+i' with j > l, or j == l and i' > i
-      int e_end = kT;
+      for (int i = 0; i < C; ++i)
+        if (st[i] && a[i] >= 0) rem |= 1u << i;
+      while (__ballot(rem != 0)) {
+        if (rem) {
+          const int i = __builtin_ctz(rem);
+          rem &= rem - 1;
+          int32_t ai = a[0];
 #pragma unroll
-      for (int q = 0; q < C; ++q) e_end = min(e_end, C * first_bit(m[q] & (q > i ? at_or_above : above)) + q);
-      const int end = min(e_end, kT);
-      double acc[kFusedFields];
+          for (int q = 1; q < C; ++q)
+            if (q == i) ai = a[q];
+          const int c = C * lane + i;
+          // next start after cell c: cell C*j+i' with j > l, or j == l and i' > i
+          int e_end = kT;
 #pragma unroll
-      for (int k = 0; k < kFusedFields; ++k) acc[k] = 0.0;
-      for (int e = c; e < end; ++e) add_cell(acc, e);
-      segment_done<R>(af, tile, a[i], acc, end == kT && next_a == a[i]);
+          for (int q = 0; q < C; ++q) e_end = min(e_end, C * first_bit(m[q] & (q > i ? at_or_above : above)) + q);
+          const int end = min(e_end, kT);
+          double acc[kFusedFields];
+#pragma unroll
+          for (int k = 0; k < kFusedFields; ++k) acc[k] = 0.0;
+          for (int e = c; e < end; ++e) add_cell(acc, e);
+          segment_done<R>(af, tile, ai, acc, end == kT && next_a == ai);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < C; ++i) {
+        if (!st[i] || a[i] < 0) continue;
+        const int c = C * lane + i;
+        int e_end = kT;
+#pragma unroll
+        for (int q = 0; q < C; ++q) e_end = min(e_end, C * first_bit(m[q] & (q > i ? at_or_above : above)) + q);
+        const int end = min(e_end, kT);
+        double acc[kFusedFields];
+#pragma unroll
+        for (int k = 0; k < kFusedFields; ++k) acc[k] = 0.0;
+        for (int e = c; e < end; ++e) add_cell(acc, e);
+        segment_done<R>(af, tile, a[i], acc, end == kT && next_a == a[i]);
+      }
     }
     // without the hand-off: the number of head cells (continuing the previous tile's
     // segment) for atmos_fixup_kernel; 0 when the tile starts a segment
