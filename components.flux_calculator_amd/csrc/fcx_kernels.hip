@@ -665,7 +665,7 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb) {
 #endif
 template <class R>
 __device__ __forceinline__ void segment_done(const AtmosFused &af, int64_t tile, int32_t a, const double *acc,
-                                             bool cont) {
+                                             bool cont, bool nt_line = false) {
   if (cont) {
 #pragma unroll
     for (int k = 0; k < kFusedFields; ++k) {
@@ -691,14 +691,20 @@ __device__ __forceinline__ void segment_done(const AtmosFused &af, int64_t tile,
 #define FCX_DBG_ATM_NOSTORE 0
 #endif
   if (FCX_DBG_ATM_NOSTORE) return;
-#ifndef FCX_ATM_NT_STORE  // A/B: non-temporal atmosphere stores
-#define FCX_ATM_NT_STORE 0
+// Non-temporal atmosphere-output stores: 3 (default) for fp64 outputs, 1 all, 0 none, 2 only
+// the lines a tile owns whole.  Since the segment sums run in rounds, a round writes the
+// tile's values of a field with one instruction, and for fp64 outputs NT stores gained
+// 3.4-4.4 % per step (periodic / random map); fp32 outputs lost 7 % with them
+// (profiles/r02/nt_atm_ab/; round 1, with one store instruction per cell position, all-NT
+// had lost 6.8 %).
+#ifndef FCX_ATM_NT_STORE
+#define FCX_ATM_NT_STORE 3
 #endif
 #pragma unroll
   for (int k = 0; k < kFusedFields; ++k) {
     if (!af.out[k]) continue;
     R *o = reinterpret_cast<R *>(af.out[k]) + tiled(a, af.out_tpad);
-    if (FCX_ATM_NT_STORE)
+    if (FCX_ATM_NT_STORE == 1 || (FCX_ATM_NT_STORE == 2 && nt_line) || (FCX_ATM_NT_STORE == 3 && sizeof(R) == 8))
       __builtin_nontemporal_store((R)acc[k], o);
     else
       *o = (R)acc[k];
@@ -849,6 +855,10 @@ __global__ __launch_bounds__(64 * atmos_waves<C>(), RAVG ? FCX_RAVG_ATMOS_BLOCKS
       // stores the six values in the same round, so a tile's atmosphere stores are six
       // store instructions per round (one round when every run is >= C cells long, as on an
       // intersection grid), not six per cell position of the lane.
+      // atmosphere cells of the tile's first and last cell: the output lines strictly between
+      // theirs hold only values of segments that start in this tile (FCX_ATM_NT_STORE 2)
+      const int32_t a_lo = __shfl(a[0], 0), a_hi = __shfl(a[C - 1], 63);
+      constexpr int kLineCells = 128 / (int)sizeof(R);
       uint32_t rem = 0;  // bit i: cell C*lane+i starts a segment not summed yet
 #pragma unroll
       for (int i = 0; i < C; ++i)
@@ -871,7 +881,8 @@ __global__ __launch_bounds__(64 * atmos_waves<C>(), RAVG ? FCX_RAVG_ATMOS_BLOCKS
 #pragma unroll
           for (int k = 0; k < kFusedFields; ++k) acc[k] = 0.0;
           for (int e = c; e < end; ++e) add_cell(acc, e);
-          segment_done<R>(af, tile, ai, acc, end == kT && next_a == ai);
+          const bool own = a_hi >= 0 && ai / kLineCells > a_lo / kLineCells && ai / kLineCells < a_hi / kLineCells;
+          segment_done<R>(af, tile, ai, acc, end == kT && next_a == ai, own);
         }
       }
     } else {
