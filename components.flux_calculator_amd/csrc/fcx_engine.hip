@@ -134,8 +134,7 @@ struct fcx_engine {
   int32_t atm_maxseg = 0;
   double *d_atm_carry = nullptr;
   uint32_t *d_atm_flag = nullptr;  // [tiles] hand-off flags (epoch tags)
-  int32_t *d_atm_head = nullptr;   // [tiles] head cells of every tile (fix-up kernel)
-  double *d_atm_headp = nullptr;   // [tiles][kHeadCells][kFusedFields] their products
+  double *d_atm_xrec = nullptr;    // [tiles][kXRec] crossing records (fix-up kernel)
   int64_t atm_crossings = 0;       // 128-cell tile boundaries inside a segment of the map
   bool carry_handoff = false;      // FCX_OPT_CARRY_HANDOFF: carries handed over inside the launch
   uint32_t *h_atm_err = nullptr;   // mapped host word: a hand-off wait gave up
@@ -301,8 +300,7 @@ extern "C" int fcx_destroy(fcx_engine *e) {
   (void)hipFree(e->d_atm_idx);
   (void)hipFree(e->d_atm_carry);
   (void)hipFree(e->d_atm_flag);
-  (void)hipFree(e->d_atm_head);
-  (void)hipFree(e->d_atm_headp);
+  (void)hipFree(e->d_atm_xrec);
   if (e->h_atm_err) (void)hipHostFree(e->h_atm_err);
   (void)hipFree(e->d_atm_col);
   (void)hipFree(e->d_atm_w);
@@ -639,8 +637,7 @@ static void plan_fused_atmos(fcx_engine *e, Plan &pl, uint32_t stages, int phase
   af.w = e->d_atm_w;
   af.carry = e->d_atm_carry;
   af.flag = e->d_atm_flag;
-  af.head = e->d_atm_head;
-  af.headp = e->d_atm_headp;
+  af.xrec = e->d_atm_xrec;
   if (e->h_atm_err && hipHostGetDevicePointer((void **)&af.err, e->h_atm_err, 0) != hipSuccess) af.err = nullptr;
   af.n_atmos = e->n_atmos;
   af.shared = e->atm_shared;
@@ -1462,8 +1459,7 @@ extern "C" int fcx_commit(fcx_engine *e) {
       HIP_TRY(hipMalloc(&e->d_atm_carry, (size_t)std::max<int64_t>(tiles, 1) * kFusedFields * sizeof(double)));
       HIP_TRY(hipMalloc(&e->d_atm_flag, (size_t)std::max<int64_t>(tiles, 1) * sizeof(uint32_t)));
       HIP_TRY(hipMemset(e->d_atm_flag, 0, (size_t)std::max<int64_t>(tiles, 1) * sizeof(uint32_t)));
-      HIP_TRY(hipMalloc(&e->d_atm_head, (size_t)std::max<int64_t>(tiles, 1) * sizeof(int32_t)));
-      HIP_TRY(hipMalloc(&e->d_atm_headp, (size_t)std::max<int64_t>(tiles, 1) * kHeadCells * kFusedFields * sizeof(double)));
+      HIP_TRY(hipMalloc(&e->d_atm_xrec, (size_t)std::max<int64_t>(tiles, 1) * kXRec * sizeof(double)));
       // tile boundaries a segment runs across: none (a map whose runs never cross a wave
       // tile) means no fix-up launch at all
       e->atm_crossings = 0;

@@ -158,7 +158,8 @@ int launch_pack_records(const AtmosArgs &a, int64_t n, bool aligned16, bool nont
 // launch: the carry is published with write-through stores and flag[tile] = epoch) or by
 // atmos_fixup_kernel after the launch (launches with a grid-stride cap).
 constexpr int kFusedFields = 6;
-constexpr int kHeadCells = 16;  // head products kept per tile for the fix-up (longer heads re-read)
+constexpr int kRecHead = 4;     // head products kept per crossing record (longer heads: recomputed)
+constexpr int kXRec = 32;       // doubles per crossing record (256 B, two lines)
 constexpr int kTile = 128;  // cells per wave iteration (64 lanes x 2)
 struct AtmosFused {
   const int32_t *idx;  // local atmosphere cell of every exchange cell (non-decreasing)
@@ -168,10 +169,10 @@ struct AtmosFused {
   double *carry;       // [n_tiles][kFusedFields]
   uint32_t *flag;      // [n_tiles]: epoch of the run whose carry[tile] is published
   uint32_t *err;       // set when a hand-off wait gave up (never in a correct run)
-  int32_t *head;       // [n_tiles]: cells at the start of the tile that continue the previous
-                       // tile's segment (written when handoff == 0; atmos_fixup_kernel)
-  double *headp;       // [n_tiles][kHeadCells][kFusedFields]: the products w * x of those
-                       // cells (the first kHeadCells of them), as the launch formed them
+  double *xrec;        // [n_tiles][kXRec] crossing records (handoff == 0, atmos_fixup_kernel):
+                       // record t = the carry of tile t-1's last segment (doubles 0..5), the
+                       // products w * x of tile t's first kRecHead head cells (6..29, cell-major)
+                       // and {head cells, their atmosphere cell} of tile t (int2 at double 30)
   uint32_t epoch;      // this run's tag (never 0); the flags start at 0
   int32_t handoff;     // 1: carries handed to the next tile's wave inside the launch
   int64_t n_atmos;

@@ -673,7 +673,7 @@ __device__ __forceinline__ void segment_done(const AtmosFused &af, int64_t tile,
       if (af.handoff)
         __hip_atomic_store(af.carry + tile * kFusedFields + k, acc[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       else
-        af.carry[tile * kFusedFields + k] = acc[k];
+        af.xrec[(tile + 1) * kXRec + k] = acc[k];  // the next tile's crossing record
     }
     if (af.handoff) {
       if (FCX_HANDOFF_ACQREL) {
@@ -911,11 +911,12 @@ __global__ __launch_bounds__(64 * atmos_waves<C>(), RAVG ? FCX_RAVG_ATMOS_BLOCKS
 #define FCX_DBG_NO_HEAD 0
 #endif
       if (FCX_DBG_NO_HEAD >= 2) head = 0;
-      if (lane == 0 && FCX_DBG_NO_HEAD < 2) af.head[tile] = head;
+      double *xr0 = af.xrec + tile * kXRec;
+      if (lane == 0 && FCX_DBG_NO_HEAD < 2) *reinterpret_cast<int2 *>(xr0 + 30) = int2{head, a[0]};
       if (FCX_DBG_NO_HEAD) head = 0;
-      // the products of the first kHeadCells head cells, one lane per cell, for the fix-up
-      if (lane < min(head, kHeadCells)) {
-        double *hp = af.headp + (tile * kHeadCells + lane) * kFusedFields;
+      // the products of the first kRecHead head cells, one lane per cell, 16-B stores
+      if (lane < min(head, kRecHead)) {
+        double hp[kFusedFields];
         if constexpr (kXF) {
           const float *xr = reinterpret_cast<const float *>(wp);
           const double we = wp[xrows_doubles<C>() + lds_slot(lane)];
@@ -925,6 +926,9 @@ __global__ __launch_bounds__(64 * atmos_waves<C>(), RAVG ? FCX_RAVG_ATMOS_BLOCKS
 #pragma unroll
           for (int k = 0; k < kFusedFields; ++k) hp[k] = wp[k * kR + lds_slot(lane)];
         }
+#pragma unroll
+        for (int q = 0; q < kFusedFields / 2; ++q)
+          reinterpret_cast<d2 *>(xr0 + kFusedFields + lane * kFusedFields)[q] = d2{hp[2 * q], hp[2 * q + 1]};
       }
     }
     // hand-off: the segment the previous tile carried into this one is continued here, from
@@ -943,13 +947,12 @@ __global__ __launch_bounds__(64 * atmos_waves<C>(), RAVG ? FCX_RAVG_ATMOS_BLOCKS
 }
 
 // Segments that straddle a tile boundary (the default, FCX_OPT_CARRY_HANDOFF = 0): the
-// launch leaves the prefix sum of a tile's last segment in carry[tile] and the number of
-// head cells of every tile (cells that continue the previous tile's segment) in head[tile];
-// this kernel continues each carry over the next tile's head cells, one thread per (tile,
-// field), in link order: the same bits as the in-launch sum.  The launch also leaves the
-// products of the first kHeadCells head cells of every tile (headp, a few dense bytes per
-// tile); the cells of a longer head are recomputed from the stored fluxes with the kernel's
-// own operation (w * x, fp32 fluxes widened).
+// launch leaves, in the crossing record of every tile t, the prefix sum of tile t-1's last
+// segment, the number of head cells of tile t (cells that continue that segment) with their
+// atmosphere cell, and the products of the first kRecHead of them; this kernel continues each
+// carry over the head cells, one thread per (tile, field), in link order: the same bits as
+// the in-launch sum.  Cells of a longer head are recomputed from the stored fluxes with the
+// kernel's own operation (w * x, fp32 fluxes widened).
 // Segments are at most half a tile (the fused path's rule), so a carry never spans a tile.
 template <class R, int kT>
 __global__ __launch_bounds__(256) void atmos_fixup_kernel(const AtmosFused af, int64_t n_tiles) {
@@ -957,23 +960,23 @@ __global__ __launch_bounds__(256) void atmos_fixup_kernel(const AtmosFused af, i
   const int64_t t = 1 + i / kFusedFields;
   const int k = (int)(i % kFusedFields);
   if (t >= n_tiles || !af.out[k]) return;
-  // every load of the common case (heads of up to 4 cells) issued before the head count is
-  // known: one memory round trip instead of one per cell
+  // one crossing record (two lines) holds everything of the common case: every load issued
+  // before the head count is known, one memory round trip
   const int64_t x0 = t * kT;
-  const double *hp = af.headp + t * kHeadCells * kFusedFields + k;
-  const int h = af.head[t];
-  const int32_t a = af.idx[x0];
-  double acc = af.carry[(t - 1) * kFusedFields + k];
-  double p[4];
+  const double *rec = af.xrec + t * kXRec;
+  const int2 ha = *reinterpret_cast<const int2 *>(rec + 30);
+  double acc = rec[k];
+  double p[kRecHead];
 #pragma unroll
-  for (int e = 0; e < 4; ++e) p[e] = hp[e * kFusedFields];
+  for (int e = 0; e < kRecHead; ++e) p[e] = rec[kFusedFields + e * kFusedFields + k];
+  const int h = ha.x;
+  const int32_t a = ha.y;
   if (h == 0) return;
 #pragma unroll
-  for (int e = 0; e < 4; ++e)
+  for (int e = 0; e < kRecHead; ++e)
     if (e < h) acc = acc + p[e];
-  for (int e = 4; e < min(h, kHeadCells); ++e) acc = acc + hp[e * kFusedFields];
   const R *xk = reinterpret_cast<const R *>(af.x[k]);
-  for (int e = kHeadCells; e < h; ++e) acc = acc + af.w[x0 + e] * (double)xk[tiled(x0 + e, af.tpad)];
+  for (int e = kRecHead; e < h; ++e) acc = acc + af.w[x0 + e] * (double)xk[tiled(x0 + e, af.tpad)];
   reinterpret_cast<R *>(af.out[k])[tiled(a, af.out_tpad)] = (R)acc;
   if (a == 0 && af.left >= 0) af.shared[(int64_t)af.left * af.stride + af.scol[k]] = acc;
   if (a == af.n_atmos - 1 && af.right >= 0) af.shared[(int64_t)af.right * af.stride + af.scol[k]] = acc;
