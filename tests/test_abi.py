@@ -154,3 +154,27 @@ def test_set_precision_validates():
     assert lib.fcx_set_precision(h, 2) == 1
     assert lib.fcx_set_precision(h, _lib.FCX_PRECISION_F32) == 0
     lib.fcx_destroy(h)
+
+
+def test_remap_and_carry_options_before_commit():
+    """FCX_OPT_REMAP_PACK (13: 0 never, 1 always, 2 auto) and FCX_OPT_CARRY_HANDOFF (14) are
+    validated without a GPU; fcx_remap_info is only answered after fcx_commit."""
+    lib = _lib.load()
+    h = ctypes.c_void_p()
+    gs = (ctypes.c_int32 * 3)(16, 16, 16)
+    _lib.check(lib.fcx_create(0, 1, gs, ctypes.byref(h)))
+    for v in (0, 1, 2):
+        _lib.check(lib.fcx_set_option(h, 13, v))
+    assert lib.fcx_set_option(h, 13, 3) == 1  # FCX_E_ARG
+    _lib.check(lib.fcx_set_option(h, 14, 1))
+    _lib.check(lib.fcx_set_option(h, 14, 0))
+    src = np.arange(16, dtype=np.int32)
+    dst = src % 4
+    w = np.ones(16)
+    rid = ctypes.c_int32()
+    _lib.check(lib.fcx_add_remap(h, 4, 16, src.ctypes.data, dst.ctypes.data, w.ctypes.data, ctypes.byref(rid)))
+    sc, pk = ctypes.c_double(), ctypes.c_int32()
+    assert lib.fcx_remap_info(h, rid.value, ctypes.byref(sc), ctypes.byref(pk)) == 2  # FCX_E_STATE
+    assert lib.fcx_add_remap(h, 4, 1, src.ctypes.data, (dst + 4).ctypes.data, w.ctypes.data,
+                             ctypes.byref(rid)) == 1  # a link outside the target grid
+    lib.fcx_destroy(h)
