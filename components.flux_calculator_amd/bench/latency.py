@@ -107,6 +107,31 @@ def main():
     for e in engines:
         e.close()
 
+    # ---- device-resident with the fused exchange -> atmosphere accumulation (6 fluxes), on
+    # the periodic map (no segment crosses a wave tile) and the random-run map, carries
+    # completed by the fix-up launch (default) or handed over inside the launch
+    from fcx.parallel import BlockedRandomAtmosMap, PeriodicAtmosMap
+    atm_fields = (("MEVA", 1), ("HLAT", 1), ("HSEN", 1), ("RBBR", 1), ("UMOM", 2), ("VMOM", 3))
+    acc = {}
+    for mname, mk in (("periodic", PeriodicAtmosMap()), ("random", BlockedRandomAtmosMap())):
+        la = mk.local(0, n, 0, 1, n)
+        for handoff in (0, 1):
+            engs = []
+            for v in VARIANTS:
+                c = build_case(v, n=n, T=1, bias=bool(a.bias), device="cuda:0", data=data)
+                outs = {k: torch.empty(la.n_atmos, dtype=torch.float64, device="cuda:0") for k, _ in atm_fields}
+                engs.append(Engine(c.lf, 1, c.methods, corrections=c.corrections, stream=stream.cuda_stream,
+                                   atmos={"local": la, "fields": [(2, 1, g, k, outs[k]) for k, g in atm_fields]},
+                                   options={"timing": 0, "carry_handoff": handoff}))
+
+            def step_atm(k, engs=engs):
+                for e in engs:
+                    e.run(PHASE_ALL, 0)
+            acc[f"{mname}_{'handoff' if handoff else 'fixup'}"] = round(timed(step_atm, a.steps), 2)
+            for e in engs:
+                e.close()
+    out["device"]["us_per_step_with_atmos_accumulation"] = acc
+
     # ---- host-bound: fcx_step per variant (upload, run, download, synchronise)
     # host_mirrors: caller heap arrays, device mirrors (caller heap arrays always take them);
     # host_library_arrays: arrays from fcx_host_malloc, used in place by default (auto
