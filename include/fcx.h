@@ -132,11 +132,11 @@ int fcx_run(fcx_engine *e, int phase, int32_t current_step_time); /* device comp
 int fcx_download(fcx_engine *e, int phase); /* D2H of host-bound outputs of the phase */
 /* the three above; with host-bound fields pipelined over cell chunks (FCX_OPT_PIPELINE_CHUNKS) */
 int fcx_step(fcx_engine *e, int phase, int32_t current_step_time);
-/* waits for the engine's stream.  A fused accumulation whose in-launch carry hand-off timed
- * out since the last check (a producer wave that was not resident, e.g. another process
- * holding the GPU) is recomputed here by the separate accumulation kernel (bit-identical
- * results, host copies refreshed) and counted (fcx_handoff_recoveries); fcx_step does the
- * same. */
+/* waits for the engine's stream.  With FCX_OPT_CARRY_HANDOFF = 1 (not the default): a fused
+ * accumulation whose in-launch carry hand-off timed out since the last check (a producer
+ * wave that was not resident, e.g. another process holding the GPU) is recomputed here by
+ * the separate accumulation kernel (bit-identical results, host copies refreshed) and
+ * counted (fcx_handoff_recoveries); fcx_step does the same. */
 int fcx_synchronize(fcx_engine *e);
 
 /* ---- per call: the reference subroutines one by one (exact drop-in semantics; each
