@@ -667,14 +667,16 @@ template <class R>
 __device__ __forceinline__ void segment_done(const AtmosFused &af, int64_t tile, int32_t a, const double *acc,
                                              bool cont, bool nt_line = false) {
   if (cont) {
+    if (!af.handoff) {  // the next tile's crossing record: the six prefix sums, 16-B stores
 #pragma unroll
-    for (int k = 0; k < kFusedFields; ++k) {
-      if (!af.out[k]) continue;
-      if (af.handoff)
-        __hip_atomic_store(af.carry + tile * kFusedFields + k, acc[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      else
-        af.xrec[(tile + 1) * kXRec + k] = acc[k];  // the next tile's crossing record
+      for (int q = 0; q < kFusedFields / 2; ++q)
+        reinterpret_cast<d2 *>(af.xrec + (tile + 1) * kXRec)[q] = d2{acc[2 * q], acc[2 * q + 1]};
+      return;
     }
+#pragma unroll
+    for (int k = 0; k < kFusedFields; ++k)
+      if (af.out[k])
+        __hip_atomic_store(af.carry + tile * kFusedFields + k, acc[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (af.handoff) {
       if (FCX_HANDOFF_ACQREL) {
         __hip_atomic_store(af.flag + tile, af.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
@@ -977,7 +979,13 @@ __global__ __launch_bounds__(256) void atmos_fixup_kernel(const AtmosFused af, i
     if (e < h) acc = acc + p[e];
   const R *xk = reinterpret_cast<const R *>(af.x[k]);
   for (int e = kRecHead; e < h; ++e) acc = acc + af.w[x0 + e] * (double)xk[tiled(x0 + e, af.tpad)];
-  reinterpret_cast<R *>(af.out[k])[tiled(a, af.out_tpad)] = (R)acc;
+#ifndef FCX_FIXUP_NT  // A/B: non-temporal fix-up stores
+#define FCX_FIXUP_NT 0
+#endif
+  if (FCX_FIXUP_NT)
+    __builtin_nontemporal_store((R)acc, reinterpret_cast<R *>(af.out[k]) + tiled(a, af.out_tpad));
+  else
+    reinterpret_cast<R *>(af.out[k])[tiled(a, af.out_tpad)] = (R)acc;
   if (a == 0 && af.left >= 0) af.shared[(int64_t)af.left * af.stride + af.scol[k]] = acc;
   if (a == af.n_atmos - 1 && af.right >= 0) af.shared[(int64_t)af.right * af.stride + af.scol[k]] = acc;
 }
