@@ -152,11 +152,12 @@ int launch_pack_records(const AtmosArgs &a, int64_t n, bool aligned16, bool nont
 
 // Exchange -> atmosphere accumulation fused into the T=1 cells kernel.  The six fluxes it
 // can take from registers, in this order: MEVA HLAT HSEN RBBR UMOM VMOM (out[k] nullptr =
-// not accumulated).  Every 128-cell wave tile sums the segments that start in it;
-// a segment running past the tile end leaves its prefix sum in carry[tile][k], continued
-// over the next tile's cells in link order either by the wave of that tile (hand-off in the
-// launch: the carry is published with write-through stores and flag[tile] = epoch) or by
-// atmos_fixup_kernel after the launch (launches with a grid-stride cap).
+// not accumulated).  Every 128-cell wave tile sums the segments that start in it; a
+// segment running past the tile end leaves its prefix sum for the next tile, whose head
+// cells continue it in link order: by default in the next tile's crossing record, which
+// atmos_fixup_kernel completes after the launch (no wave waits on another); with
+// FCX_OPT_CARRY_HANDOFF in carry[tile][k], published with write-through stores and
+// flag[tile] = epoch for the wave of the next tile inside the launch.
 constexpr int kFusedFields = 6;
 constexpr int kRecHead = 4;     // head products kept per crossing record (longer heads: recomputed)
 constexpr int kXRec = 32;       // doubles per crossing record (256 B, two lines)
@@ -166,13 +167,14 @@ struct AtmosFused {
   const double *w;
   double *out[kFusedFields];
   const double *x[kFusedFields];  // the stored outputs (read by the fix-up only)
-  double *carry;       // [n_tiles][kFusedFields]
+  double *carry;       // [n_tiles][kFusedFields] (hand-off only)
   uint32_t *flag;      // [n_tiles]: epoch of the run whose carry[tile] is published
   uint32_t *err;       // set when a hand-off wait gave up (never in a correct run)
   double *xrec;        // [n_tiles][kXRec] crossing records (handoff == 0, atmos_fixup_kernel):
                        // record t = the carry of tile t-1's last segment (doubles 0..5), the
                        // products w * x of tile t's first kRecHead head cells (6..29, cell-major)
-                       // and {head cells, their atmosphere cell} of tile t (int2 at double 30)
+                       // and {head cells, their atmosphere cell} of tile t (int2 at double 30);
+                       // fp32 engines index the records by their 256-cell tiles
   uint32_t epoch;      // this run's tag (never 0); the flags start at 0
   int32_t handoff;     // 1: carries handed to the next tile's wave inside the launch
   int64_t n_atmos;
