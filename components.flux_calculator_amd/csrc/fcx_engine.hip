@@ -638,6 +638,7 @@ static void plan_fused_atmos(fcx_engine *e, Plan &pl, uint32_t stages, int phase
   af.carry = e->d_atm_carry;
   af.flag = e->d_atm_flag;
   af.xrec = e->d_atm_xrec;
+  af.xrec_on = e->atm_crossings > 0;
   if (e->h_atm_err && hipHostGetDevicePointer((void **)&af.err, e->h_atm_err, 0) != hipSuccess) af.err = nullptr;
   af.n_atmos = e->n_atmos;
   af.shared = e->atm_shared;

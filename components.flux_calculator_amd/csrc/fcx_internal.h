@@ -175,6 +175,7 @@ struct AtmosFused {
                        // products w * x of tile t's first kRecHead head cells (6..29, cell-major)
                        // and {head cells, their atmosphere cell} of tile t (int2 at double 30);
                        // fp32 engines index the records by their 256-cell tiles
+  int32_t xrec_on;     // some segment crosses a tile boundary: the launch fills the records
   uint32_t epoch;      // this run's tag (never 0); the flags start at 0
   int32_t handoff;     // 1: carries handed to the next tile's wave inside the launch
   int64_t n_atmos;

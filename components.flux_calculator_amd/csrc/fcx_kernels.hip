@@ -905,7 +905,7 @@ __global__ __launch_bounds__(64 * atmos_waves<C>(), RAVG ? FCX_RAVG_ATMOS_BLOCKS
     }
     // without the hand-off: the number of head cells (continuing the previous tile's
     // segment) for atmos_fixup_kernel; 0 when the tile starts a segment
-    if (!af.handoff) {
+    if (!af.handoff && af.xrec_on) {  // (a map whose segments never cross a tile needs no records)
       int head = kT;
 #pragma unroll
       for (int q = 0; q < C; ++q) head = min(head, C * first_bit(m[q]) + q);
