@@ -368,13 +368,31 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
     }                                                                                  \
   }
 #define HOLD(var, grp, member) HOLDX(var, grp, member, false)
-#define HOLDA(var, grp, member) HOLDX(var, grp, member, true)
+// FCX_HOLD_MASK (A/B): which atmosphere-side inputs are held (bit 0 PSUR, 1 PATM, 2 QATM,
+// 3 TATM, 4 UATM, 5 VATM, 6 AMOI, 7 AMOM); the others are reloaded per type
+#ifndef FCX_HOLD_MASK
+#define FCX_HOLD_MASK 0xff
+#endif
+#define HOLDA(var, grp, member, bit) HOLDX(var, grp, member, ((FCX_HOLD_MASK >> (bit)) & 1))
   constexpr bool kHoldAtm = !kReload || (TM == 0 && FCX_HOLD_SHARED);
+  constexpr bool kHoldAll = !kReload || (TM == 0 && FCX_HOLD_SHARED && (FCX_HOLD_MASK & 0xff) == 0xff);
+  constexpr bool kHoldWind = !kReload || (TM == 0 && FCX_HOLD_SHARED && (FCX_HOLD_MASK & 0x30) == 0x30);
 
   for (int s = 0; s < T; ++s) {
     if constexpr (kReload) {  // no bottom-side input of the previous type stays live
       ts = fi = cmoi = chea = cmom = Vec<C, R>{};
       if constexpr (!kHoldAtm) ps = pa = qa = ta = u = v = amoi = amom = vel = Vec<C, R>{};
+      if constexpr (kHoldAtm && !kHoldAll) {  // the atmosphere-side inputs not held (A/B)
+        if constexpr (!(FCX_HOLD_MASK & 1)) ps = Vec<C, R>{};
+        if constexpr (!(FCX_HOLD_MASK & 2)) pa = Vec<C, R>{};
+        if constexpr (!(FCX_HOLD_MASK & 4)) qa = Vec<C, R>{};
+        if constexpr (!(FCX_HOLD_MASK & 8)) ta = Vec<C, R>{};
+        if constexpr (!(FCX_HOLD_MASK & 16)) u = Vec<C, R>{};
+        if constexpr (!(FCX_HOLD_MASK & 32)) v = Vec<C, R>{};
+        if constexpr (!(FCX_HOLD_MASK & 64)) amoi = Vec<C, R>{};
+        if constexpr (!(FCX_HOLD_MASK & 128)) amom = Vec<C, R>{};
+        if constexpr (!kHoldWind) vel = Vec<C, R>{};
+      }
     }
     const TypeParams &tp = P->type[s];
     const TGridPtrs &g = tp.t;
@@ -390,20 +408,20 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
       Vec<C, R> qs = {}, me = {};
       HOLD(ts, t, tsur)
       HOLD(fi, t, fice)
-      HOLDA(ps, t, psur)
-      HOLDA(pa, t, patm)
-      HOLDA(qa, t, qatm)
-      HOLDA(ta, t, tatm)
-      const bool wind_new = !kHoldAtm ? (g.uatm || g.vatm) : ((g.uatm && g.uatm != h_u) || (g.vatm && g.vatm != h_v));
-      HOLDA(u, t, uatm)
-      HOLDA(v, t, vatm)
-      HOLDA(amoi, t, amoi)
+      HOLDA(ps, t, psur, 0)
+      HOLDA(pa, t, patm, 1)
+      HOLDA(qa, t, qatm, 2)
+      HOLDA(ta, t, tatm, 3)
+      const bool wind_new = !kHoldWind ? (g.uatm || g.vatm) : ((g.uatm && g.uatm != h_u) || (g.vatm && g.vatm != h_v));
+      HOLDA(u, t, uatm, 4)
+      HOLDA(v, t, vatm, 5)
+      HOLDA(amoi, t, amoi, 6)
       HOLD(cmoi, t, cmoi)
       HOLD(chea, t, chea)
       if (g.qsur_in) qs = LD(g.qsur_in, j0, nt);  // may be written by this pass: never held
       if (g.meva_in) me = LD(g.meva_in, j0, nt);
       if constexpr (MERGED) {
-        HOLDA(amom, uv[0], amom)
+        HOLDA(amom, uv[0], amom, 7)
         HOLD(cmom, uv[0], cmom)
       }
       if (wind_new) FOR_C vel.v[i] = wind(u.v[i], v.v[i]);
