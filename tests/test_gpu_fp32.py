@@ -197,7 +197,7 @@ def test_fp32_engine_rejects_fp64_outputs():
 
 # run lengths: 1..7 and 40..64 (the fp32 fused kernel, 256-cell wave tiles: segments within
 # a tile or crossing one boundary), 1..400 (longer than half a 128-cell tile: atmos_kernel)
-@pytest.mark.parametrize("lengths", [(1, 7), (40, 64), (1, 400)])
+@pytest.mark.parametrize("lengths", [(1, 5), (1, 7), (40, 64), (1, 400)])
 @pytest.mark.parametrize("mode", ["handoff", "fixup", "capped", "pipelined"])
 @pytest.mark.parametrize("variant", ["CCLM", "MOM5", "RCO"])
 def test_fp32_fused_accumulation(variant, mode, lengths):
@@ -209,7 +209,7 @@ def test_fp32_fused_accumulation(variant, mode, lengths):
     from fcx.parallel import local_atmos
     from test_gpu_multirank import random_run_map
 
-    n = 300_001 if mode == "pipelined" else 70_001
+    n = 300_001 if mode.endswith("pipelined") else 70_001
     case = build_case(variant, n=n, T=1, bias=True, seed=23)
     c32 = as_dtype(case, "float32")
     amap = random_run_map(n, lengths, seed=lengths[1] + 5)

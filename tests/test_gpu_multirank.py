@@ -82,7 +82,7 @@ def random_run_map(n, lengths, seed):
 # run lengths: 1..7 and 20..64 (the fused kernel: segments within a tile or crossing one
 # boundary; heads longer than the fix-up's kHeadCells = 16 kept products are recomputed);
 # 130..140 and 1..400 (longer than half a tile: the engine runs atmos_kernel instead)
-@pytest.mark.parametrize("lengths", [(1, 7), (20, 64), (130, 140), (1, 400)])
+@pytest.mark.parametrize("lengths", [(1, 5), (1, 7), (20, 64), (130, 140), (1, 400)])
 @pytest.mark.parametrize("mode", ["handoff", "fixup", "capped", "pipelined"])
 def test_fused_accumulation_long_segments(lengths, mode):
     """The accumulation with segments crossing 128-cell wave tiles: carries handed to the next
@@ -94,7 +94,7 @@ def test_fused_accumulation_long_segments(lengths, mode):
     from fcx.engine import Engine
     from fcx.parallel import local_atmos
 
-    n = 300_001 if mode == "pipelined" else 70_001
+    n = 300_001 if mode.endswith("pipelined") else 70_001
     case = build_case("CCLM", n=n, T=1, bias=True, seed=17)
     amap = random_run_map(n, lengths, seed=lengths[1])
     la = local_atmos(amap, 0, 1)
