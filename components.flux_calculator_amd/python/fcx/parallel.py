@@ -41,6 +41,21 @@ def task_range(task, mype):
     return int(hit[0]), int(hit.size)
 
 
+def task_ranges(task, nranks):
+    """Every rank's (offset, size, right_slot) from the `task` vector (io:77-107).
+
+    A rank may own no cells (io:101-104).  The boundary slot between two ranks is numbered
+    by the rank on its right minus one, so a rank's right slot is that of the next rank WITH
+    cells: an empty rank between two shards that share an atmosphere cell must not split
+    their partial sums into two slots."""
+    r = [task_range(task, m) for m in range(nranks)]
+    out = []
+    for m, (off, size) in enumerate(r):
+        nxt = next((k for k in range(m + 1, nranks) if r[k][1] > 0), None)
+        out.append((off, size, (nxt - 1) if nxt is not None else m))
+    return out
+
+
 @dataclass
 class AtmosMap:
     """Global exchange -> atmosphere map: atmos_index[x] non-decreasing, weight[x]."""
@@ -77,7 +92,9 @@ class LocalAtmos:
     n_boundaries: int
 
 
-def local_atmos(amap: AtmosMap, rank, nranks, offset=None, size=None):
+def local_atmos(amap: AtmosMap, rank, nranks, offset=None, size=None, right_slot=None):
+    """right_slot: the slot of the boundary after this rank's cells (default `rank`; with
+    empty ranks in between, task_ranges gives it)."""
     if offset is None:
         offset, size = apple_range(amap.atmos_index.shape[0], rank, nranks)
     gi = amap.atmos_index[offset: offset + size]
@@ -86,7 +103,8 @@ def local_atmos(amap: AtmosMap, rank, nranks, offset=None, size=None):
     a0, a1 = int(gi[0]), int(gi[-1])
     left = rank - 1 if (offset > 0 and amap.atmos_index[offset - 1] == a0) else -1
     end = offset + size
-    right = rank if (end < amap.atmos_index.shape[0] and amap.atmos_index[end] == a1) else -1
+    right_slot = rank if right_slot is None else right_slot
+    right = right_slot if (end < amap.atmos_index.shape[0] and amap.atmos_index[end] == a1) else -1
     if left >= 0 and right >= 0 and a0 == a1:
         raise ValueError(f"rank {rank}: its {size} cells lie inside one atmosphere cell shared "
                          "with both neighbours (shard smaller than an atmosphere cell)")

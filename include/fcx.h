@@ -187,7 +187,9 @@ int fcx_add_atmos_field(fcx_engine *e, int phase, int surface_type, int grid, in
                         double *out, int flags);
 /* shared: device buffer [n_boundaries][stride] (zero on entry, re-zeroed by finish); the
  * rank's first local atmosphere cell is boundary `left` (-1: not shared), its last one
- * boundary `right`; field f of the accumulation uses column f (f < stride) */
+ * boundary `right`; field f of the accumulation uses column f (f < stride).  Boundary m - 1
+ * is the one just before rank m's cells: left = rank - 1, right = (next rank with cells) - 1
+ * (a rank with an empty task, io:101-104, sits between two slots' owners without one) */
 int fcx_set_atmos_shared(fcx_engine *e, double *shared, int32_t n_boundaries, int32_t stride,
                          int32_t left, int32_t right);
 /* instead of fcx_set_atmos_shared: the engine allocates the [n_boundaries][fields] slots

@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 
 import oracle_lib
-from fcx.parallel import (apple_range, local_atmos, pack_boundaries, synthetic_atmos_map,
+from fcx.parallel import (apple_range, local_atmos, pack_boundaries, synthetic_atmos_map, task_ranges,
                           task_range, unpack_boundaries)
 from fcx.synthetic import build_case
 from parity import assert_parity, mixed_error
@@ -96,7 +96,7 @@ def _global_reference(n, amap):
     return case, out, fields
 
 
-def _rank_main(rank, world, port, n, q):
+def _rank_main(rank, world, port, n, q, task=None):
     import torch.distributed as dist
     import torch
 
@@ -104,7 +104,11 @@ def _rank_main(rank, world, port, n, q):
     try:
         amap = synthetic_atmos_map(n)
         full, _, _ = _global_reference(n, amap)
-        la = local_atmos(amap, rank, world)
+        if task is None:
+            la = local_atmos(amap, rank, world)
+        else:  # the exchange grid's task vector; a rank may own no cells
+            off, size, right_slot = task_ranges(task, world)[rank]
+            la = local_atmos(amap, rank, world, off, size, right_slot=right_slot)
         lo, hi = la.offset, la.offset + la.size
         # this rank's shard: the same inputs, cut to its APPLE range
         case = build_case("CCLM", n=la.size, T=1, bias=True, seed=777)
@@ -138,15 +142,25 @@ def _free_port():
     return port
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_sharded_step_with_one_allreduce_matches_single_process(world):
+def _empty_middle_task(n, amap):
+    """Task vector of 3 ranks: rank 1 owns no cells (io:101-104), and the cut between ranks 0
+    and 2 falls inside an atmosphere cell, so ranks 0 and 2 share it across the empty rank."""
+    k = next(i for i in range(n // 2, n) if amap.atmos_index[i - 1] == amap.atmos_index[i])
+    task = np.full(n, 2, np.int32)
+    task[:k] = 0
+    return task
+
+
+@pytest.mark.parametrize("world,empty_middle", [(2, False), (3, False), (3, True)])
+def test_sharded_step_with_one_allreduce_matches_single_process(world, empty_middle):
     import torch.multiprocessing as mp
 
     n = 30_011
+    task = _empty_middle_task(n, synthetic_atmos_map(n)) if empty_middle else None
     ctx = mp.get_context("spawn")
     q = ctx.SimpleQueue()
     port = _free_port()
-    procs = [ctx.Process(target=_rank_main, args=(r, world, port, n, q)) for r in range(world)]
+    procs = [ctx.Process(target=_rank_main, args=(r, world, port, n, q, task)) for r in range(world)]
     for p in procs:
         p.start()
     results = [q.get() for _ in range(world)]
