@@ -335,3 +335,43 @@ def test_atmos_accumulation_of_type0_averages(variant, T, fused):
     assert_parity({k: np.asarray(case.lf.field[k]) for k in case.outputs},
                   {k: ref[k] for k in case.outputs}, label=f"{variant} T{T}")
     eng.close()
+
+
+@pytest.mark.parametrize("fused", [True, False])
+def test_sharded_engines_empty_middle_rank(fused):
+    """Three shards from a task vector whose middle rank owns no cells (io:101-104), the cut
+    between ranks 0 and 2 inside an atmosphere cell: the empty rank's engine steps and takes
+    part in the slot sum, and the shared cell is completed through one slot
+    (fcx.parallel.task_ranges)."""
+    import torch
+    from fcx.parallel import task_ranges
+
+    n, world = 20_011, 3
+    full, amap, ref = reference(n, "MOM5")
+    k = next(i for i in range(n // 2, n) if amap.atmos_index[i - 1] == amap.atmos_index[i])
+    task = np.full(n, 2, np.int32)
+    task[:k] = 0
+    stride = len(FIELDS)
+    engines = []
+    for r, (off, size, right_slot) in enumerate(task_ranges(task, world)):
+        la = local_atmos(amap, r, world, off, size, right_slot=right_slot)
+        shared = torch.zeros((world - 1) * stride, dtype=torch.float64, device="cuda:0")
+        case = shard_case(full, off, off + size, "MOM5")
+        eng, outs = make_engine(case, la, shared, stride, fused=fused)
+        engines.append((la, shared, eng, outs))
+    assert engines[0][0].right == engines[2][0].left == 1 and engines[1][0].size == 0
+    for la, shared, eng, outs in engines:
+        eng.upload(PHASE_ALL)
+        eng.run(PHASE_ALL, 7200)
+        eng.synchronize()
+    total = sum(sh for _, sh, _, _ in engines)
+    for la, shared, eng, outs in engines:
+        shared.copy_(total)
+        eng.atmos_finish()
+        eng.synchronize()
+    got = {name: np.full(amap.n_atmos, np.nan) for name, _ in FIELDS}
+    for la, shared, eng, outs in engines:
+        for name, _ in FIELDS:
+            got[name][la.atmos_offset: la.atmos_offset + la.n_atmos] = outs[name].cpu().numpy()[: la.n_atmos]
+        eng.close()
+    assert_parity(got, ref, label="empty middle rank")
