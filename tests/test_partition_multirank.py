@@ -37,6 +37,15 @@ def test_task_vector_rule():
     assert task_range(task, 3) == (0, 0)  # empty task (io:101-104)
 
 
+def test_task_ranges_slot_rule():
+    """Right slot = (next rank with cells) - 1; empty ranks anywhere (io:101-104)."""
+    t = np.array([0, 0, 2, 2, 2, 4], np.int32)  # ranks 1 and 3 empty, 5 absent
+    assert task_ranges(t, 6) == [(0, 2, 1), (0, 0, 1), (2, 3, 3), (0, 0, 3), (5, 1, 4), (0, 0, 5)]
+    assert task_ranges(np.zeros(4, np.int32), 3) == [(0, 4, 0), (0, 0, 1), (0, 0, 2)]
+    # with every rank owning cells the rule is the APPLE one: right slot = rank
+    assert [r for _, _, r in task_ranges(np.repeat(np.arange(4), 3), 4)] == [0, 1, 2, 3]
+
+
 def test_synthetic_map_is_conservative_and_sorted():
     m = synthetic_atmos_map(100_003)
     assert np.all(np.diff(m.atmos_index) >= 0)
