@@ -80,9 +80,6 @@ def parse():
                         "(tile-blocked, FCX_OPT_TILED_LAYOUT) are uploaded once before the timed region")
     p.add_argument("--tiled", type=int, default=1, help="FCX_OPT_TILED_LAYOUT of the engines (A/B)")
     p.add_argument("--nontemporal", type=int, default=1, help="FCX_OPT_NONTEMPORAL of the engines (A/B)")
-    p.add_argument("--carry-handoff", type=int, default=0,
-                   help="FCX_OPT_CARRY_HANDOFF of the engines (A/B): 1 = carries across wave tiles handed "
-                        "over inside the launch instead of the fix-up kernel")
     p.add_argument("--precision", choices=("f64", "f32"), default="f64",
                    help="f32: the fp32 variant (config 5): fp32 cell pass with the accumulation fused in "
                         "(fp32 fluxes, fp64 weights, products and sums, fp32 outputs)")
@@ -290,8 +287,7 @@ def main():
 
     coll = comm if comm is not None else (TorchCollective() if world > 1 else None)
 
-    engine_options = {"tiled_layout": args.tiled, "nontemporal": args.nontemporal,
-                      "carry_handoff": args.carry_handoff}
+    engine_options = {"tiled_layout": args.tiled, "nontemporal": args.nontemporal}
     if args.max_blocks is not None:
         engine_options["max_blocks"] = args.max_blocks
     # this rank's APPLE range (decomp_def.F90:23-31): weak scaling (every rank owns args.cells

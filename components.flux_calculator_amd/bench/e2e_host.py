@@ -5,8 +5,9 @@ fused kernels, D2H of the outputs ("kernel-only and end-to-end wit
 reported separately"; 8f rank 1).  bench.py's `value` is the HBM-resident rate; this is the
 rate a host that hands over host buffers sees.
 
-Sweeps: pageable vs page-locked caller arrays (FCX_OPT_PIN_HOST) and sequential vs
-pipelined steps (FCX_OPT_PIPELINE_CHUNKS).  The ceiling is the host link: the same bytes as
+Sweeps: caller heap arrays through the engine's staging arena (FCX_OPT_HOST_STAGING, the
+default) or one runtime copy per array, library arrays (fcx_host_malloc: direct DMA or
+zero-copy), and sequential vs pipelined steps (FCX_OPT_PIPELINE_CHUNKS).  The ceiling is the host link: the same bytes as
 one pinned hipMemcpy per direction, measured here with torch, H2D and D2H concurrently.
 
   python components.flux_calculator_amd/bench/e2e_host.py [--cells N] [--steps K]
@@ -57,11 +58,12 @@ def link_ceiling(h2d_bytes, d2h_bytes, reps=5):
             "concurrent_s": t_both, "concurrent_GBps": (h2d_bytes + d2h_bytes) / t_both / 1e9}
 
 
-SWEEP = [("pageable, sequential", {"pin_host": 0, "pipeline_chunks": 1}),
-         ("pinned, sequential", {"pin_host": 1, "pipeline_chunks": 1}),
-         ("pinned, 4 chunks", {"pin_host": 1, "pipeline_chunks": 4}),
-         ("pinned, 8 chunks", {"pin_host": 1, "pipeline_chunks": 8}),
-         ("pinned, 16 chunks", {"pin_host": 1, "pipeline_chunks": 16}),
+SWEEP = [("heap, runtime copies, sequential", {"host_staging": 0, "pipeline_chunks": 1}),
+         ("heap, runtime copies, 8 chunks", {"host_staging": 0, "pipeline_chunks": 8}),
+         ("heap, staged, sequential", {"pipeline_chunks": 1}),
+         ("heap, staged, 4 chunks", {"pipeline_chunks": 4}),
+         ("heap, staged, 8 chunks", {"pipeline_chunks": 8}),   # the default transport
+         ("heap, staged, 16 chunks", {"pipeline_chunks": 16}),
          ("zero-copy", {"zero_copy": 1}),                       # arrays from fcx_host_malloc
          ("library arrays, 8 chunks", {"zero_copy": 0, "pipeline_chunks": 8})]
 LIBRARY_ARRAYS = ("zero-copy", "library arrays, 8 chunks")
@@ -88,7 +90,7 @@ def child(a):
         arena.adopt(case.lf)
     opts = {**dict(SWEEP)[a.only], "timing": 1}  # device_timeline_ms / kernel_ms below
     eng = Engine(case.lf, 1, case.methods, options=opts)
-    pinned = eng.pinned_bytes()
+    staging = eng.staging_bytes()
     eng.step(PHASE_ALL, 0)  # warm-up (first touch, plan, code objects)
     t = []
     for k in range(a.steps):
@@ -103,7 +105,7 @@ def child(a):
     eng.close()
     print(json.dumps({"ms_per_step": round(ms, 3), "Mcells_per_s": round(n / ms / 1e3, 1),
                       "device_timeline_ms": round(dev_ms, 3), "kernel_ms": round(kern_ms, 4),
-                      "pinned_MB": round(pinned / 1e6, 1)}))
+                      "staging_MB": round(staging / 1e6, 1)}))
 
 
 def main():

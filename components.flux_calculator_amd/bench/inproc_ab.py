@@ -94,7 +94,7 @@ def main():
                    device=0, stream=stream.cuda_stream,
                    atmos=({"local": la, "fields": [(PHASE_NORMAL, s0, g, name, o[name]) for name, g in FIELDS]}
                           if a.atmos and lname not in no_atmos else None),
-                   options={"atmos_in_run": 0, "timing": 0, "pin_host": 0, **extra_opts.get(lname, {})}, lib=lib)
+                   options={"atmos_in_run": 0, "timing": 0, "host_staging": 0, **extra_opts.get(lname, {})}, lib=lib)
             for c, o in zip(cases, outs)]
         if a.host:
             for e in engines[lname]:

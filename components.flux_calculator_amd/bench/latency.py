@@ -108,37 +108,39 @@ def main():
         e.close()
 
     # ---- device-resident with the fused exchange -> atmosphere accumulation (6 fluxes), on
-    # the periodic map (no segment crosses a wave tile) and the random-run map, carries
-    # completed by the fix-up launch (default) or handed over inside the launch
+    # the periodic map (no segment crosses a wave tile) and the random-run map (carries
+    # completed by the fix-up launch)
     from fcx.parallel import BlockedRandomAtmosMap, PeriodicAtmosMap
     atm_fields = (("MEVA", 1), ("HLAT", 1), ("HSEN", 1), ("RBBR", 1), ("UMOM", 2), ("VMOM", 3))
     acc = {}
     for mname, mk in (("periodic", PeriodicAtmosMap()), ("random", BlockedRandomAtmosMap())):
         la = mk.local(0, n, 0, 1, n)
-        for handoff in (0, 1):
-            engs = []
-            for v in VARIANTS:
-                c = build_case(v, n=n, T=1, bias=bool(a.bias), device="cuda:0", data=data)
-                outs = {k: torch.empty(la.n_atmos, dtype=torch.float64, device="cuda:0") for k, _ in atm_fields}
-                engs.append(Engine(c.lf, 1, c.methods, corrections=c.corrections, stream=stream.cuda_stream,
-                                   atmos={"local": la, "fields": [(2, 1, g, k, outs[k]) for k, g in atm_fields]},
-                                   options={"timing": 0, "carry_handoff": handoff}))
+        engs = []
+        for v in VARIANTS:
+            c = build_case(v, n=n, T=1, bias=bool(a.bias), device="cuda:0", data=data)
+            outs = {k: torch.empty(la.n_atmos, dtype=torch.float64, device="cuda:0") for k, _ in atm_fields}
+            engs.append(Engine(c.lf, 1, c.methods, corrections=c.corrections, stream=stream.cuda_stream,
+                               atmos={"local": la, "fields": [(2, 1, g, k, outs[k]) for k, g in atm_fields]},
+                               options={"timing": 0}))
 
-            def step_atm(k, engs=engs):
-                for e in engs:
-                    e.run(PHASE_ALL, 0)
-            acc[f"{mname}_{'handoff' if handoff else 'fixup'}"] = round(timed(step_atm, a.steps), 2)
+        def step_atm(k, engs=engs):
             for e in engs:
-                e.close()
+                e.run(PHASE_ALL, 0)
+        acc[mname] = round(timed(step_atm, a.steps), 2)
+        for e in engs:
+            e.close()
     out["device"]["us_per_step_with_atmos_accumulation"] = acc
 
     # ---- host-bound: fcx_step per variant (upload, run, download, synchronise)
-    # host_mirrors: caller heap arrays, device mirrors (caller heap arrays always take them);
+    # host_heap_staged: caller heap arrays (a Fortran host's ALLOCATEd fields) through the
+    # engine's staging arena (the default transport); host_heap_runtime_copies: the same with
+    # one runtime copy per array (FCX_OPT_HOST_STAGING=0, round 2's default);
     # host_library_arrays: arrays from fcx_host_malloc, used in place by default (auto
     # zero-copy); host_library_mirrors: the same arrays through mirrors (FCX_OPT_ZERO_COPY=0)
     from fcx.host_alloc import Arena
 
-    for mode, opts, lib_arrays in (("host_mirrors", {}, False),
+    for mode, opts, lib_arrays in (("host_heap_staged", {}, False),
+                                   ("host_heap_runtime_copies", {"host_staging": 0}, False),
                                    ("host_library_arrays", {}, True),
                                    ("host_library_mirrors", {"zero_copy": 0}, True)):
         hb = {}

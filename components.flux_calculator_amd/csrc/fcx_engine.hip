@@ -9,17 +9,22 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cctype>
+#include <chrono>
+#include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
 #include <set>
 #include <string>
+#include <thread>
 #include <vector>
 
-#include <unistd.h>
+#include <sched.h>
 
 #include "fcx_internal.h"
 
@@ -50,12 +55,42 @@ const char *kVarNames[kNumVars] = {
     "VATM", "U10M", "V10M", "CMOM", "CMOI", "CHEA", "QSUR", "HLAT", "HSEN", "MEVA", "MPRE", "MRAI",
     "MSNO", "RBBR", "RLWD", "RLWU", "RSID", "RSIU", "RSIN", "RSDD", "RSDR", "UMOM", "VMOM"};
 
+// Where a device mirror sits inside its pool, and so its image in the staging arena
+// (FCX_OPT_HOST_STAGING): pool `sp` of the engine's StagePools, byte offset `soff` from the
+// pool's base (tiled pools: the slot's offset in the first tile row).  sp < 0: the mirror is
+// fed by direct copies (fcx_host_malloc memory, or staging off).
+struct StageRef {
+  int sp = -1;
+  size_t soff = 0;
+};
+
 struct Buffer {
   double *host = nullptr;  // caller array (nullptr for device-bound)
   double *dev = nullptr;   // device memory (engine pool or caller's)
   int64_t n = 0;
   bool external = false;   // caller-owned device memory (or a host array used in place)
   bool in_place = false;   // a host array the kernels use through its mapped address
+  StageRef st;
+};
+
+// A device pool with host-bound mirrors and its page-locked host image: the same bytes at
+// the same offsets, so a contiguous run of mirrors is one DMA.  Tiled pools (the field
+// mirrors of FCX_OPT_TILED_LAYOUT, the tiled atmosphere outputs) are rows of `pitch` bytes
+// (one layout tile of every slot), slot k at k * slot bytes of every row; plain pools hold
+// each mirror contiguously.
+struct StagePool {
+  char *dev = nullptr, *host = nullptr;
+  size_t bytes = 0;
+  bool tiled = false;
+  size_t slot = 0, pitch = 0;  // tiled: bytes of one slot's tile, bytes of one row
+};
+
+// One host array <-> its mirror through the staging arena: `n` elements of `es` bytes.
+struct Xfer {
+  int sp;
+  size_t soff;
+  char *host;
+  int64_t n;
 };
 
 struct Csr {
@@ -83,9 +118,111 @@ struct Plan {
 
 int var0(int var) { return var - 1; }
 
-}  // namespace
+// Host copies of the staging arena (gather of the caller's arrays into it, scatter out of
+// it), spread over a process-wide pool of worker threads.  The calling thread takes part;
+// workers spin ~100 us after a batch before sleeping, so the scatter that follows a step's
+// gather finds them awake.  One batch at a time (engines on several host threads queue).
+struct CopyJob {
+  char *dst;
+  const char *src;
+  size_t bytes;
+};
 
-static void unpin_host_arrays(fcx_engine *e);
+class CopyPool {
+ public:
+  static CopyPool &get() {
+    static CopyPool *p = new CopyPool();  // never destroyed: workers may outlive static dtors
+    return *p;
+  }
+  // every job done when this returns; `threads` counts the caller
+  void run(const std::vector<CopyJob> &jobs, int threads) {
+    if (jobs.empty()) return;
+    std::lock_guard<std::mutex> one(batch_mu_);
+    const int helpers = std::max(0, std::min<int>({threads - 1, (int)jobs.size() - 1, 63}));
+    if (helpers == 0) {
+      for (const auto &j : jobs) std::memcpy(j.dst, j.src, j.bytes);
+      return;
+    }
+    grow(helpers);
+    jobs_ = jobs.data();
+    njobs_ = jobs.size();
+    next_.store(0, std::memory_order_relaxed);
+    busy_.store(helpers, std::memory_order_relaxed);
+    // one word: batch counter and the number of helpers, so a worker reads both at once
+    count_ += 1;
+    gen_.store((count_ << 8) | (uint64_t)helpers, std::memory_order_seq_cst);
+    if (sleepers_.load(std::memory_order_seq_cst) > 0) {
+      std::lock_guard<std::mutex> lk(mu_);
+      cv_.notify_all();
+    }
+    work();
+    while (busy_.load(std::memory_order_acquire) > 0) __builtin_ia32_pause();
+    jobs_ = nullptr;
+  }
+
+ private:
+  void work() {
+    for (size_t i; (i = next_.fetch_add(1, std::memory_order_relaxed)) < njobs_;)
+      std::memcpy(jobs_[i].dst, jobs_[i].src, jobs_[i].bytes);
+  }
+  void grow(int n) {
+    while ((int)workers_.size() < n) {
+      const int id = (int)workers_.size();
+      workers_.emplace_back([this, id] { loop(id); });
+      workers_.back().detach();
+    }
+  }
+  void loop(int id) {
+    uint64_t seen = gen_.load(std::memory_order_acquire);
+    for (;;) {
+      // spin for a while, then sleep until the next batch
+      auto t0 = std::chrono::steady_clock::now();
+      uint64_t g;
+      while ((g = gen_.load(std::memory_order_acquire)) == seen) {
+        __builtin_ia32_pause();
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(100)) {
+          std::unique_lock<std::mutex> lk(mu_);
+          sleepers_.fetch_add(1, std::memory_order_seq_cst);
+          cv_.wait(lk, [&] { return gen_.load(std::memory_order_seq_cst) != seen; });
+          sleepers_.fetch_sub(1, std::memory_order_seq_cst);
+          t0 = std::chrono::steady_clock::now();
+        }
+      }
+      seen = g;
+      if (id < (int)(g & 0xff)) {  // a helper of this batch: the caller waits for it
+        work();
+        busy_.fetch_sub(1, std::memory_order_acq_rel);
+      }
+    }
+  }
+  std::mutex batch_mu_, mu_;
+  std::condition_variable cv_;
+  std::vector<std::thread> workers_;
+  const CopyJob *jobs_ = nullptr;
+  size_t njobs_ = 0;
+  std::atomic<size_t> next_{0};
+  std::atomic<int> busy_{0}, sleepers_{0};
+  std::atomic<uint64_t> gen_{0};  // (batch counter << 8) | helpers of the batch
+  uint64_t count_ = 0;
+};
+
+// threads of the host copies: FCX_OPT_HOST_THREADS, else min(8, OMP_NUM_THREADS if set, else
+// the CPUs this process may run on) -- an MPI rank pinned to one core copies alone
+int default_host_threads() {
+  static const int n = [] {
+    int cpus = 1;
+    cpu_set_t set;
+    if (sched_getaffinity(0, sizeof set, &set) == 0) cpus = std::max(1, CPU_COUNT(&set));
+    if (const char *omp = std::getenv("OMP_NUM_THREADS")) {
+      const int t = std::atoi(omp);
+      if (t > 0) cpus = std::min(cpus, t);
+    }
+    return std::max(1, std::min(cpus, 8));
+  }();
+  return n;
+}
+
+}  // namespace
 
 struct fcx_engine {
   int device = 0;
@@ -124,6 +261,7 @@ struct fcx_engine {
     int phase, s, g, var;
     double *out_host = nullptr, *out_dev = nullptr;
     bool external = false;
+    StageRef st;
   };
   int64_t n_atmos = -1;
   std::vector<int32_t> atm_row, atm_col;
@@ -132,13 +270,8 @@ struct fcx_engine {
   int32_t *d_atm_row = nullptr, *d_atm_col = nullptr, *d_atm_idx = nullptr;
   std::vector<int32_t> atm_idx;
   int32_t atm_maxseg = 0;
-  double *d_atm_carry = nullptr;
-  uint32_t *d_atm_flag = nullptr;  // [tiles] hand-off flags (epoch tags)
   double *d_atm_xrec = nullptr;    // [tiles][kXRec] crossing records (fix-up kernel)
   int64_t atm_crossings = 0;       // 128-cell tile boundaries inside a segment of the map
-  bool carry_handoff = false;      // FCX_OPT_CARRY_HANDOFF: carries handed over inside the launch
-  uint32_t *h_atm_err = nullptr;   // mapped host word: a hand-off wait gave up
-  uint32_t atm_epoch = 0;          // tag of the current run's hand-offs
   double *d_atm_w = nullptr;
   std::vector<AtmosField> atm_fields;
   double *atm_shared = nullptr;
@@ -152,14 +285,12 @@ struct fcx_engine {
   int64_t atm_out_tpad = 0;  // tile-blocked atmosphere outputs (kernels: tiled(a, atm_out_tpad))
   bool atmos_in_run = true;
   bool atm_done_fused = false;  // the last fcx_run already accumulated the atmosphere fields
-  int last_phase = FCX_PHASE_ALL;     // phase of the last fused accumulation
-  int64_t handoff_recoveries = 0;     // fused accumulations recomputed after a hand-off timeout
-  bool test_handoff_timeout = false;  // FCX_OPT_TEST_HANDOFF_TIMEOUT
   // exchange -> model remaps (SCRIP links, CSR by destination in link order)
   struct RemapField {
     int phase, s, g, var;
     double *out_host = nullptr, *out_dev = nullptr;
     bool external = false;
+    StageRef st;
   };
   struct Remap {
     int64_t n_dst = 0, n_links = 0;
@@ -170,6 +301,7 @@ struct fcx_engine {
     double *d_w = nullptr;
     std::vector<RemapField> fields;
     void *pool = nullptr;
+    size_t pool_bytes = 0;
     // gather scatter of the map: distinct 64-B segments of a field array (8 fp64 cells) the
     // links of a 256-destination block touch, per link (sampled at commit).  About 0.3 on
     // the geometric and the 1-link synthetic maps, 0.66 on the shuffled 2-link map.
@@ -180,8 +312,8 @@ struct fcx_engine {
   void *d_rec = nullptr;     // remap records scratch (pack_records), shared by every remap launch
   size_t rec_bytes = 0;
   const Plan *rec_plan = nullptr;  // the whole-phase plan the current run launched (its records)
-  // host-bound steps: page-locked caller arrays and the H2D / compute / D2H pipeline
-  bool pin_host = false;  // FCX_OPT_PIN_HOST: opt-in
+  bool rec_written = false;        // the last flux launch wrote its plan's remap records
+  // host-bound steps: the H2D / compute / D2H pipeline
   int chunks = 8;                                   // fcx_step pipeline depth (1 = off)
   int64_t min_chunk = 256 * 1024;                   // cells per chunk at least (~2 MB/array)
   // kernels use the host arrays in place: 0 off, 1 on, 2 auto (default: grids below two
@@ -193,9 +325,17 @@ struct fcx_engine {
   // ev0/ev1 around every run (fcx_last_kernel_ms).  Off by default: on the 32K-cell grid the
   // two event records per run made the 3-variant step 41 us instead of 16.5 us
   bool timing = false;
-  std::vector<std::pair<char *, size_t>> pinned;    // hipHostRegister'ed page ranges
   hipStream_t s_in = nullptr, s_out = nullptr;      // copy streams of the pipeline
-  std::vector<hipEvent_t> ev_in, ev_comp;           // per chunk
+  std::vector<hipEvent_t> ev_in, ev_comp, ev_out;   // per chunk
+  // staging arena of caller heap arrays (FCX_OPT_HOST_STAGING): page-locked host images of
+  // the device pools that hold their mirrors, allocated at the first staged transfer
+  bool staging = true;
+  int host_threads = 0;                 // FCX_OPT_HOST_THREADS (0: default_host_threads)
+  std::vector<StagePool> spools;
+  std::vector<Xfer> pending_out;        // D2H into the arena whose scatter waits for the stream
+  hipEvent_t ev_stage_in = nullptr;     // the last H2D out of the arena
+  bool stage_in_live = false;
+  size_t pool_bytes = 0, tiled_bytes = 0, atm_pool_bytes = 0;  // device pool sizes
   // tile-blocked mirrors (FCX_OPT_TILED_LAYOUT): tpad = tile stride - kLayoutTile elements,
   // 0 when the field buffers are plain contiguous arrays
   bool tiled_opt = true;
@@ -213,6 +353,8 @@ struct fcx_engine {
     return b < 0 ? nullptr : bufs[b].dev;
   }
 };
+
+static void stage_free(fcx_engine *e);
 
 // ------------------------------------------------------------------ utilities
 
@@ -298,10 +440,7 @@ extern "C" int fcx_destroy(fcx_engine *e) {
   (void)hipFree(e->corr_dev);
   (void)hipFree(e->d_atm_row);
   (void)hipFree(e->d_atm_idx);
-  (void)hipFree(e->d_atm_carry);
-  (void)hipFree(e->d_atm_flag);
   (void)hipFree(e->d_atm_xrec);
-  if (e->h_atm_err) (void)hipHostFree(e->h_atm_err);
   (void)hipFree(e->d_atm_col);
   (void)hipFree(e->d_atm_w);
   (void)hipFree(e->atm_pool);
@@ -319,9 +458,10 @@ extern "C" int fcx_destroy(fcx_engine *e) {
   if (e->ev1) (void)hipEventDestroy(e->ev1);
   for (hipEvent_t ev : e->ev_in) (void)hipEventDestroy(ev);
   for (hipEvent_t ev : e->ev_comp) (void)hipEventDestroy(ev);
+  for (hipEvent_t ev : e->ev_out) (void)hipEventDestroy(ev);
+  stage_free(e);
   if (e->s_in) (void)hipStreamDestroy(e->s_in);
   if (e->s_out) (void)hipStreamDestroy(e->s_out);
-  unpin_host_arrays(e);
   if (e->own_stream && e->stream) (void)hipStreamDestroy(e->stream);
   delete e;
   return FCX_OK;
@@ -635,11 +775,8 @@ static void plan_fused_atmos(fcx_engine *e, Plan &pl, uint32_t stages, int phase
   if (nf == 0) return;
   af.idx = e->d_atm_idx;
   af.w = e->d_atm_w;
-  af.carry = e->d_atm_carry;
-  af.flag = e->d_atm_flag;
   af.xrec = e->d_atm_xrec;
   af.xrec_on = e->atm_crossings > 0;
-  if (e->h_atm_err && hipHostGetDevicePointer((void **)&af.err, e->h_atm_err, 0) != hipSuccess) af.err = nullptr;
   af.n_atmos = e->n_atmos;
   af.shared = e->atm_shared;
   af.stride = e->atm_stride;
@@ -1063,113 +1200,6 @@ extern "C" int fcx_host_free(void *ptr) {
   return FCX_OK;
 }
 
-// Process-wide page-lock registry.  The runtime locks whole pages, so two registrations
-// that touch one page -- two arrays of one engine, or arrays of two live engines, sharing a
-// page -- would tear down each other's lock when either is unregistered (the runtime aborts
-// in hipHostUnregister / hipFree).  Every registration made here therefore owns its pages
-// exclusively: ranges of one engine that share a page are merged, the same exact range
-// asked for again (another engine over the same arrays) is shared by reference count, and
-// a range whose pages meet a different live registration stays pageable.
-namespace {
-
-struct PinEntry {
-  uintptr_t a, b;  // registered bytes [a, b)
-  unsigned flags;
-  int refs;
-};
-std::mutex g_pin_mu;
-std::map<uintptr_t, PinEntry> g_pins;  // keyed by first page number; page spans disjoint
-
-uintptr_t page_shift() {
-  static const uintptr_t s = [] {
-    long ps = sysconf(_SC_PAGESIZE);
-    uintptr_t k = 12;
-    while (ps > 0 && ((uintptr_t)1 << k) < (uintptr_t)ps) ++k;
-    return k;
-  }();
-  return s;
-}
-
-// true: [a, b) is page-locked for the caller (new or shared registration)
-bool pin_range(uintptr_t a, uintptr_t b, unsigned flags) {
-  const uintptr_t sh = page_shift(), pa = a >> sh, pb = (b - 1) >> sh;
-  std::lock_guard<std::mutex> lk(g_pin_mu);
-  auto it = g_pins.upper_bound(pb);
-  if (it != g_pins.begin()) {
-    --it;  // the registration with the largest first page <= pb
-    PinEntry &x = it->second;
-    if (((x.b - 1) >> sh) >= pa) {
-      if (x.a == a && x.b == b && x.flags == flags) {
-        ++x.refs;
-        return true;
-      }
-      return false;  // pages shared with another registration: stay pageable
-    }
-  }
-  if (hipHostRegister(reinterpret_cast<void *>(a), b - a, flags) != hipSuccess) {
-    (void)hipGetLastError();  // e.g. registered by the caller already: leave it
-    return false;
-  }
-  g_pins.emplace(pa, PinEntry{a, b, flags, 1});
-  return true;
-}
-
-void unpin_range(uintptr_t a) {
-  std::lock_guard<std::mutex> lk(g_pin_mu);
-  auto it = g_pins.find(a >> page_shift());
-  if (it == g_pins.end() || it->second.a != a) return;
-  if (--it->second.refs == 0) {
-    (void)hipHostUnregister(reinterpret_cast<void *>(a));
-    g_pins.erase(it);
-  }
-}
-
-}  // namespace
-
-// Page-lock the caller's host arrays once: the per-step H2D/D2H then run as DMA at the link
-// rate and overlap with compute.  The registered ranges are the arrays' own bytes (merged
-// where two arrays share a page, which only spans bytes inside pages already touched); they
-// are not rounded out to pages: a registered range that swallowed the head of some other
-// allocation would make the runtime treat that memory as part of ours and reject copies
-// running past our end.  A range that cannot be registered exclusively stays pageable (its
-// copies are still correct, only staged).
-static void pin_host_arrays(fcx_engine *e) {
-  std::vector<std::pair<uintptr_t, uintptr_t>> r;
-  auto add = [&](const void *p, size_t bytes) {
-    if (!p || !bytes) return;
-    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-    r.push_back({a, a + bytes});
-  };
-  auto add_own = [&](const void *p, size_t bytes) {  // library blocks are locked already
-    if (p && !lib_block_device_ptr(p, bytes)) add(p, bytes);
-  };
-  for (auto &bf : e->bufs)
-    if (!bf.external) add_own(bf.host, (size_t)bf.n * e->esize);
-  for (auto &f : e->atm_fields)
-    if (!f.external) add_own(f.out_host, (size_t)std::max<int64_t>(e->n_atmos, 0) * e->esize);
-  for (auto &rm : e->remaps)
-    for (auto &f : rm.fields)
-      if (!f.external) add_own(f.out_host, (size_t)rm.n_dst * e->esize);
-  std::sort(r.begin(), r.end());
-  const uintptr_t sh = page_shift();
-  std::vector<std::pair<uintptr_t, uintptr_t>> m;
-  for (auto &x : r) {
-    if (!m.empty() && (x.first >> sh) <= ((m.back().second - 1) >> sh))
-      m.back().second = std::max(m.back().second, x.second);  // overlap or shared page
-    else
-      m.push_back(x);
-  }
-  const unsigned flags = hipHostRegisterDefault;
-  for (auto &x : m)
-    if (pin_range(x.first, x.second, flags))
-      e->pinned.push_back({reinterpret_cast<char *>(x.first), x.second - x.first});
-}
-
-static void unpin_host_arrays(fcx_engine *e) {
-  for (auto &r : e->pinned) unpin_range(reinterpret_cast<uintptr_t>(r.first));
-  e->pinned.clear();
-}
-
 // Zero-copy (FCX_OPT_ZERO_COPY): a host array inside an fcx_host_malloc block is used by the
 // kernels in place through its device-visible address -- no device mirror, no copy call; the
 // cells kernel streams it over the host link.  For the latency-bound small grids this
@@ -1260,6 +1290,7 @@ static int alloc_tiled(fcx_engine *e) {
   const int64_t S = std::max(1, std::max(count[kRead], count[kWrite]));
   const int64_t tiles = std::max<int64_t>(1, (n_max + kLayoutTile - 1) / kLayoutTile);
   const size_t bytes = (size_t)tiles * S * kLayoutTile * e->esize;
+  e->tiled_bytes = bytes;
   // pool and slot of every buffer: read pool, write pool, then the cold ones S to a pool
   std::vector<std::pair<int, int>> at(e->bufs.size());
   int npools = 0, fill[3] = {0, 0, 0}, pool_of[2] = {-1, -1}, cold_pool = -1;
@@ -1332,6 +1363,219 @@ static hipError_t zero_cells(const fcx_engine *e, double *dev, int64_t n, hipStr
   return hipSuccess;
 }
 
+// ---- staging arena (FCX_OPT_HOST_STAGING) ---------------------------------------------
+//
+// Caller heap arrays (a Fortran host's ALLOCATEd local_field arrays, numpy arrays) are never
+// page-locked or mapped: every transfer goes through an engine-owned page-locked image of
+// the device pool that holds their mirrors, with the same bytes at the same offsets.  An
+// upload copies the arrays into the image on the host (CopyPool threads), then moves each
+// run of consecutive mirrors with ONE DMA (a tiled pool's run of slots is one 2-D copy over
+// the tile rows, one 1-D copy when it spans whole rows); a download is the reverse, its host
+// copies done once the stream has drained (fcx_synchronize).  Against one runtime copy per
+// array (the pageable path, FCX_OPT_HOST_STAGING = 0) this removes ~15 of the ~17 copy calls
+// of a step, whose fixed cost dominates the Baltic-size grid.
+
+// which pool holds the mirror at device address d; sp = -1 when none with host-bound mirrors
+static StageRef stage_ref(fcx_engine *e, const void *d) {
+  StageRef r;
+  const char *p = reinterpret_cast<const char *>(d);
+  for (size_t i = 0; i < e->spools.size(); ++i) {
+    const StagePool &q = e->spools[i];
+    if (p >= q.dev && p < q.dev + q.bytes) {
+      r.sp = (int)i;
+      r.soff = (size_t)(p - q.dev);
+      return r;
+    }
+  }
+  return r;
+}
+
+// at commit: the pools of the engine's mirrors, and for every caller heap array (not
+// fcx_host_malloc memory, which is copied by direct DMA, and not device or in-place memory)
+// its place in them.  The host images are allocated at the first staged transfer.
+static void stage_setup(fcx_engine *e) {
+  if (!e->staging) return;
+  const size_t es = e->esize;
+  std::vector<StagePool> cand;
+  for (void *p : e->tiled_pools)
+    cand.push_back(StagePool{(char *)p, nullptr, e->tiled_bytes, true, (size_t)kLayoutTile * es,
+                             (size_t)(kLayoutTile + e->tpad) * es});
+  if (e->pool) cand.push_back(StagePool{(char *)e->pool, nullptr, e->pool_bytes, false, 0, 0});
+  if (e->atm_pool) {
+    const bool t = e->atm_out_tpad != 0;
+    cand.push_back(StagePool{(char *)e->atm_pool, nullptr, e->atm_pool_bytes, t, t ? (size_t)kLayoutTile * es : 0,
+                             t ? (size_t)(kLayoutTile + e->atm_out_tpad) * es : 0});
+  }
+  for (auto &rm : e->remaps)
+    if (rm.pool) cand.push_back(StagePool{(char *)rm.pool, nullptr, rm.pool_bytes, false, 0, 0});
+  // keep the pools some heap array's mirror lives in
+  auto heap = [&](const void *host, int64_t n) { return host && !lib_block_device_ptr(host, (size_t)std::max<int64_t>(n, 1) * es); };
+  std::vector<char> used(cand.size(), 0);
+  auto mark = [&](const void *dev) {
+    for (size_t i = 0; i < cand.size(); ++i)
+      if ((const char *)dev >= cand[i].dev && (const char *)dev < cand[i].dev + cand[i].bytes) used[i] = 1;
+  };
+  for (auto &bf : e->bufs)
+    if (!bf.external && heap(bf.host, bf.n)) mark(bf.dev);
+  for (auto &f : e->atm_fields)
+    if (!f.external && heap(f.out_host, e->n_atmos)) mark(f.out_dev);
+  for (auto &rm : e->remaps)
+    for (auto &f : rm.fields)
+      if (!f.external && heap(f.out_host, rm.n_dst)) mark(f.out_dev);
+  for (size_t i = 0; i < cand.size(); ++i)
+    if (used[i]) e->spools.push_back(cand[i]);
+  for (auto &bf : e->bufs)
+    if (!bf.external && heap(bf.host, bf.n)) bf.st = stage_ref(e, bf.dev);
+  for (auto &f : e->atm_fields)
+    if (!f.external && heap(f.out_host, e->n_atmos)) f.st = stage_ref(e, f.out_dev);
+  for (auto &rm : e->remaps)
+    for (auto &f : rm.fields)
+      if (!f.external && heap(f.out_host, rm.n_dst)) f.st = stage_ref(e, f.out_dev);
+}
+
+static int stage_alloc(fcx_engine *e) {
+  for (auto &p : e->spools)
+    if (!p.host) {
+      hipError_t err = hipHostMalloc((void **)&p.host, std::max<size_t>(p.bytes, 1), hipHostMallocDefault);
+      if (err != hipSuccess)
+        return fail(FCX_E_NOMEM, "hipHostMalloc(%zu) for the staging arena: %s", p.bytes, hipGetErrorString(err));
+    }
+  return FCX_OK;
+}
+
+static void stage_free(fcx_engine *e) {
+  for (auto &p : e->spools)
+    if (p.host) (void)hipHostFree(p.host);
+  e->spools.clear();
+  if (e->ev_stage_in) (void)hipEventDestroy(e->ev_stage_in);
+  e->ev_stage_in = nullptr;
+}
+
+// host copies of elements [a, z) (z < 0: to the array's end) of every transfer, caller array
+// -> arena image (gather) or back (scatter), spread over the copy threads
+static void stage_copy(fcx_engine *e, const std::vector<Xfer> &xs, int64_t a, int64_t z, bool gather) {
+  constexpr size_t kPiece = size_t(64) << 10;
+  const size_t es = e->esize;
+  std::vector<CopyJob> jobs;
+  auto add = [&](char *img, char *host, size_t bytes) {
+    for (size_t o = 0; o < bytes; o += kPiece) {
+      const size_t b = std::min(kPiece, bytes - o);
+      jobs.push_back(gather ? CopyJob{img + o, host + o, b} : CopyJob{host + o, img + o, b});
+    }
+  };
+  for (const Xfer &x : xs) {
+    const StagePool &p = e->spools[(size_t)x.sp];
+    const int64_t lo = std::min(a, x.n), hi = z < 0 ? x.n : std::min(z, x.n);
+    if (hi <= lo) continue;
+    if (!p.tiled) {
+      add(p.host + x.soff + (size_t)lo * es, x.host + (size_t)lo * es, (size_t)(hi - lo) * es);
+      continue;
+    }
+    for (int64_t t0 = lo; t0 < hi;) {
+      const int64_t row = t0 >> kLayoutShift, t1 = std::min(hi, (row + 1) << kLayoutShift);
+      add(p.host + x.soff + (size_t)row * p.pitch + (size_t)(t0 - (row << kLayoutShift)) * es,
+          x.host + (size_t)t0 * es, (size_t)(t1 - t0) * es);
+      t0 = t1;
+    }
+  }
+  CopyPool::get().run(jobs, e->host_threads > 0 ? e->host_threads : default_host_threads());
+}
+
+// DMAs of elements [a, z) of the transfers' mirrors between arena and device: per pool,
+// every run of consecutive mirrors in one copy.  Tiled pools: a run is adjacent slots, moved
+// over the tile rows [a / tile, ceil(z / tile)) as one 2-D copy (1-D when the run is whole
+// rows); plain pools: mirrors back to back (256-B aligned), whole arrays only.  A run holds
+// transfer members only, so an upload never overwrites another mirror.
+static hipError_t stage_dma(fcx_engine *e, std::vector<Xfer> xs, int64_t a, int64_t z, bool h2d, hipStream_t s) {
+  const size_t es = e->esize;
+  std::sort(xs.begin(), xs.end(), [](const Xfer &l, const Xfer &r) {
+    return l.sp != r.sp ? l.sp < r.sp : l.soff < r.soff;
+  });
+  const hipMemcpyKind kind = h2d ? hipMemcpyHostToDevice : hipMemcpyDeviceToHost;
+  size_t i = 0;
+  while (i < xs.size()) {
+    const StagePool &p = e->spools[(size_t)xs[i].sp];
+    size_t j = i + 1;
+    int64_t hi = z < 0 ? xs[i].n : std::min(z, xs[i].n);
+    if (p.tiled) {
+      size_t end = xs[i].soff + p.slot;
+      while (j < xs.size() && xs[j].sp == xs[i].sp && (xs[j].soff == end || xs[j].soff + p.slot == end)) {
+        end = std::max(end, xs[j].soff + p.slot);
+        hi = std::max(hi, z < 0 ? xs[j].n : std::min(z, xs[j].n));
+        ++j;
+      }
+      const int64_t r0 = a >> kLayoutShift, r1 = (hi + kLayoutTile - 1) >> kLayoutShift;
+      if (r1 > r0 && hi > a) {
+        const size_t off = xs[i].soff + (size_t)r0 * p.pitch, width = end - xs[i].soff;
+        char *d = p.dev + off, *h = p.host + off;
+        hipError_t r = width == p.pitch
+                           ? hipMemcpyAsync(h2d ? (void *)d : (void *)h, h2d ? (void *)h : (void *)d,
+                                            (size_t)(r1 - r0) * p.pitch, kind, s)
+                           : hipMemcpy2DAsync(h2d ? (void *)d : (void *)h, p.pitch, h2d ? (void *)h : (void *)d,
+                                              p.pitch, width, (size_t)(r1 - r0), kind, s);
+        if (r != hipSuccess) return r;
+      }
+    } else {
+      const int64_t lo = std::min(a, xs[i].n);
+      size_t end = xs[i].soff + (size_t)hi * es;
+      if (a == 0 && z < 0)  // whole arrays: the next mirror starts at the 256-B aligned end
+        while (j < xs.size() && xs[j].sp == xs[i].sp && xs[j].soff <= (end + 255) / 256 * 256 && xs[j].soff >= xs[i].soff) {
+          end = std::max(end, xs[j].soff + (size_t)xs[j].n * es);
+          ++j;
+        }
+      if (end > xs[i].soff + (size_t)lo * es) {
+        const size_t off = xs[i].soff + (size_t)lo * es;
+        hipError_t r = hipMemcpyAsync(h2d ? (void *)(p.dev + off) : (void *)(p.host + off),
+                                      h2d ? (void *)(p.host + off) : (void *)(p.dev + off), end - off, kind, s);
+        if (r != hipSuccess) return r;
+      }
+    }
+    i = j;
+  }
+  return hipSuccess;
+}
+
+static int stage_flush(fcx_engine *e);
+
+// upload through the arena: the previous upload's DMA must have left the image, and
+// outputs still waiting for their host copies are completed first
+static int stage_in(fcx_engine *e, const std::vector<Xfer> &xs, hipStream_t s) {
+  if (xs.empty()) return FCX_OK;
+  if (int r = stage_alloc(e)) return r;
+  if (!e->pending_out.empty()) {
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    if (int r = stage_flush(e)) return r;
+  }
+  if (e->stage_in_live) HIP_TRY(hipEventSynchronize(e->ev_stage_in));
+  stage_copy(e, xs, 0, -1, true);
+  HIP_TRY(stage_dma(e, xs, 0, -1, true, s));
+  if (!e->ev_stage_in) HIP_TRY(hipEventCreateWithFlags(&e->ev_stage_in, hipEventDisableTiming));
+  HIP_TRY(hipEventRecord(e->ev_stage_in, s));
+  e->stage_in_live = true;
+  return FCX_OK;
+}
+
+// download through the arena: the DMAs now, the host copies at the next synchronisation
+static int stage_out(fcx_engine *e, const std::vector<Xfer> &xs, hipStream_t s) {
+  if (xs.empty()) return FCX_OK;
+  if (int r = stage_alloc(e)) return r;
+  HIP_TRY(stage_dma(e, xs, 0, -1, false, s));
+  e->pending_out.insert(e->pending_out.end(), xs.begin(), xs.end());
+  return FCX_OK;
+}
+
+// after the stream has drained: the pending downloads into the caller's arrays
+static int stage_flush(fcx_engine *e) {
+  if (e->pending_out.empty()) return FCX_OK;
+  stage_copy(e, e->pending_out, 0, -1, false);
+  e->pending_out.clear();
+  return FCX_OK;
+}
+
+static Xfer xfer_of(const StageRef &st, void *host, int64_t n) {
+  return Xfer{st.sp, st.soff, reinterpret_cast<char *>(host), n};
+}
+
 extern "C" int fcx_set_precision(fcx_engine *e, int precision) {
   if (!e) return fail(FCX_E_ARG, "NULL engine");
   if (e->committed) return fail(FCX_E_STATE, "engine already committed");
@@ -1391,11 +1635,9 @@ extern "C" int fcx_commit(fcx_engine *e) {
   if (int r = gpu_init(e)) return r;
   // Zero-copy of fcx_host_malloc arrays.  2 (auto, default): where the pipelined step would
   // not apply (grids below two chunks, where the step is latency-bound and per-array copies
-  // dominate it); 1: at any size; 0: never.  Caller heap arrays always take mirrors, fed by
-  // DMA from their page-locked ranges (FCX_OPT_PIN_HOST) or staged copies.
+  // dominate it); 1: at any size; 0: never.  Caller heap arrays always take mirrors.
   const int64_t n_big = std::max(e->n[0], std::max(e->n[1], e->n[2]));
   const bool small = n_big < 2 * e->min_chunk;
-  if (e->pin_host) pin_host_arrays(e);
   if (e->zero_copy == 1 || (e->zero_copy == 2 && small)) e->zc_active = map_host_arrays(e) > 0;
   bool any_external = false;
   for (auto &bf : e->bufs) any_external = any_external || bf.external;
@@ -1413,6 +1655,7 @@ extern "C" int fcx_commit(fcx_engine *e) {
     total += ((size_t)e->bufs[b].n * e->esize + 255) / 256 * 256;
   }
   if (total) {
+    e->pool_bytes = total;
     hipError_t err = hipMalloc(&e->pool, total);
     if (err != hipSuccess)
       return fail(FCX_E_NOMEM, "hipMalloc(%zu) for the field mirrors: %s", total, hipGetErrorString(err));
@@ -1457,18 +1700,11 @@ extern "C" int fcx_commit(fcx_engine *e) {
       HIP_TRY(hipMemcpy(e->d_atm_idx, e->atm_idx.data(), e->atm_idx.size() * sizeof(int32_t),
                         hipMemcpyHostToDevice));
       const int64_t tiles = (e->n[0] + kTile - 1) / kTile;
-      HIP_TRY(hipMalloc(&e->d_atm_carry, (size_t)std::max<int64_t>(tiles, 1) * kFusedFields * sizeof(double)));
-      HIP_TRY(hipMalloc(&e->d_atm_flag, (size_t)std::max<int64_t>(tiles, 1) * sizeof(uint32_t)));
-      HIP_TRY(hipMemset(e->d_atm_flag, 0, (size_t)std::max<int64_t>(tiles, 1) * sizeof(uint32_t)));
       HIP_TRY(hipMalloc(&e->d_atm_xrec, (size_t)std::max<int64_t>(tiles, 1) * kXRec * sizeof(double)));
       // tile boundaries a segment runs across: none (a map whose runs never cross a wave
       // tile) means no fix-up launch at all
       e->atm_crossings = 0;
       for (size_t b = kTile; b < e->atm_idx.size(); b += kTile) e->atm_crossings += e->atm_idx[b - 1] == e->atm_idx[b];
-      if (!e->h_atm_err) {
-        HIP_TRY(hipHostMalloc((void **)&e->h_atm_err, sizeof(uint32_t), hipHostMallocMapped));
-        *e->h_atm_err = 0;
-      }
     }
     if (!e->atm_contiguous) {
       HIP_TRY(hipMalloc(&e->d_atm_col, std::max<size_t>(e->atm_col.size(), 1) * sizeof(int32_t)));
@@ -1488,13 +1724,15 @@ extern "C" int fcx_commit(fcx_engine *e) {
     const int64_t nfa = (int64_t)e->atm_fields.size();
     if (FCX_TILED_ATM && e->tpad && !atm_ext && nfa >= 2 && e->n_atmos > 0) {
       const int64_t tiles = (e->n_atmos + kLayoutTile - 1) / kLayoutTile;
-      HIP_TRY(hipMalloc(&e->atm_pool, (size_t)tiles * nfa * kLayoutTile * e->esize));
+      e->atm_pool_bytes = (size_t)tiles * nfa * kLayoutTile * e->esize;
+      HIP_TRY(hipMalloc(&e->atm_pool, e->atm_pool_bytes));
       for (int64_t k = 0; k < nfa; ++k)
         e->atm_fields[k].out_dev = reinterpret_cast<double *>((char *)e->atm_pool + (size_t)k * kLayoutTile * e->esize);
       e->atm_out_tpad = (nfa - 1) * kLayoutTile;
       need = 0;
     }
     if (need) {
+      e->atm_pool_bytes = need;
       HIP_TRY(hipMalloc(&e->atm_pool, need));
       size_t off = 0;
       for (auto &f : e->atm_fields)
@@ -1531,6 +1769,7 @@ extern "C" int fcx_commit(fcx_engine *e) {
     size_t need = 0;
     for (auto &f : rm.fields) need += f.external ? 0 : one;
     if (need) {
+      rm.pool_bytes = need;
       HIP_TRY(hipMalloc(&rm.pool, need));
       size_t off = 0;
       for (auto &f : rm.fields)
@@ -1551,6 +1790,7 @@ extern "C" int fcx_commit(fcx_engine *e) {
       e->rec_bytes = std::max(e->rec_bytes, (size_t)(rm.max_src + 1) * rec_width(e, (int)nf_max) * e->esize);
   }
   if (e->rec_bytes) HIP_TRY(hipMalloc(&e->d_rec, e->rec_bytes));
+  stage_setup(e);
   e->committed = true;
   return FCX_OK;
 }
@@ -1575,16 +1815,22 @@ static const double *month_slice(fcx_engine *e, int32_t t, int *rc) {
   return reinterpret_cast<const double *>((const char *)e->corr_dev + (size_t)(m - 1) * e->n[0] * e->esize);
 }
 
-static int copy_bufs(fcx_engine *e, const std::vector<int> &ids, bool h2d) {
+// the mirrors of buffers `ids` <-> their host arrays on the engine stream: caller heap arrays
+// through the staging arena, fcx_host_malloc arrays (and staging off) by direct copies
+static int copy_bufs(fcx_engine *e, const std::vector<int> &ids, bool h2d, std::vector<Xfer> *more = nullptr) {
+  std::vector<Xfer> xs;
+  if (more) xs.swap(*more);
   for (int b : ids) {
     const Buffer &bf = e->bufs[b];
     if (bf.external || bf.n == 0) continue;
+    if (bf.st.sp >= 0) {
+      xs.push_back(xfer_of(bf.st, bf.host, bf.n));
+      continue;
+    }
     HIP_TRY(copy_cells(e, bf, 0, bf.n, h2d, e->stream));
   }
-  return FCX_OK;
+  return h2d ? stage_in(e, xs, e->stream) : stage_out(e, xs, e->stream);
 }
-
-static int check_handoff(fcx_engine *e);
 
 static int launch_plan(fcx_engine *e, Plan *pl, const double *corr_m, int64_t lo = 0, int64_t hi = -1,
                        bool fixup = true) {
@@ -1600,35 +1846,24 @@ static int launch_plan(fcx_engine *e, Plan *pl, const double *corr_m, int64_t lo
   lc.variant = (e->specialize && lc.merged) ? pl->variant : 0;
   lc.f32 = e->f32;
   lc.ravg = pl->host.ravg_on != 0;
-  lc.rec = pl->host.rec != nullptr;
+  // remap records only from the T=1 specialised fp64 kernels with two cells per lane (the
+  // rule plan_fused_records applied when it built the plan)
+  lc.rec = pl->host.rec != nullptr && lc.variant && lc.cells_per_thread == 2 && !lc.f32;
+  e->rec_written = lc.rec;
   const bool fused = pl->atm_fused && lc.variant && lc.cells_per_thread == 2;
   if (fused) {  // the shared-slot pointers may have been set after the plan was built
     pl->af.shared = e->atm_shared;
     pl->af.stride = e->atm_stride;
     pl->af.left = e->atm_left;
     pl->af.right = e->atm_right;
-    // carries handed to the next tile's wave inside the launch: only when every wave makes
-    // one trip (no grid-stride cap), so a wave only ever waits on an earlier-dispatched one;
-    // a run's chunk launches share its epoch (lo == 0 starts a run)
-    // (FCX_OPT_CARRY_HANDOFF; the default leaves the carries to atmos_fixup_kernel)
-    pl->af.handoff = e->carry_handoff && lc.max_blocks <= 0 && pl->af.err != nullptr;
-    if (lo == 0 && ++e->atm_epoch == 0) e->atm_epoch = 1;
-    pl->af.epoch = e->atm_epoch;
   }
   const int r = launch_cells(&pl->host, pl->dev, corr_m, lc, e->stream, fused ? &pl->af : nullptr);
   if (r) return fail(FCX_E_HIP, "cells_kernel launch: %s", hipGetErrorString((hipError_t)r));
-  if (fused && fixup && !pl->af.handoff && e->atm_crossings > 0) {
+  if (fused && fixup && e->atm_crossings > 0) {
     const int r2 = launch_atmos_fixup(pl->af, pl->host.n_max, lc.f32, e->stream);
     if (r2) return fail(FCX_E_HIP, "atmos_fixup launch: %s", hipGetErrorString((hipError_t)r2));
   }
-  if (fused) {
-    e->atm_done_fused = true;
-    e->last_phase = pl->atm_phase;
-    if (e->test_handoff_timeout && pl->af.handoff) {  // test hook: as if a wait had given up
-      HIP_TRY(hipStreamSynchronize(e->stream));
-      __atomic_store_n(e->h_atm_err, 1u, __ATOMIC_RELEASE);
-    }
-  }
+  if (fused) e->atm_done_fused = true;
   return FCX_OK;
 }
 
@@ -1636,7 +1871,7 @@ static int regrid_var(fcx_engine *e, int var, int surface_type);
 static int comm_exchange(fcx_engine *e);
 static hipError_t get_atm(const fcx_engine *e, double *host, const double *dev, hipStream_t s);
 static int run_remaps(fcx_engine *e, int phase);
-static int download_remaps(fcx_engine *e, int phase, hipStream_t s);
+static int download_remaps(fcx_engine *e, int phase, hipStream_t s, std::vector<Xfer> *xs);
 
 // the reference step order with do_regridding after each calc (flux_calculator.F90:972-991)
 static int staged_sequence(int phase, std::vector<std::pair<uint32_t, int>> &seq) {
@@ -1673,11 +1908,16 @@ extern "C" int fcx_download(fcx_engine *e, int phase) {
   if (phase < 1 || phase > 3) return fail(FCX_E_ARG, "phase %d unknown", phase);
   Plan *pl;
   if (int r = get_plan(e, phase_stages(phase), phase, &pl)) return r;
-  if (int r = copy_bufs(e, pl->writes, false)) return r;
+  std::vector<Xfer> xs;  // every staged download of the phase in one set of DMAs
+  std::vector<int> ids = pl->writes;
   for (auto &f : e->atm_fields)
-    if ((f.phase & phase) && !f.external && e->n_atmos > 0)
-      HIP_TRY(get_atm(e, f.out_host, f.out_dev, e->stream));
-  if (int r = download_remaps(e, phase, e->stream)) return r;
+    if ((f.phase & phase) && !f.external && e->n_atmos > 0) {
+      if (f.st.sp >= 0)
+        xs.push_back(xfer_of(f.st, f.out_host, e->n_atmos));
+      else
+        HIP_TRY(get_atm(e, f.out_host, f.out_dev, e->stream));
+    }
+  if (int r = download_remaps(e, phase, e->stream, &xs)) return r;
   if (e->any_regrid) {  // device-side regrid destinations of the fields this phase computes
     std::vector<int> extra;
     std::vector<int> vars;
@@ -1691,11 +1931,11 @@ extern "C" int fcx_download(fcx_engine *e, int phase) {
             for (int k = 0; k < 3; ++k)
               if ((e->put_to[s][g - 1][v - 1] >> k) & 1)
                 if (e->buf(s, k + 1, v) >= 0) extra.push_back(e->buf(s, k + 1, v));
-    std::sort(extra.begin(), extra.end());
-    extra.erase(std::unique(extra.begin(), extra.end()), extra.end());
-    if (int r = copy_bufs(e, extra, false)) return r;
+    ids.insert(ids.end(), extra.begin(), extra.end());
   }
-  return FCX_OK;
+  std::sort(ids.begin(), ids.end());
+  ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
+  return copy_bufs(e, ids, false, &xs);
 }
 
 // an atmosphere output mirror -> its host array (2-D copy of the whole tiles when tiled)
@@ -1795,11 +2035,16 @@ static int run_remaps(fcx_engine *e, int phase) {
   return FCX_OK;
 }
 
-static int download_remaps(fcx_engine *e, int phase, hipStream_t s) {
+// remap outputs -> host: staged ones appended to xs, the others copied directly
+static int download_remaps(fcx_engine *e, int phase, hipStream_t s, std::vector<Xfer> *xs) {
   for (auto &rm : e->remaps)
     for (auto &f : rm.fields)
-      if ((f.phase & phase) && !f.external && rm.n_dst > 0)
-        HIP_TRY(hipMemcpyAsync(f.out_host, f.out_dev, rm.n_dst * e->esize, hipMemcpyDeviceToHost, s));
+      if ((f.phase & phase) && !f.external && rm.n_dst > 0) {
+        if (f.st.sp >= 0)
+          xs->push_back(xfer_of(f.st, f.out_host, rm.n_dst));
+        else
+          HIP_TRY(hipMemcpyAsync(f.out_host, f.out_dev, rm.n_dst * e->esize, hipMemcpyDeviceToHost, s));
+      }
   return FCX_OK;
 }
 
@@ -1817,7 +2062,7 @@ extern "C" int fcx_run(fcx_engine *e, int phase, int32_t t) {
     Plan *pl;
     if (int r = get_plan(e, phase_stages(phase), phase, &pl)) return r;
     if (int r = launch_plan(e, pl, corr_m)) return r;
-    e->rec_plan = pl;
+    e->rec_plan = e->rec_written ? pl : nullptr;  // run_remaps gathers the records it wrote
   } else {
     std::vector<std::pair<uint32_t, int>> seq;
     staged_sequence(phase, seq);
@@ -1856,7 +2101,10 @@ static int copy_slice(fcx_engine *e, const Buffer &bf, int64_t lo, int64_t hi, b
 // fcx_step of a host-bound engine as a 3-stage pipeline over cell chunks: H2D of chunk k+1
 // (s_in), the cells kernel of chunk k (engine stream) and D2H of chunk k-1 (s_out) overlap,
 // so a step costs ~max(H2D bytes, D2H bytes) / link rate instead of their sum plus compute.
-// The accumulation fix-up / separate kernel and the atmosphere outputs follow the last chunk.
+// Caller heap arrays go through the staging arena: this thread copies chunk k into it before
+// its DMA is queued, and copies chunk k-2 out once its DMA has landed, while the copy
+// engines move the chunks in between.  The accumulation fix-up / separate kernel and the
+// atmosphere outputs follow the last chunk.
 static int step_pipelined(fcx_engine *e, int phase, int32_t t, Plan *pl) {
   int rc;
   const double *corr_m = month_slice(e, t, &rc);
@@ -1874,12 +2122,51 @@ static int step_pipelined(fcx_engine *e, int phase, int32_t t, Plan *pl) {
   if (!e->s_in) HIP_TRY(hipStreamCreateWithFlags(&e->s_in, hipStreamNonBlocking));
   if (!e->s_out) HIP_TRY(hipStreamCreateWithFlags(&e->s_out, hipStreamNonBlocking));
   while ((int)e->ev_in.size() < K) {
-    hipEvent_t a, b;
+    hipEvent_t a, b, c;
     HIP_TRY(hipEventCreateWithFlags(&a, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&b, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&c, hipEventDisableTiming));
     e->ev_in.push_back(a);
     e->ev_comp.push_back(b);
+    e->ev_out.push_back(c);
   }
+  // staged (caller heap) and direct (library memory) transfers
+  std::vector<Xfer> xin, xout;
+  std::vector<int> din, dout;
+  for (int b : pl->reads) {
+    const Buffer &bf = e->bufs[b];
+    if (bf.external || bf.n == 0) continue;
+    if (bf.st.sp >= 0) xin.push_back(xfer_of(bf.st, bf.host, bf.n));
+    else din.push_back(b);
+  }
+  for (int b : pl->writes) {
+    const Buffer &bf = e->bufs[b];
+    if (bf.external || bf.n == 0) continue;
+    if (bf.st.sp >= 0) xout.push_back(xfer_of(bf.st, bf.host, bf.n));
+    else dout.push_back(b);
+  }
+  if (!xin.empty() || !xout.empty()) {
+    if (int r = stage_alloc(e)) return r;
+    if (!e->pending_out.empty()) {  // earlier downloads still owe their host copies
+      HIP_TRY(hipStreamSynchronize(e->stream));
+      if (int r = stage_flush(e)) return r;
+    }
+    if (e->stage_in_live) HIP_TRY(hipEventSynchronize(e->ev_stage_in));
+  }
+  auto range = [&](int k, int64_t *lo, int64_t *hi) {  // the last chunk takes the arrays' tails
+    *lo = k * per;
+    *hi = k == K - 1 ? -1 : std::min(n, *lo + per);
+  };
+  int scattered = 0;  // chunks whose outputs are in the caller's arrays
+  auto scatter_upto = [&](int k_end) -> int {
+    for (; scattered < k_end; ++scattered) {
+      int64_t lo, hi;
+      range(scattered, &lo, &hi);
+      HIP_TRY(hipEventSynchronize(e->ev_out[scattered]));
+      stage_copy(e, xout, lo, hi, false);
+    }
+    return FCX_OK;
+  };
   if (e->timing) HIP_TRY(hipEventRecord(e->ev0, e->s_in));
   e->atm_done_fused = false;
   e->atm_done = e->exchanged = false;
@@ -1887,15 +2174,24 @@ static int step_pipelined(fcx_engine *e, int phase, int32_t t, Plan *pl) {
   for (int k = 0; k < K; ++k) {
     const int64_t lo = k * per, hi = std::min(n, lo + per);
     const bool last = k == K - 1;
-    for (int b : pl->reads)
+    if (!xin.empty()) {
+      stage_copy(e, xin, lo, last ? -1 : hi, true);
+      HIP_TRY(stage_dma(e, xin, lo, last ? -1 : hi, true, e->s_in));
+    }
+    for (int b : din)
       if (int r = copy_slice(e, e->bufs[b], lo, hi, last, true, e->s_in)) return r;
     HIP_TRY(hipEventRecord(e->ev_in[k], e->s_in));
     HIP_TRY(hipStreamWaitEvent(e->stream, e->ev_in[k], 0));
     if (int r = launch_plan(e, pl, corr_m, lo, hi, last)) return r;
+    if (!e->rec_written) e->rec_plan = nullptr;
     HIP_TRY(hipEventRecord(e->ev_comp[k], e->stream));
     HIP_TRY(hipStreamWaitEvent(e->s_out, e->ev_comp[k], 0));
-    for (int b : pl->writes)
+    if (!xout.empty()) HIP_TRY(stage_dma(e, xout, lo, last ? -1 : hi, false, e->s_out));
+    for (int b : dout)
       if (int r = copy_slice(e, e->bufs[b], lo, hi, last, false, e->s_out)) return r;
+    HIP_TRY(hipEventRecord(e->ev_out[k], e->s_out));
+    if (!xout.empty() && k >= 2)
+      if (int r = scatter_upto(k - 1)) return r;  // chunk k-2 has had two chunks' time to land
   }
   if (e->atmos_in_run && !e->atm_done_fused)
     if (int r = run_atmos(e, phase)) return r;
@@ -1905,16 +2201,25 @@ static int step_pipelined(fcx_engine *e, int phase, int32_t t, Plan *pl) {
   if (int r = run_remaps(e, phase)) return r;
   HIP_TRY(hipEventRecord(e->ev_comp[K - 1], e->stream));
   HIP_TRY(hipStreamWaitEvent(e->s_out, e->ev_comp[K - 1], 0));
+  std::vector<Xfer> xa;  // atmosphere and remap outputs
   if (e->atmos_in_run || e->atm_done_fused)
     for (auto &f : e->atm_fields)
-      if ((f.phase & phase) && !f.external && e->n_atmos > 0)
-        HIP_TRY(get_atm(e, f.out_host, f.out_dev, e->s_out));
-  if (int r = download_remaps(e, phase, e->s_out)) return r;
+      if ((f.phase & phase) && !f.external && e->n_atmos > 0) {
+        if (f.st.sp >= 0)
+          xa.push_back(xfer_of(f.st, f.out_host, e->n_atmos));
+        else
+          HIP_TRY(get_atm(e, f.out_host, f.out_dev, e->s_out));
+      }
+  if (int r = download_remaps(e, phase, e->s_out, &xa)) return r;
+  if (!xa.empty()) HIP_TRY(stage_dma(e, xa, 0, -1, false, e->s_out));
   if (e->timing) HIP_TRY(hipEventRecord(e->ev1, e->s_out));
   e->timed = e->timing;
+  if (!xout.empty())
+    if (int r = scatter_upto(K)) return r;
   HIP_TRY(hipStreamSynchronize(e->s_out));
   HIP_TRY(hipStreamSynchronize(e->stream));
-  return check_handoff(e);
+  if (!xa.empty()) stage_copy(e, xa, 0, -1, false);
+  return FCX_OK;
 }
 
 static bool host_bound(const fcx_engine *e, const Plan *pl) {
@@ -1939,26 +2244,10 @@ extern "C" int fcx_step(fcx_engine *e, int phase, int32_t t) {
   return fcx_synchronize(e);
 }
 
-// A fused accumulation whose carry hand-off gave up (a flag that never came: a producer
-// wave not resident, e.g. another process holding the CUs) left wrong atmosphere values.
-// Recompute them with the separate accumulation kernel over the fluxes the run stored (the
-// same sums in the same order, bit-identical), refresh the host copies, and count it.
-static int check_handoff(fcx_engine *e) {
-  if (!e->h_atm_err || !__atomic_load_n(e->h_atm_err, __ATOMIC_ACQUIRE)) return FCX_OK;
-  *e->h_atm_err = 0;
-  ++e->handoff_recoveries;
-  if (int r = run_atmos(e, e->last_phase)) return r;
-  for (auto &f : e->atm_fields)
-    if ((f.phase & e->last_phase) && !f.external && e->n_atmos > 0)
-      HIP_TRY(get_atm(e, f.out_host, f.out_dev, e->stream));
-  HIP_TRY(hipStreamSynchronize(e->stream));
-  return FCX_OK;
-}
-
 extern "C" int fcx_synchronize(fcx_engine *e) {
   if (!e) return fail(FCX_E_ARG, "NULL engine");
   HIP_TRY(hipStreamSynchronize(e->stream));
-  return check_handoff(e);
+  return stage_flush(e);
 }
 
 // one reference subroutine: upload what it reads, run, download what it writes
@@ -2075,17 +2364,12 @@ extern "C" int fcx_last_kernel_ms(fcx_engine *e, float *ms) {
   return FCX_OK;
 }
 
-extern "C" int fcx_pinned_bytes(fcx_engine *e, int64_t *bytes) {
-  if (!e || !bytes) return fail(FCX_E_ARG, "NULL argument");
+extern "C" int fcx_staging_bytes(fcx_engine *e, int64_t *bytes) {
+  if (int r = check(e)) return r;
+  if (!bytes) return fail(FCX_E_ARG, "NULL argument");
   int64_t b = 0;
-  for (auto &r : e->pinned) b += (int64_t)r.second;
+  for (auto &p : e->spools) b += (int64_t)p.bytes;
   *bytes = b;
-  return FCX_OK;
-}
-
-extern "C" int fcx_handoff_recoveries(fcx_engine *e, int64_t *count) {
-  if (!e || !count) return fail(FCX_E_ARG, "NULL argument");
-  *count = e->handoff_recoveries;
   return FCX_OK;
 }
 
@@ -2148,11 +2432,28 @@ extern "C" int fcx_memcpy(void *dst, const void *src, size_t bytes, int kind) {
 
 // ------------------------------------------------------------------ tuning
 
+// The cached plans were built for the launch options of their time (which kernel writes the
+// remap records, whether the accumulation rides in the flux launch): options that change
+// that drop them, and the next run builds them again.
+static int drop_plans(fcx_engine *e) {
+  if (e->plans.empty()) return FCX_OK;
+  if (e->stream) HIP_TRY(hipStreamSynchronize(e->stream));
+  for (auto &kv : e->plans) {
+    (void)hipFree(kv.second.dev);
+    (void)hipFree(kv.second.host.rec);
+  }
+  e->plans.clear();
+  e->rec_plan = nullptr;
+  return FCX_OK;
+}
+
 extern "C" int fcx_set_option(fcx_engine *e, int option, int64_t value) {
   if (!e) return fail(FCX_E_ARG, "NULL engine");
   switch (option) {
     case FCX_OPT_CELLS_PER_THREAD:
       if (value != 1 && value != 2) return fail(FCX_E_ARG, "cells per thread must be 1 or 2");
+      if (e->launch.cells_per_thread != (int)value)
+        if (int r = drop_plans(e)) return r;
       e->launch.cells_per_thread = (int)value;
       return FCX_OK;
     case FCX_OPT_MAX_BLOCKS:
@@ -2163,14 +2464,12 @@ extern "C" int fcx_set_option(fcx_engine *e, int option, int64_t value) {
       e->launch.nontemporal = value != 0;
       return FCX_OK;
     case FCX_OPT_SPECIALIZE:
+      if (e->specialize != (value != 0))
+        if (int r = drop_plans(e)) return r;
       e->specialize = value != 0;
       return FCX_OK;
     case FCX_OPT_ATMOS_IN_RUN:
       e->atmos_in_run = value != 0;
-      return FCX_OK;
-    case FCX_OPT_PIN_HOST:
-      if (e->committed) return fail(FCX_E_STATE, "pin_host is applied at fcx_commit");
-      e->pin_host = value != 0;
       return FCX_OK;
     case FCX_OPT_TIMING:
       e->timing = value != 0;
@@ -2191,11 +2490,13 @@ extern "C" int fcx_set_option(fcx_engine *e, int option, int64_t value) {
       if (value < 1 || value > 1024) return fail(FCX_E_ARG, "pipeline chunks %lld outside 1..1024", (long long)value);
       e->chunks = (int)value;
       return FCX_OK;
-    case FCX_OPT_TEST_HANDOFF_TIMEOUT:
-      e->test_handoff_timeout = value != 0;
+    case FCX_OPT_HOST_STAGING:
+      if (e->committed) return fail(FCX_E_STATE, "host_staging is applied at fcx_commit");
+      e->staging = value != 0;
       return FCX_OK;
-    case FCX_OPT_CARRY_HANDOFF:
-      e->carry_handoff = value != 0;
+    case FCX_OPT_HOST_THREADS:
+      if (value < 0 || value > 64) return fail(FCX_E_ARG, "host threads %lld outside 0..64", (long long)value);
+      e->host_threads = (int)value;
       return FCX_OK;
     case FCX_OPT_REMAP_PACK:
       if (e->committed) return fail(FCX_E_STATE, "remap_pack is applied at fcx_commit");

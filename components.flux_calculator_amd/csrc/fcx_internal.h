@@ -3,6 +3,28 @@
 #include <cstdint>
 #include "../../include/fcx.h"
 
+// Measurement switches that make the kernels compute WRONG results (they take work out to
+// time what is left).  They exist for the A/B builds of tools/build_variant.sh only, which
+// define FCX_AB_BUILD; a product build that sets one of them does not compile.
+#if !defined(FCX_AB_BUILD)
+#if defined(FCX_TRIVIAL_MATH) || defined(FCX_DBG_ATM_NOLDS) || defined(FCX_DBG_ATM_NOSTORE) || \
+    defined(FCX_DBG_NO_HEAD)
+#error "FCX_TRIVIAL_MATH / FCX_DBG_*: wrong-result measurement builds need FCX_AB_BUILD"
+#endif
+#endif
+#ifndef FCX_TRIVIAL_MATH  // every formula returns a plain sum of its inputs
+#define FCX_TRIVIAL_MATH 0
+#endif
+#ifndef FCX_DBG_ATM_NOLDS  // no LDS products in the fused accumulation (sums of garbage)
+#define FCX_DBG_ATM_NOLDS 0
+#endif
+#ifndef FCX_DBG_ATM_NOSTORE  // no atmosphere-output stores
+#define FCX_DBG_ATM_NOSTORE 0
+#endif
+#ifndef FCX_DBG_NO_HEAD  // no crossing-record head stores
+#define FCX_DBG_NO_HEAD 0
+#endif
+
 namespace fcx {
 
 constexpr int kMaxTypes = FCX_MAX_SURFACE_TYPES;
@@ -153,11 +175,9 @@ int launch_pack_records(const AtmosArgs &a, int64_t n, bool aligned16, bool nont
 // Exchange -> atmosphere accumulation fused into the T=1 cells kernel.  The six fluxes it
 // can take from registers, in this order: MEVA HLAT HSEN RBBR UMOM VMOM (out[k] nullptr =
 // not accumulated).  Every 128-cell wave tile sums the segments that start in it; a
-// segment running past the tile end leaves its prefix sum for the next tile, whose head
-// cells continue it in link order: by default in the next tile's crossing record, which
-// atmos_fixup_kernel completes after the launch (no wave waits on another); with
-// FCX_OPT_CARRY_HANDOFF in carry[tile][k], published with write-through stores and
-// flag[tile] = epoch for the wave of the next tile inside the launch.
+// segment running past the tile end leaves its prefix sum in the next tile's crossing
+// record, whose head cells atmos_fixup_kernel adds after the launch in link order (no wave
+// ever waits on another).
 constexpr int kFusedFields = 6;
 constexpr int kRecHead = 4;     // head products kept per crossing record (longer heads: recomputed)
 constexpr int kXRec = 32;       // doubles per crossing record (256 B, two lines)
@@ -167,17 +187,13 @@ struct AtmosFused {
   const double *w;
   double *out[kFusedFields];
   const double *x[kFusedFields];  // the stored outputs (read by the fix-up only)
-  double *carry;       // [n_tiles][kFusedFields] (hand-off only)
-  uint32_t *flag;      // [n_tiles]: epoch of the run whose carry[tile] is published
-  uint32_t *err;       // set when a hand-off wait gave up (never in a correct run)
-  double *xrec;        // [n_tiles][kXRec] crossing records (handoff == 0, atmos_fixup_kernel):
+  double *xrec;        // [n_tiles][kXRec] crossing records (atmos_fixup_kernel):
                        // record t = the carry of tile t-1's last segment (doubles 0..5), the
                        // products w * x of tile t's first kRecHead head cells (6..29, cell-major)
                        // and {head cells, their atmosphere cell} of tile t (int2 at double 30);
                        // fp32 engines index the records by their 256-cell tiles
   int32_t xrec_on;     // some segment crosses a tile boundary: the launch fills the records
-  uint32_t epoch;      // this run's tag (never 0); the flags start at 0
-  int32_t handoff;     // 1: carries handed to the next tile's wave inside the launch
+  int32_t pad0;
   int64_t n_atmos;
   double *shared;
   int32_t stride, left, right;

@@ -327,72 +327,35 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
   // CMOM) are reloaded for every type, and the atmosphere-side inputs (PSUR PATM QATM TATM
   // UATM VATM AMOI AMOM, aliased into every surface type by distribute_input_field,
   // basic:334-358) are held across the types and reloaded only when a type binds another
-  // array (FCX_HOLD_SHARED).  Measured at T = 2 (profiles/r02/t2_reload_ab): the per-type
-  // reloads of the shared fields cost 8 % of the step (a build that skips them, wrong results,
-  // is the floor); holding them costs 36 VGPRs, so the multi-type fused kernels run 3 instead
-  // of 4 waves per SIMD and still gain 6-7 % per step (RCO stays at 4 waves).  Holding every
-  // input (FCX_HOLD_ACROSS_TYPES=1, round 1) kept ~56 VGPRs live and lost; reloading the shared
-  // fields with temporal loads (FCX_TEMPORAL_SHARED=1) hits L2 but is slower still.
-#ifndef FCX_HOLD_ACROSS_TYPES
-#define FCX_HOLD_ACROSS_TYPES 0
-#endif
-#ifndef FCX_TEMPORAL_SHARED
-#define FCX_TEMPORAL_SHARED 0
-#endif
-  constexpr bool kReload = TM == 0 && !FCX_HOLD_ACROSS_TYPES;
-// FCX_DBG_SKIP_SHARED=1 (A/B measurement builds only: WRONG results): an input whose pointer
-// equals the previous type's is not loaded again and reads as 0 -- the floor of removing the
-// shared reloads without holding anything.
-#ifndef FCX_DBG_SKIP_SHARED
-#define FCX_DBG_SKIP_SHARED 0
-#endif
+  // array (a wave-uniform pointer compare).  Measured at T = 2 (profiles/r02/t2_reload_ab):
+  // the per-type reloads of the shared fields cost 8 % of the step; holding them costs 36
+  // VGPRs, so the multi-type fused kernels run 3 instead of 4 waves per SIMD and still gain
+  // 6-7 % per step.  Holding every input (round 1) kept ~56 VGPRs live and lost.
+  // FCX_HOLD_SHARED = 0 (A/B): the atmosphere-side inputs are reloaded per type too.
 #ifndef FCX_HOLD_SHARED
 #define FCX_HOLD_SHARED 1
 #endif
-  // grp.member names the pointer in TypeParams (the next type's is compared when
-  // FCX_TEMPORAL_SHARED is on).  ATM: an atmosphere-side input (FCX_HOLD_SHARED).
-#define HOLDX(var, grp, member, ATM)                                                   \
-  {                                                                                    \
-    const double *ptr_ = tp.grp.member;                                                \
-    if constexpr (kReload && !(FCX_HOLD_SHARED && ATM)) {                              \
-      if (FCX_DBG_SKIP_SHARED && s > 0 && P->type[s - 1].grp.member == ptr_) {         \
-      } else if (ptr_) {                                                               \
-        if (FCX_TEMPORAL_SHARED && s + 1 < T && P->type[s + 1].grp.member == ptr_)     \
-          var = ld<C, false, R>(reinterpret_cast<const R *>(ptr_) + D_, j0, nt);       \
-        else                                                                           \
-          var = LD(ptr_, j0, nt);                                                      \
-      }                                                                                \
-    } else if (ptr_ && ptr_ != h_##var) {                                              \
-      var = LD(ptr_, j0, nt);                                                          \
-      h_##var = ptr_;                                                                  \
-    }                                                                                  \
+  constexpr bool kReload = TM == 0;  // bottom-side inputs: loaded per type
+  constexpr bool kHoldAtm = TM == 1 || FCX_HOLD_SHARED;
+  // grp.member names the pointer in TypeParams.  ATM: an atmosphere-side input.
+#define HOLDX(var, grp, member, ATM)                  \
+  {                                                   \
+    const double *ptr_ = tp.grp.member;               \
+    if constexpr (kReload && !(kHoldAtm && ATM)) {    \
+      if (ptr_) var = LD(ptr_, j0, nt);               \
+    } else if (ptr_ && ptr_ != h_##var) {             \
+      var = LD(ptr_, j0, nt);                         \
+      h_##var = ptr_;                                 \
+    }                                                 \
   }
 #define HOLD(var, grp, member) HOLDX(var, grp, member, false)
-// FCX_HOLD_MASK (A/B): which atmosphere-side inputs are held (bit 0 PSUR, 1 PATM, 2 QATM,
-// 3 TATM, 4 UATM, 5 VATM, 6 AMOI, 7 AMOM); the others are reloaded per type
-#ifndef FCX_HOLD_MASK
-#define FCX_HOLD_MASK 0xff
-#endif
-#define HOLDA(var, grp, member, bit) HOLDX(var, grp, member, ((FCX_HOLD_MASK >> (bit)) & 1))
-  constexpr bool kHoldAtm = !kReload || (TM == 0 && FCX_HOLD_SHARED);
-  constexpr bool kHoldAll = !kReload || (TM == 0 && FCX_HOLD_SHARED && (FCX_HOLD_MASK & 0xff) == 0xff);
-  constexpr bool kHoldWind = !kReload || (TM == 0 && FCX_HOLD_SHARED && (FCX_HOLD_MASK & 0x30) == 0x30);
+#define HOLDA(var, grp, member, bit) HOLDX(var, grp, member, true)
+  constexpr bool kHoldWind = kHoldAtm;
 
   for (int s = 0; s < T; ++s) {
     if constexpr (kReload) {  // no bottom-side input of the previous type stays live
       ts = fi = cmoi = chea = cmom = Vec<C, R>{};
       if constexpr (!kHoldAtm) ps = pa = qa = ta = u = v = amoi = amom = vel = Vec<C, R>{};
-      if constexpr (kHoldAtm && !kHoldAll) {  // the atmosphere-side inputs not held (A/B)
-        if constexpr (!(FCX_HOLD_MASK & 1)) ps = Vec<C, R>{};
-        if constexpr (!(FCX_HOLD_MASK & 2)) pa = Vec<C, R>{};
-        if constexpr (!(FCX_HOLD_MASK & 4)) qa = Vec<C, R>{};
-        if constexpr (!(FCX_HOLD_MASK & 8)) ta = Vec<C, R>{};
-        if constexpr (!(FCX_HOLD_MASK & 16)) u = Vec<C, R>{};
-        if constexpr (!(FCX_HOLD_MASK & 32)) v = Vec<C, R>{};
-        if constexpr (!(FCX_HOLD_MASK & 64)) amoi = Vec<C, R>{};
-        if constexpr (!(FCX_HOLD_MASK & 128)) amom = Vec<C, R>{};
-        if constexpr (!kHoldWind) vel = Vec<C, R>{};
-      }
     }
     const TypeParams &tp = P->type[s];
     const TGridPtrs &g = tp.t;
@@ -618,9 +581,6 @@ struct LdsEmitT {
   template <int CC, class R>
   __device__ __forceinline__ void operator()(int k, const Vec<CC, R> &x) const {
     static_assert(CC == C, "one emitter per cell width");
-#ifndef FCX_DBG_ATM_NOLDS  // A/B measurement builds only: no LDS products (sums of garbage)
-#define FCX_DBG_ATM_NOLDS 0
-#endif
     if (FCX_DBG_ATM_NOLDS) return;
     if constexpr (sizeof(R) == 4 && C == 4) {  // one 16-B store of the lane's four fluxes
       const int lane = threadIdx.x & 63;
@@ -661,55 +621,19 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb) {
 }
 
 // Where a finished segment sum goes: a segment that continues into the next tile leaves its
-// prefix as the carry of this tile -- published for the next tile's wave (hand-off, below)
-// or left for atmos_fixup_kernel; a complete one is the atmosphere value (and the boundary
-// slot of a first/last atmosphere cell shared with a neighbour rank).
+// prefix in the next tile's crossing record for atmos_fixup_kernel; a complete one is the
+// atmosphere value (and the boundary slot of a first/last atmosphere cell shared with a
+// neighbour rank).
 // R: the engine's output type (an fp32 engine's atmosphere outputs are float, rounded once)
-//
-// Hand-off ordering.  The carries and the flag are agent-scope atomics: each is a
-// `global_store/load ... sc1`, coherent across the XCDs at the memory side, so the only
-// question is order.  Producer: the carry stores, then s_waitcnt vmcnt(0) (every carry store
-// acknowledged by the coherence point), then the flag store; the compiler fences around the
-// wait keep the compiler from moving the stores across it.  Consumer: the flag poll loop
-// exits on the loaded value, so the carry loads issue only after the flag load returned
-// (a control dependency; the compiler fence keeps them behind the loop, and the GPU does
-// not issue loads speculatively).  The C++-model form of the same protocol (flag store
-// __ATOMIC_RELEASE, poll __ATOMIC_ACQUIRE, agent scope) compiles on gfx950 to a
-// `buffer_wbl2 sc1` (write-back of the XCD's whole L2) per published carry and a
-// `buffer_inv sc1` (invalidate of its L2) per taken one; FCX_HANDOFF_ACQREL=1 builds it
-// for the A/B measurement.
-#ifndef FCX_HANDOFF_ACQREL
-#define FCX_HANDOFF_ACQREL 0
-#endif
 template <class R>
 __device__ __forceinline__ void segment_done(const AtmosFused &af, int64_t tile, int32_t a, const double *acc,
                                              bool cont, bool nt_line = false) {
-  if (cont) {
-    if (!af.handoff) {  // the next tile's crossing record: the six prefix sums, 16-B stores
+  if (cont) {  // the next tile's crossing record: the six prefix sums, 16-B stores
 #pragma unroll
-      for (int q = 0; q < kFusedFields / 2; ++q)
-        reinterpret_cast<d2 *>(af.xrec + (tile + 1) * kXRec)[q] = d2{acc[2 * q], acc[2 * q + 1]};
-      return;
-    }
-#pragma unroll
-    for (int k = 0; k < kFusedFields; ++k)
-      if (af.out[k])
-        __hip_atomic_store(af.carry + tile * kFusedFields + k, acc[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (af.handoff) {
-      if (FCX_HANDOFF_ACQREL) {
-        __hip_atomic_store(af.flag + tile, af.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-      } else {
-        __atomic_signal_fence(__ATOMIC_SEQ_CST);
-        __builtin_amdgcn_s_waitcnt(0);  // the carry stores have completed before the flag is set
-        __atomic_signal_fence(__ATOMIC_SEQ_CST);
-        __hip_atomic_store(af.flag + tile, af.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
+    for (int q = 0; q < kFusedFields / 2; ++q)
+      reinterpret_cast<d2 *>(af.xrec + (tile + 1) * kXRec)[q] = d2{acc[2 * q], acc[2 * q + 1]};
     return;
   }
-#ifndef FCX_DBG_ATM_NOSTORE  // A/B measurement builds only: drop the atmosphere stores
-#define FCX_DBG_ATM_NOSTORE 0
-#endif
   if (FCX_DBG_ATM_NOSTORE) return;
 // Non-temporal atmosphere-output stores: 3 (default) for fp64 outputs, 1 all, 0 none, 2 only
 // the lines a tile owns whole.  Since the segment sums run in rounds, a round writes the
@@ -731,33 +655,6 @@ __device__ __forceinline__ void segment_done(const AtmosFused &af, int64_t tile,
     if (a == 0 && af.left >= 0) af.shared[(int64_t)af.left * af.stride + af.scol[k]] = acc[k];
     if (a == af.n_atmos - 1 && af.right >= 0) af.shared[(int64_t)af.right * af.stride + af.scol[k]] = acc[k];
   }
-}
-
-// The carry of `tile` published with this run's epoch.  Every wait ends: the producer of
-// tile - 1 is the previous block of the same XCD run (dispatched 8 blocks earlier, resident
-// or done) or, for the first tile of an XCD run, the last block of the previous run, which
-// the dispatcher reaches because at most 7 such waves wait at any time.  Should a flag never
-// come (a producer not resident, e.g. another process holding the CUs), the wait gives up
-// after ~2^20 polls (about a second) and raises af.err; the engine then recomputes the
-// atmosphere outputs with atmos_kernel at its next synchronisation (fcx_engine.hip,
-// check_handoff), so the results stay exact.
-__device__ __forceinline__ void take_carry(const AtmosFused &af, int64_t tile, double *acc) {
-  bool ok = false;
-  for (int it = 0; it < (1 << 20); ++it) {
-    if (__hip_atomic_load(af.flag + tile, FCX_HANDOFF_ACQREL ? __ATOMIC_ACQUIRE : __ATOMIC_RELAXED,
-                          __HIP_MEMORY_SCOPE_AGENT) == af.epoch) {
-      ok = true;
-      break;
-    }
-    __builtin_amdgcn_s_sleep(2);
-  }
-  if (!ok) __hip_atomic_store(af.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  __atomic_signal_fence(__ATOMIC_SEQ_CST);  // the carry loads stay behind the flag poll
-#pragma unroll
-  for (int k = 0; k < kFusedFields; ++k)
-    acc[k] = af.out[k] ? __hip_atomic_load(af.carry + tile * kFusedFields + k, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT)
-                       : 0.0;
 }
 
 // blocks per CU the multi-type (RAVG) fused kernel is compiled for: 3 -> <= 168 VGPRs, room
@@ -921,15 +818,12 @@ __global__ __launch_bounds__(64 * atmos_waves<C>(), RAVG ? FCX_RAVG_ATMOS_BLOCKS
         segment_done<R>(af, tile, a[i], acc, end == kT && next_a == a[i]);
       }
     }
-    // without the hand-off: the number of head cells (continuing the previous tile's
-    // segment) for atmos_fixup_kernel; 0 when the tile starts a segment
-    if (!af.handoff && af.xrec_on) {  // (a map whose segments never cross a tile needs no records)
+    // the number of head cells (continuing the previous tile's segment) for
+    // atmos_fixup_kernel; 0 when the tile starts a segment
+    if (af.xrec_on) {  // (a map whose segments never cross a tile needs no records)
       int head = kT;
 #pragma unroll
       for (int q = 0; q < C; ++q) head = min(head, C * first_bit(m[q]) + q);
-#ifndef FCX_DBG_NO_HEAD  // A/B measurement builds only (WRONG atmosphere values): no head stores
-#define FCX_DBG_NO_HEAD 0
-#endif
       if (FCX_DBG_NO_HEAD >= 2) head = 0;
       double *xr0 = af.xrec + tile * kXRec;
       if (lane == 0 && FCX_DBG_NO_HEAD < 2) *reinterpret_cast<int2 *>(xr0 + 30) = int2{head, a[0]};
@@ -951,23 +845,11 @@ __global__ __launch_bounds__(64 * atmos_waves<C>(), RAVG ? FCX_RAVG_ATMOS_BLOCKS
           reinterpret_cast<d2 *>(xr0 + kFusedFields + lane * kFusedFields)[q] = d2{hp[2 * q], hp[2 * q + 1]};
       }
     }
-    // hand-off: the segment the previous tile carried into this one is continued here, from
-    // its carry over this tile's products of the segment's cells, in link order
-    if (af.handoff && lane == 0 && a[0] >= 0 && a[0] == prev_tile) {
-      int end = kT;
-#pragma unroll
-      for (int q = 0; q < C; ++q) end = min(end, C * first_bit(m[q]) + q);
-      double acc[kFusedFields];
-      take_carry(af, tile - 1, acc);
-      for (int e = 0; e < end; ++e) add_cell(acc, e);
-      segment_done<R>(af, tile, a[0], acc, end == kT && next_a == a[0]);
-    }
     wave_sync();  // every lane is done reading before the next tile overwrites the region
   }
 }
 
-// Segments that straddle a tile boundary (the default, FCX_OPT_CARRY_HANDOFF = 0): the
-// launch leaves, in the crossing record of every tile t, the prefix sum of tile t-1's last
+// Segments that straddle a tile boundary: the launch leaves, in the crossing record of every tile t, the prefix sum of tile t-1's last
 // segment, the number of head cells of tile t (cells that continue that segment) with their
 // atmosphere cell, and the products of the first kRecHead of them; this kernel continues each
 // carry over the head cells, one thread per (tile, field), in link order: the same bits as

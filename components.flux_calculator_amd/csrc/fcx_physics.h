@@ -12,15 +12,15 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include "fcx_internal.h"
+
 namespace fcx {
 
-// FCX_TRIVIAL_MATH=1 (A/B measurement builds only, never the product): every formula returns
-// a plain sum of its inputs, so the kernels keep their loads, stores and accumulation but lose
-// the fp64 exp/log/sqrt/division work -- the streaming ceiling of the kernel's own structure.
-#ifndef FCX_TRIVIAL_MATH
-#define FCX_TRIVIAL_MATH 0
-#endif
-#define FCX_TRIVIAL(...)              \
+// FCX_TRIVIAL_MATH=1 (A/B measurement builds only, FCX_AB_BUILD, never the product; see
+// fcx_internal.h): every formula returns a plain sum of its inputs, so the kernels keep their
+// loads, stores and accumulation but lose the fp64 exp/log/sqrt/division work -- the
+// streaming ceiling of the kernel's own structure.
+#define FCX_TRIVIAL(...)            \
   if constexpr (FCX_TRIVIAL_MATH) {   \
     return __VA_ARGS__;               \
   }

@@ -20,9 +20,10 @@ MODULE fcx_c_api
   ! regridding matrices (enum fcx_regrid)
   INTEGER(c_int), PARAMETER :: FCX_U_TO_T = 0, FCX_V_TO_T = 1, FCX_T_TO_U = 2, FCX_T_TO_V = 3
   ! fcx_set_option (enum fcx_option)
-  INTEGER(c_int), PARAMETER :: FCX_OPT_NONTEMPORAL = 3, FCX_OPT_ATMOS_IN_RUN = 5, FCX_OPT_PIN_HOST = 6, &
+  INTEGER(c_int), PARAMETER :: FCX_OPT_NONTEMPORAL = 3, FCX_OPT_ATMOS_IN_RUN = 5, &
                                FCX_OPT_PIPELINE_CHUNKS = 7, FCX_OPT_ZERO_COPY = 9, FCX_OPT_TIMING = 10, &
-                               FCX_OPT_TILED_LAYOUT = 11, FCX_OPT_REMAP_PACK = 13, FCX_OPT_CARRY_HANDOFF = 14
+                               FCX_OPT_TILED_LAYOUT = 11, FCX_OPT_REMAP_PACK = 13, &
+                               FCX_OPT_HOST_STAGING = 15, FCX_OPT_HOST_THREADS = 16
   ! the RCCL unique id travels between the ranks as these many bytes (MPI_Bcast)
   INTEGER, PARAMETER :: FCX_COMM_ID_BYTES = 128
 
@@ -260,11 +261,11 @@ MODULE fcx_c_api
       INTEGER(c_int64_t), VALUE :: value
       INTEGER(c_int) :: fcx_set_option
     END FUNCTION
-    FUNCTION fcx_handoff_recoveries(engine, count) BIND(C, name='fcx_handoff_recoveries')
+    FUNCTION fcx_staging_bytes(engine, bytes) BIND(C, name='fcx_staging_bytes')
       IMPORT :: c_int, c_int64_t, c_ptr
       TYPE(c_ptr), VALUE :: engine
-      INTEGER(c_int64_t), INTENT(OUT) :: count
-      INTEGER(c_int) :: fcx_handoff_recoveries
+      INTEGER(c_int64_t), INTENT(OUT) :: bytes
+      INTEGER(c_int) :: fcx_staging_bytes
     END FUNCTION
     FUNCTION fcx_zero_copy_bytes(engine, bytes) BIND(C, name='fcx_zero_copy_bytes')
       IMPORT :: c_int, c_int64_t, c_ptr

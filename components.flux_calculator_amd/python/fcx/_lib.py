@@ -64,9 +64,8 @@ SIGNATURES = [
     ("fcx_device_ptr", _I, [_P, _I, _I, _I, _c.POINTER(_DP)]),
     ("fcx_device_layout", _I, [_P, _c.POINTER(_I64), _c.POINTER(_I64)]),
     ("fcx_last_kernel_ms", _I, [_P, _c.POINTER(_c.c_float)]),
-    ("fcx_pinned_bytes", _I, [_P, _P]),
+    ("fcx_staging_bytes", _I, [_P, _c.POINTER(_I64)]),
     ("fcx_algorithmic_bytes", _I, [_P, _I, _c.POINTER(_I64)]),
-    ("fcx_handoff_recoveries", _I, [_P, _c.POINTER(_I64)]),
     ("fcx_zero_copy_bytes", _I, [_P, _c.POINTER(_I64)]),
     ("fcx_host_malloc", _I, [_c.c_size_t, _c.POINTER(_P)]),
     ("fcx_set_atmos_boundaries", _I, [_P, _I32, _I32, _I32]),

@@ -163,9 +163,10 @@ class Engine:
         _lib.check(self.lib.fcx_algorithmic_bytes(self.h, phase, ctypes.byref(b)))
         return b.value
 
-    def pinned_bytes(self):
+    def staging_bytes(self):
+        """bytes of the page-locked staging arena of caller heap arrays (fcx_staging_bytes)"""
         b = ctypes.c_int64()
-        _lib.check(self.lib.fcx_pinned_bytes(self.h, ctypes.byref(b)))
+        _lib.check(self.lib.fcx_staging_bytes(self.h, ctypes.byref(b)))
         return b.value
 
     def zero_copy_bytes(self):
@@ -177,16 +178,9 @@ class Engine:
     def zero_copy_active(self):
         return self.zero_copy_bytes() > 0
 
-    def handoff_recoveries(self):
-        """fused accumulations recomputed after a carry hand-off timeout"""
-        c = ctypes.c_int64()
-        _lib.check(self.lib.fcx_handoff_recoveries(self.h, ctypes.byref(c)))
-        return c.value
-
     OPTIONS = {"cells_per_thread": 1, "max_blocks": 2, "nontemporal": 3, "specialize": 4,
-               "atmos_in_run": 5, "pin_host": 6, "pipeline_chunks": 7,
-               "pipeline_min_chunk": 8, "zero_copy": 9,
-               "timing": 10, "tiled_layout": 11, "test_handoff_timeout": 12, "remap_pack": 13, "carry_handoff": 14}
+               "atmos_in_run": 5, "pipeline_chunks": 7, "pipeline_min_chunk": 8, "zero_copy": 9,
+               "timing": 10, "tiled_layout": 11, "remap_pack": 13, "host_staging": 15, "host_threads": 16}
 
     def run_atmos(self, phase=PHASE_ALL):
         _lib.check(self.lib.fcx_run_atmos(self.h, phase))

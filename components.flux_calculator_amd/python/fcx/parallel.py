@@ -168,7 +168,10 @@ class PeriodicAtmosMap:
             tot += np.where((k < length) & (y < n_global), self.area(y), 0.0)
         return self.area(x) / tot
 
-    def local(self, offset, size, rank, nranks, n_global):
+    def local(self, offset, size, rank, nranks, n_global, right_slot=None):
+        """right_slot: the boundary slot after this rank's cells (default `rank`; with empty
+        ranks in the decomposition, the next rank with cells minus one, as task_ranges)."""
+        right_slot = rank if right_slot is None else right_slot
         x = np.arange(offset, offset + size, dtype=np.int64)
         gi = self.index(x)
         if size == 0:
@@ -176,7 +179,7 @@ class PeriodicAtmosMap:
         a0, a1 = int(gi[0]), int(gi[-1])
         left = rank - 1 if (offset > 0 and int(self.index(offset - 1)) == a0) else -1
         end = offset + size
-        right = rank if (end < n_global and int(self.index(end)) == a1) else -1
+        right = right_slot if (end < n_global and int(self.index(end)) == a1) else -1
         return LocalAtmos(offset, size, a0, a1 - a0 + 1, np.ascontiguousarray(gi - a0, dtype=np.int32),
                           np.ascontiguousarray(self.weight(x, n_global)), left, right, max(nranks - 1, 0))
 
@@ -223,7 +226,9 @@ class BlockedRandomAtmosMap:
         s = lo - b0 * self.BLOCK
         return idx[s: s + (hi - lo)], w[s: s + (hi - lo)]
 
-    def local(self, offset, size, rank, nranks, n_global):
+    def local(self, offset, size, rank, nranks, n_global, right_slot=None):
+        """right_slot: as PeriodicAtmosMap.local."""
+        right_slot = rank if right_slot is None else right_slot
         if size == 0:
             return LocalAtmos(offset, 0, 0, 0, np.zeros(0, np.int32), np.zeros(0), -1, -1, max(nranks - 1, 0))
         lo, hi = max(offset - 1, 0), min(offset + size + 1, n_global)  # one neighbour cell each side
@@ -232,7 +237,7 @@ class BlockedRandomAtmosMap:
         g, wm = gi[mine], w[mine]
         a0, a1 = int(g[0]), int(g[-1])
         left = rank - 1 if (offset > 0 and int(gi[0]) == a0) else -1
-        right = rank if (offset + size < n_global and int(gi[-1]) == a1) else -1
+        right = right_slot if (offset + size < n_global and int(gi[-1]) == a1) else -1
         return LocalAtmos(offset, size, a0, a1 - a0 + 1, np.ascontiguousarray(g - a0, dtype=np.int32),
                           np.ascontiguousarray(wm), left, right, max(nranks - 1, 0))
 

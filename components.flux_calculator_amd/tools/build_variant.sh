@@ -5,7 +5,7 @@ set -e
 HERE="$(cd "$(dirname "$0")/.." && pwd)"
 OUT="$1"; shift
 mkdir -p "$OUT/obj"
-FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function -I$HERE/csrc -I$HERE/../include"
+FLAGS="-DFCX_AB_BUILD --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function -I$HERE/csrc -I$HERE/../include"
 /opt/rocm/bin/hipcc $FLAGS "$@" -c "$HERE/csrc/fcx_kernels.hip" -o "$OUT/obj/fcx_kernels.o" &
 /opt/rocm/bin/hipcc $FLAGS "$@" -c "$HERE/csrc/fcx_engine.hip" -o "$OUT/obj/fcx_engine.o" &
 wait

@@ -132,11 +132,9 @@ int fcx_run(fcx_engine *e, int phase, int32_t current_step_time); /* device comp
 int fcx_download(fcx_engine *e, int phase); /* D2H of host-bound outputs of the phase */
 /* the three above; with host-bound fields pipelined over cell chunks (FCX_OPT_PIPELINE_CHUNKS) */
 int fcx_step(fcx_engine *e, int phase, int32_t current_step_time);
-/* waits for the engine's stream.  With FCX_OPT_CARRY_HANDOFF = 1 (not the default): a fused
- * accumulation whose in-launch carry hand-off timed out since the last check (a producer
- * wave that was not resident, e.g. another process holding the GPU) is recomputed here by
- * the separate accumulation kernel (bit-identical results, host copies refreshed) and
- * counted (fcx_handoff_recoveries); fcx_step does the same. */
+/* waits for the engine's stream; the caller's host arrays hold the downloaded outputs once it
+ * returns (caller heap arrays are filled from the engine's staging arena here,
+ * FCX_OPT_HOST_STAGING).  fcx_step and the per-call subroutines end with it. */
 int fcx_synchronize(fcx_engine *e);
 
 /* ---- per call: the reference subroutines one by one (exact drop-in semantics; each
@@ -163,10 +161,8 @@ int fcx_device_layout(fcx_engine *e, int64_t *tile, int64_t *tile_stride);
 /* device time (hipEvents on the engine stream) of the kernels of the last fcx_run;
    needs FCX_OPT_TIMING = 1 */
 int fcx_last_kernel_ms(fcx_engine *e, float *ms);
-/* bytes of caller host memory page-locked by this engine (FCX_OPT_PIN_HOST) */
-int fcx_pinned_bytes(fcx_engine *e, int64_t *bytes);
-/* fused accumulations recomputed after a carry hand-off timeout (fcx_synchronize) */
-int fcx_handoff_recoveries(fcx_engine *e, int64_t *count);
+/* bytes of the engine's page-locked staging arena for caller heap arrays (0: none) */
+int fcx_staging_bytes(fcx_engine *e, int64_t *bytes);
 /* bytes of host arrays the kernels use in place (FCX_OPT_ZERO_COPY) */
 int fcx_zero_copy_bytes(fcx_engine *e, int64_t *bytes);
 /* algorithmic HBM bytes of one fcx_run(phase) (each distinct array read once, written once) */
@@ -254,12 +250,6 @@ enum fcx_option {
   FCX_OPT_NONTEMPORAL = 3,      /* non-temporal hint on streamed loads/stores (default 1) */
   FCX_OPT_SPECIALIZE = 4,       /* T=1 CCLM/MOM5/RCO specialised kernels (default 1)      */
   FCX_OPT_ATMOS_IN_RUN = 5,     /* fcx_run also runs the atmosphere accumulation (def. 1) */
-  FCX_OPT_PIN_HOST = 6,         /* hipHostRegister the caller's heap arrays at fcx_commit,
-                                   so their copies run as direct DMA (default 0: on ROCm
-                                   7.x, DMA and kernel access through registered heap ranges
-                                   faulted or read a neighbouring page in long test runs;
-                                   arrays from fcx_host_malloc are page-locked by the
-                                   library and need no registration)                      */
   FCX_OPT_PIPELINE_CHUNKS = 7,  /* fcx_step of host-bound fields: H2D/compute/D2H overlap
                                    over this many cell chunks (default 8; 1 = sequential) */
   FCX_OPT_PIPELINE_MIN_CHUNK = 8, /* ... of at least this many cells (multiple of 1024;
@@ -271,17 +261,17 @@ enum fcx_option {
                                    Caller heap arrays always take device mirrors */
   FCX_OPT_TIMING = 10,          /* record the events behind fcx_last_kernel_ms (default 0:
                                    two event records per run cost ~8 us on small grids) */
-  FCX_OPT_TEST_HANDOFF_TIMEOUT = 12, /* test hook (default 0): report every fused launch's
-                                   carry hand-off as timed out, so that the recovery of
-                                   fcx_synchronize (atmos_kernel recomputes the atmosphere
-                                   outputs) runs; the results must be unchanged            */
-  FCX_OPT_CARRY_HANDOFF = 14,   /* fused accumulation, segments crossing a 128-cell wave
-                                   tile: 0 (default) the launch leaves each carry and tile
-                                   head count, atmos_fixup_kernel completes them after it
-                                   (one small launch, none when no segment crosses a tile);
-                                   1: the next tile's wave waits for the carry inside the
-                                   launch (spin-wait on a flag; measured 1.5x slower per
-                                   step on a map whose segments cross tiles)               */
+  FCX_OPT_HOST_STAGING = 15,    /* caller heap arrays (not fcx_host_malloc memory) reach
+                                   their device mirrors through an engine-owned page-locked
+                                   staging arena laid out like the mirrors: host threads copy
+                                   the arrays into it, then ONE DMA per pool and direction
+                                   (per chunk when pipelined), and back.  1 (default); 0:
+                                   one runtime copy per array (pageable, staged by HIP).
+                                   Nothing of the caller's memory is ever page-locked or
+                                   mapped.  Applied at fcx_commit                          */
+  FCX_OPT_HOST_THREADS = 16,    /* host threads of those copies (the calling thread
+                                   included); 0 (default): min(8, OMP_NUM_THREADS if set,
+                                   else the CPUs of the process affinity set)              */
   FCX_OPT_REMAP_PACK = 13,      /* exchange -> model remaps: the fields of a launch packed
                                    cell-major into one record per exchange cell before the
                                    gather, so a link reads one record instead of nf

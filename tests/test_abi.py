@@ -156,9 +156,11 @@ def test_set_precision_validates():
     lib.fcx_destroy(h)
 
 
-def test_remap_and_carry_options_before_commit():
-    """FCX_OPT_REMAP_PACK (13: 0 never, 1 always, 2 auto) and FCX_OPT_CARRY_HANDOFF (14) are
-    validated without a GPU; fcx_remap_info is only answered after fcx_commit."""
+def test_remap_and_staging_options_before_commit():
+    """FCX_OPT_REMAP_PACK (13: 0 never, 1 always, 2 auto), FCX_OPT_HOST_STAGING (15) and
+    FCX_OPT_HOST_THREADS (16: 0..64) are validated without a GPU; the options removed in
+    round 3 (6 page-locking of caller memory, 12/14 the in-launch carry hand-off) are
+    unknown; fcx_remap_info is only answered after fcx_commit."""
     lib = _lib.load()
     h = ctypes.c_void_p()
     gs = (ctypes.c_int32 * 3)(16, 16, 16)
@@ -166,8 +168,14 @@ def test_remap_and_carry_options_before_commit():
     for v in (0, 1, 2):
         _lib.check(lib.fcx_set_option(h, 13, v))
     assert lib.fcx_set_option(h, 13, 3) == 1  # FCX_E_ARG
-    _lib.check(lib.fcx_set_option(h, 14, 1))
-    _lib.check(lib.fcx_set_option(h, 14, 0))
+    for v in (0, 1):
+        _lib.check(lib.fcx_set_option(h, 15, v))
+    for v in (0, 1, 8, 64):
+        _lib.check(lib.fcx_set_option(h, 16, v))
+    assert lib.fcx_set_option(h, 16, 65) == 1
+    assert lib.fcx_set_option(h, 16, -1) == 1
+    for gone in (6, 12, 14):
+        assert lib.fcx_set_option(h, gone, 1) == 1
     src = np.arange(16, dtype=np.int32)
     dst = src % 4
     w = np.ones(16)

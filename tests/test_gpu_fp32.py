@@ -198,13 +198,13 @@ def test_fp32_engine_rejects_fp64_outputs():
 # run lengths: 1..7 and 40..64 (the fp32 fused kernel, 256-cell wave tiles: segments within
 # a tile or crossing one boundary), 1..400 (longer than half a 128-cell tile: atmos_kernel)
 @pytest.mark.parametrize("lengths", [(1, 5), (1, 7), (40, 64), (1, 400)])
-@pytest.mark.parametrize("mode", ["handoff", "fixup", "capped", "pipelined"])
+@pytest.mark.parametrize("mode", ["fixup", "capped", "pipelined", "pipelined_runtime"])
 @pytest.mark.parametrize("variant", ["CCLM", "MOM5", "RCO"])
 def test_fp32_fused_accumulation(variant, mode, lengths):
     """The fp32 engine's flux kernel with the accumulation fused in (4 cells per lane,
-    products and sums in fp64, outputs rounded once): carries handed between 256-cell tiles
-    inside the launch, across the chunk launches of the pipelined step, and the separate
-    kernel under a grid-stride cap.  Bit-identical to the sequential fp64 sum of the GPU's own
+    products and sums in fp64, outputs rounded once): carries between 256-cell tiles completed
+    by the fix-up kernel, across the chunk launches of the pipelined step (staging arena, and
+    one runtime copy per array), and the separate kernel under a grid-stride cap.  Bit-identical to the sequential fp64 sum of the GPU's own
     fp32 fluxes, rounded once; the fluxes within the fp32 gate of the oracle."""
     from fcx.parallel import local_atmos
     from test_gpu_multirank import random_run_map
@@ -215,11 +215,12 @@ def test_fp32_fused_accumulation(variant, mode, lengths):
     amap = random_run_map(n, lengths, seed=lengths[1] + 5)
     la = local_atmos(amap, 0, 1)
     outs = {k: np.full(la.n_atmos, np.nan, np.float32) for k, _ in ATM_FIELDS}
-    opts = {"handoff": {"carry_handoff": 1}, "fixup": {}, "capped": {"max_blocks": 64},
-            "pipelined": {"pipeline_chunks": 4, "pipeline_min_chunk": 65536, "zero_copy": 0}}[mode]
+    pipe = {"pipeline_chunks": 4, "pipeline_min_chunk": 65536, "zero_copy": 0}
+    opts = {"fixup": {}, "capped": {"max_blocks": 64}, "pipelined": pipe,
+            "pipelined_runtime": {**pipe, "host_staging": 0}}[mode]
     eng = Engine(c32.lf, 1, c32.methods, corrections=c32.corrections,
                  atmos={"local": la, "fields": [(2, 1, g, k, outs[k]) for k, g in ATM_FIELDS]}, options=opts)
-    for step in range(2):  # later runs' epochs must not see stale flags
+    for step in range(2):  # later runs reuse the crossing records
         for o in outs.values():
             o[:] = np.nan
         eng.step(PHASE_ALL, STEP_T + 3600 * step)

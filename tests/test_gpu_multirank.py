@@ -83,12 +83,12 @@ def random_run_map(n, lengths, seed):
 # boundary; heads longer than the fix-up's kHeadCells = 16 kept products are recomputed);
 # 130..140 and 1..400 (longer than half a tile: the engine runs atmos_kernel instead)
 @pytest.mark.parametrize("lengths", [(1, 5), (1, 7), (20, 64), (130, 140), (1, 400)])
-@pytest.mark.parametrize("mode", ["handoff", "fixup", "capped", "pipelined"])
+@pytest.mark.parametrize("mode", ["fixup", "capped", "pipelined", "pipelined_runtime"])
 def test_fused_accumulation_long_segments(lengths, mode):
-    """The accumulation with segments crossing 128-cell wave tiles: carries handed to the next
-    tile's wave inside the launch (default one-trip grid), left to the fix-up kernel (a
-    grid-stride cap), and across the chunk launches of the pipelined host step; long
-    segments through atmos_kernel.  Bit-identical to the sequential sum of the GPU's own
+    """The accumulation with segments crossing 128-cell wave tiles: carries left to the fix-up
+    kernel (default one-trip grid, and a grid-stride cap), and across the chunk launches of
+    the pipelined host step (through the staging arena, and with one runtime copy per array);
+    long segments through atmos_kernel.  Bit-identical to the sequential sum of the GPU's own
     fluxes."""
     import torch
     from fcx.engine import Engine
@@ -101,10 +101,11 @@ def test_fused_accumulation_long_segments(lengths, mode):
     outs = {name: torch.full((la.n_atmos,), float("nan"), dtype=torch.float64, device="cuda:0")
             for name, _ in FIELDS}
     atmos = {"local": la, "fields": [(2, 1, g, name, outs[name]) for name, g in FIELDS]}
-    opts = {"handoff": {"carry_handoff": 1}, "fixup": {}, "capped": {"max_blocks": 64},
-            "pipelined": {"pipeline_chunks": 4, "pipeline_min_chunk": 65536, "zero_copy": 0}}[mode]
+    pipe = {"pipeline_chunks": 4, "pipeline_min_chunk": 65536, "zero_copy": 0}
+    opts = {"fixup": {}, "capped": {"max_blocks": 64}, "pipelined": pipe,
+            "pipelined_runtime": {**pipe, "host_staging": 0}}[mode]
     eng = Engine(case.lf, 1, case.methods, corrections=case.corrections, atmos=atmos, options=opts)
-    for step in range(3):  # the epochs of later runs must not see stale flags
+    for step in range(3):  # later runs reuse the crossing records
         for o in outs.values():
             o.fill_(float("nan"))
         eng.step(PHASE_ALL, 3600 * step)
@@ -113,40 +114,6 @@ def test_fused_accumulation_long_segments(lengths, mode):
             gpu_flux = np.asarray(case.lf.field[(1, g, name)])
             want = oracle_lib.atmos_accumulate(amap.atmos_index, amap.weight, gpu_flux, amap.n_atmos)
             np.testing.assert_array_equal(outs[name].cpu().numpy(), want, err_msg=f"{name} step {step}")
-    eng.close()
-
-
-@pytest.mark.parametrize("host_outputs", [False, True])
-def test_handoff_timeout_recovery(host_outputs):
-    """A carry hand-off that gives up (forced by the FCX_OPT_TEST_HANDOFF_TIMEOUT hook) is
-    recovered at the synchronisation: atmos_kernel recomputes the atmosphere outputs from
-    the stored fluxes, bit-identical to the sequential sum; host outputs are refreshed."""
-    import torch
-    from fcx.engine import Engine
-
-    n = 70_001
-    case = build_case("MOM5", n=n, T=1, bias=True, seed=23)
-    amap = random_run_map(n, (1, 7), seed=3)
-    la = local_atmos(amap, 0, 1)
-    if host_outputs:
-        outs = {name: np.full(la.n_atmos, np.nan) for name, _ in FIELDS}
-    else:
-        outs = {name: torch.full((la.n_atmos,), float("nan"), dtype=torch.float64, device="cuda:0")
-                for name, _ in FIELDS}
-    atmos = {"local": la, "fields": [(2, 1, g, name, outs[name]) for name, g in FIELDS]}
-    eng = Engine(case.lf, 1, case.methods, corrections=case.corrections, atmos=atmos,
-                 options={"test_handoff_timeout": 1, "carry_handoff": 1})
-    for step in range(2):
-        for o in outs.values():
-            o[:] = float("nan")
-        eng.step(PHASE_ALL, 3600 * step)
-        torch.cuda.synchronize()
-        assert eng.handoff_recoveries() == step + 1
-        for name, g in FIELDS:
-            gpu_flux = np.asarray(case.lf.field[(1, g, name)])
-            want = oracle_lib.atmos_accumulate(amap.atmos_index, amap.weight, gpu_flux, amap.n_atmos)
-            got = outs[name] if host_outputs else outs[name].cpu().numpy()
-            np.testing.assert_array_equal(got, want, err_msg=f"{name} step {step}")
     eng.close()
 
 

@@ -1,9 +1,10 @@
-"""The host-bound fcx_step: caller arrays copied through the runtime's staging (default),
-page-locked at commit (FCX_OPT_PIN_HOST, opt-in) or in library memory, and the step pipelined over cell chunks (FCX_OPT_PIPELINE_CHUNKS: H2D of chunk k+1, kernel of chunk k,
-D2H of chunk k-1 on three streams).  Every chunking must give the bits of the sequential
-upload/run/download step, and those are within tests/parity.py of the oracle."""
-import os
-
+"""The host-bound fcx_step: caller heap arrays through the engine's page-locked staging arena
+(FCX_OPT_HOST_STAGING, default) or one runtime copy per array, arrays in library memory
+(fcx_host_malloc, direct DMA or zero-copy), and the step pipelined over cell chunks
+(FCX_OPT_PIPELINE_CHUNKS: H2D of chunk k+1, kernel of chunk k, D2H of chunk k-1 on three
+streams, the staging copies of chunk k+1 and k-2 on the host in between).  Every transport
+and chunking must give the bits of the sequential upload/run/download step, and those are
+within tests/parity.py of the oracle."""
 import numpy as np
 import pytest
 
@@ -18,11 +19,6 @@ from fcx.parallel import local_atmos, synthetic_atmos_map  # noqa: E402
 from fcx.synthetic import build_case  # noqa: E402
 
 STEP_T = 3600 * 24 * 40
-# hipHostRegister of caller heap ranges (FCX_OPT_PIN_HOST=1) is opt-in: in a long suite run a
-# DMA through such a registration faulted (illegal memory access), and a
-# fault poisons the whole process.  Its tests run on request.
-pin_host_tests = pytest.mark.skipif(not os.environ.get("FCX_TEST_PIN_HOST"),
-                                    reason="FCX_OPT_PIN_HOST is opt-in; FCX_TEST_PIN_HOST=1 runs its tests")
 
 
 def library(case):
@@ -68,9 +64,10 @@ def same_bits(a, b):
 @pytest.mark.parametrize("variant", ["CCLM", "RCO"])
 def test_pipeline_chunkings_bit_identical(variant):
     case = build_case(variant, n=100_003, T=1, bias=True)
-    seq = run(case, {"pipeline_chunks": 1, "pin_host": 0})
+    seq = run(case, {"pipeline_chunks": 1})
     for chunks in (2, 3, 8, 97):
         same_bits(run(case, {"pipeline_chunks": chunks}), seq)
+        same_bits(run(case, {"pipeline_chunks": chunks, "host_staging": 0}), seq)
     ref = oracle_lib.run_case(case, "c", current_step_time=STEP_T)
     assert_parity(seq, ref, label=variant)
 
@@ -88,34 +85,51 @@ def test_pipeline_generic_kernel_separate_grids_and_averages():
     case = build_case("CCLM", n=20_011, T=3, sep_grids=(19_997, 20_101), bias=True)
     seq = run(case, {"pipeline_chunks": 1})
     same_bits(run(case, {"pipeline_chunks": 5}), seq)
-    same_bits(run(case, {"pipeline_chunks": 5, "pin_host": 0}), seq)
+    same_bits(run(case, {"pipeline_chunks": 5, "host_staging": 0}), seq)
+    same_bits(run(case, {"pipeline_chunks": 5, "tiled_layout": 0}), seq)  # plain mirror pool
     ref = oracle_lib.run_case(case, "c", current_step_time=STEP_T)
     assert_parity(seq, ref, label="T3 sep")
 
 
-@pin_host_tests
-def test_pinned_small_arrays_sharing_pages():
-    """Many small arrays (several per page): merged page ranges are registered once."""
-    case = build_case("CCLM", n=3_000, T=2, bias=True)
-    a = run(case, {"pipeline_chunks": 2, "pin_host": 1})
-    b = run(case, {"pipeline_chunks": 1, "pin_host": 0})
+@pytest.mark.parametrize("n", [3_000, 32_768])
+@pytest.mark.parametrize("atmos", [False, True])
+def test_staging_matches_runtime_copies(n, atmos):
+    """The Baltic-size step (32,768 cells) and small arrays several to a heap page (3,000
+    cells, T = 2): the staging arena gives the bits of one runtime copy per array, with the
+    atmosphere outputs staged too; only the staged engine holds an arena."""
+    case = build_case("CCLM", n=n, T=2 if n < 10_000 else 1, bias=True)
+    a = run(case, {"pipeline_chunks": 2}, atmos_n=n if atmos else None)
+    b = run(case, {"pipeline_chunks": 1, "host_staging": 0}, atmos_n=n if atmos else None)
     same_bits(a, b)
+    eng = Engine(case.lf, case.num_surface_types, case.methods, corrections=case.corrections,
+                 averages=case.averages)
+    assert eng.staging_bytes() > 0
+    eng.close()
+    eng = Engine(case.lf, case.num_surface_types, case.methods, corrections=case.corrections,
+                 averages=case.averages, options={"host_staging": 0})
+    assert eng.staging_bytes() == 0
+    eng.close()
 
 
-@pin_host_tests
-def test_page_lock_registry_shared_and_conflicting_engines():
-    """Page-locked ranges are process-wide and page-exclusive: a second live engine over the
-    same arrays shares the registration (reference count), one whose small arrays sit on the
-    same heap pages stays pageable, and closing engines in either order leaves the others
-    correct and unregisters the pages exactly once."""
+@pytest.mark.parametrize("threads", [1, 3, 8])
+def test_staging_host_threads(threads):
+    """The arena's host copies on 1, 3 or 8 threads: the same bits."""
+    case = build_case("MOM5", n=40_001, T=1, bias=True)
+    same_bits(run(case, {"host_threads": threads}), run(case, {"host_staging": 0}))
+
+
+def test_engines_sharing_heap_arrays_and_pages():
+    """Two live engines over the same heap arrays and a third whose small arrays sit on the
+    same heap pages, each with its own arena, closed in every order: every remaining engine
+    stays correct (nothing of the caller's memory is locked or mapped, so nothing is shared
+    between them but the arrays)."""
     a = build_case("CCLM", n=2_001, T=2, bias=True)
     b = build_case("CCLM", n=2_001, T=2, bias=True)  # allocated right after: shares pages
-    ref_a = run(a, {"pin_host": 0})
-    ref_b = run(b, {"pin_host": 0})
+    ref_a = run(a, {"host_staging": 0})
+    ref_b = run(b, {"host_staging": 0})
 
     def engine(case):
-        return Engine(case.lf, 2, case.methods, corrections=case.corrections,
-                      averages=case.averages, options={"pin_host": 1})
+        return Engine(case.lf, 2, case.methods, corrections=case.corrections, averages=case.averages)
 
     def step(eng, case):
         for k in case.outputs:
@@ -125,8 +139,6 @@ def test_page_lock_registry_shared_and_conflicting_engines():
 
     for close_first in (0, 1, 2):
         e = [engine(a), engine(a), engine(b)]
-        assert e[0].pinned_bytes() > 0
-        assert e[1].pinned_bytes() == e[0].pinned_bytes()  # the same ranges, shared
         e[close_first].close()
         for i, (eng, case, ref) in enumerate(((e[0], a, ref_a), (e[1], a, ref_a), (e[2], b, ref_b))):
             if i != close_first:
@@ -134,10 +146,26 @@ def test_page_lock_registry_shared_and_conflicting_engines():
         for i in range(3):
             if i != close_first:
                 e[i].close()
-    e = engine(a)  # everything unregistered: pinning works again from scratch
-    assert e.pinned_bytes() > 0
-    same_bits(step(e, a), ref_a)
-    e.close()
+
+
+def test_upload_run_download_synchronize():
+    """The split step: outputs reach the caller's arrays at fcx_synchronize; an upload issued
+    while a download still owes its host copies completes that download first."""
+    case = build_case("RCO", n=20_011, T=1, bias=True)
+    want = run(case, {"host_staging": 0})
+    for k in case.outputs:
+        case.lf.field[k][:] = np.nan
+    eng = Engine(case.lf, 1, case.methods, corrections=case.corrections, averages=case.averages)
+    for rep in range(2):
+        eng.upload(PHASE_ALL)
+        eng.run(PHASE_ALL, STEP_T)
+        eng.download(PHASE_ALL)
+        if rep == 1:
+            eng.synchronize()
+        else:
+            eng.upload(PHASE_ALL)  # no synchronize in between: the download is completed here
+        same_bits({k: np.array(case.lf.field[k], copy=True) for k in case.outputs}, want)
+    eng.close()
 
 
 def test_default_min_chunk_keeps_small_grids_sequential():
@@ -183,6 +211,18 @@ def steps_with_changing_inputs(case, options, steps=3):
 
 
 @pytest.mark.parametrize("variant", ["CCLM", "MOM5", "RCO"])
+def test_staged_steps_see_fresh_inputs(variant):
+    """Heap arrays through the staging arena over several steps, the host rewriting the inputs
+    between them: each step gathers the current host values."""
+    case = build_case(variant, n=40_001, T=1, bias=True)
+    staged = steps_with_changing_inputs(case, {})
+    direct = steps_with_changing_inputs(case, {"host_staging": 0})
+    for a, b in zip(staged, direct):
+        same_bits(a, b)
+    assert not any(np.isnan(v).any() for v in staged[-1].values())
+
+
+@pytest.mark.parametrize("variant", ["CCLM", "MOM5", "RCO"])
 def test_zero_copy_matches_mirrors_over_steps(variant):
     case = build_case(variant, n=40_001, T=1, bias=True)
     arena = library(case)
@@ -219,7 +259,7 @@ def test_zero_copy_per_call_dropin():
         case.lf.field[k][:] = np.nan
     eng = Engine(case.lf, 2, case.methods, corrections=case.corrections, averages=case.averages,
                  options={"zero_copy": 1})
-    assert eng.zero_copy_bytes() > 0 and eng.pinned_bytes() == 0
+    assert eng.zero_copy_bytes() > 0 and eng.staging_bytes() == 0
     lib, h = eng.lib, eng.h
     assert lib.fcx_calc_flux_radiation_blackbody(h) == 0
     for g in (1, 2, 3):

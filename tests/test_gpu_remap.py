@@ -245,3 +245,34 @@ def test_remap_records_from_the_flux_launch(variant, atmos, host):
         for name, g in names:
             want = oracle_lib.atmos_accumulate(amap.atmos_index, amap.weight, flux(name, g), amap.n_atmos)
             np.testing.assert_array_equal(atm[name], want, err_msg=f"atmos {name}")
+
+
+@pytest.mark.parametrize("change", [("specialize", 0), ("cells_per_thread", 1)])
+def test_launch_options_changed_after_runs(change):
+    """A remap engine whose records the T=1 flux launch writes (specialize=1, two cells per
+    lane): switching the launch options after runs drops the cached plans, so the next run
+    takes the generic kernel and the packing pass with the same bits, and switching back
+    returns to the records."""
+    n = 30_011
+    case = build_case("CCLM", n=n, T=1, bias=True)
+    mmap = synthetic_model_map(n, 2_000, links_per_cell=2)
+    outs = {k: np.full(mmap.n_model, np.nan) for k, _ in FIELDS}
+    eng = Engine(case.lf, 1, case.methods, corrections=case.corrections, remaps=[remap_spec(mmap, outs)],
+                 options={"remap_pack": 1})
+    res = []
+    for setting in (None, change[1], 1 if change[0] == "specialize" else 2):
+        if setting is not None:
+            eng.set_option(change[0], setting)
+        for o in outs.values():
+            o[:] = np.nan
+        eng.step(PHASE_ALL, STEP_T)
+        res.append(({k: o.copy() for k, o in outs.items()}, eng.remap_info(0)[1]))
+    eng.close()
+    assert [p for _, p in res] == [2, 1, 2]  # records from the flux launch / packing pass / flux launch
+    for got, _ in res[1:]:
+        for k in outs:
+            np.testing.assert_array_equal(got[k], res[0][0][k], err_msg=k)
+    for name, g in FIELDS:
+        want = oracle_lib.remap_apply(mmap.src, mmap.dst, mmap.weight, np.asarray(case.lf.field[(1, g, name)]),
+                                      mmap.n_model)
+        np.testing.assert_array_equal(res[0][0][name], want, err_msg=name)

@@ -1,22 +1,29 @@
-"""Host memory transports and the page-lock registry, each hazard forced deterministically
-(DESIGN.md section 5).
+"""Host memory transports, each hazard forced deterministically.
 
-Kernels used caller heap arrays in place (zero-copy through hipHostRegister mappings) until
-round 2; twice that lost data: round 1 a MEVA whose stores never reached the host array,
-round 2 an HLAT computed from MEVA read one 4 KiB page off (cells 2414.. got the values of
-cells 2926..).  Kernels now use only library-allocated memory (fcx_host_malloc) in place;
-caller heap arrays take device mirrors fed by DMA from their page-locked ranges.  Set up
-here on purpose:
+Until round 2 the engine reached caller heap memory through hipHostRegister: kernels used
+registered arrays in place, later only DMAs did, and a process-wide registry shared one
+registration between engines that asked for the same virtual byte range.  Three wrong
+results came out of that (round 1: MEVA stores that never reached the host array; round 2:
+an HLAT computed from MEVA one 4 KiB page off; an illegal memory access in a DMA out of
+fresh heap arrays).  A registration pins the physical pages behind a range at the moment it
+is made, while everything that looks it up -- the registry, the runtime's own map of host
+memory -- goes by virtual address; once the allocation behind the range is freed and its
+address handed out again (glibc reuses a freed mapping of the same size at the same
+address), a lookup by address finds a registration of pages that no longer back it.  Since
+round 3 nothing of the caller's memory is registered or mapped: heap arrays move through the
+engine's own page-locked staging arena, read and written by host copies at the arrays'
+virtual addresses at every step.  Set up here on purpose:
 
-  * an output whose page meets another live engine's registration (it stays pageable:
-    staged copies), before and after that engine is closed;
+  * the virtual address of live engines' arrays unmapped and mapped again with new contents
+    (MAP_FIXED) before a second engine binds the same addresses;
+  * an output whose page meets another live engine's arrays, before and after that engine
+    is closed;
   * an engine dropped without close() and collected by the garbage collector between the
     commit and the step of a new engine over fresh arrays;
-  * two live engines over the same arrays (a registration shared by reference count), one
-    closed before the other steps;
-  * library arrays in place with non-temporal and plain accesses, over several steps with
-    the host rewriting inputs, and a per-call chain where each kernel reads the previous
-    kernel's outputs in host memory;
+  * two live engines over the same arrays, one closed before the other steps;
+  * library arrays (fcx_host_malloc) in place with non-temporal and plain accesses, over
+    several steps with the host rewriting inputs, and a per-call chain where each kernel
+    reads the previous kernel's outputs in host memory;
   * caller heap arrays are never used in place, whatever FCX_OPT_ZERO_COPY says.
 """
 import gc
@@ -77,8 +84,7 @@ def carve(cases, first_key=None):
 
 
 def test_output_page_shared_with_another_live_engine():
-    """Case B's MEVA begins on the page where case A's arrays end: in B it cannot be
-    page-locked exclusively, so its copies are staged."""
+    """Case B's MEVA begins on the page where case A's arrays end, both engines live."""
     a = build_case("MOM5", n=4097, T=1)
     b = build_case("MOM5", n=4097, T=1)
     keep = carve([a, b], first_key=(1, 1, "MEVA"))
@@ -110,15 +116,14 @@ def test_engine_collected_between_commit_and_step():
         del a
         b = build_case("MOM5", n=n, T=1)
         eb = engine_for(b)
-        gc.collect()  # the old engine's fcx_destroy runs here: its page locks are dropped
+        gc.collect()  # the old engine's fcx_destroy runs here
         eb.step(PHASE_ALL, T_STEP)
         check(b, f"n={n} after collecting the old engine")
         eb.close()
 
 
-def test_registration_shared_by_two_engines():
-    """Two live engines over the same arrays share one registration (reference count);
-    closing the first leaves the second's mapping intact."""
+def test_two_engines_over_the_same_arrays():
+    """Two live engines over the same arrays; closing the first leaves the second intact."""
     c = build_case("CCLM", n=4097, T=1, bias=True)
     e1 = engine_for(c)
     e2 = engine_for(c)
@@ -188,7 +193,7 @@ def test_library_pinned_arrays_zero_copy(variant, n):
         arena.adopt(c.lf)
         e = engine_for(c)
         assert e.zero_copy_active()
-        assert e.pinned_bytes() == 0  # nothing of the caller's was registered
+        assert e.staging_bytes() == 0  # library memory: no staging arena either
         for k in range(3):
             reset_outputs(c)
             e.step(PHASE_ALL, T_STEP)
@@ -208,3 +213,58 @@ def test_heap_arrays_never_used_in_place(zero_copy):
     e.step(PHASE_ALL, T_STEP)
     check(c, "mirrors")
     e.close()
+
+
+def _libc():
+    import ctypes
+
+    libc = ctypes.CDLL(None, use_errno=True)
+    libc.mmap.restype = ctypes.c_void_p
+    libc.mmap.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_long]
+    libc.munmap.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+    return libc
+
+
+PROT_RW, MAP_PRIVATE_ANON, MAP_FIXED = 0x3, 0x22, 0x10
+
+
+@pytest.mark.parametrize("variant", ["CCLM", "MOM5"])
+def test_recycled_virtual_address_between_engines(variant):
+    """Engine A binds arrays in an anonymous mapping; the mapping is then replaced at the same
+    virtual address (MAP_FIXED: new zero pages) and filled with another case's inputs while A
+    is alive; engine B binds the same addresses.  Both engines must compute from the new
+    contents -- the address-keyed registration sharing of round 2 would have handed B (and A)
+    the pages of the old mapping."""
+    import ctypes
+
+    libc = _libc()
+    a = build_case(variant, n=10_007, T=1, bias=True, seed=3)
+    b = build_case(variant, n=10_007, T=1, bias=True, seed=4)
+    size = 2 * 1024 * 1024
+    addr = libc.mmap(None, size, PROT_RW, MAP_PRIVATE_ANON, -1, 0)
+    assert addr not in (None, ctypes.c_void_p(-1).value)
+    view = np.frombuffer((ctypes.c_char * size).from_address(addr), dtype=np.uint8)
+    try:
+        end_a = rehome(a.lf, view, 8 * 3)  # mid-page start
+        ea = engine_for(a)
+        ea.step(PHASE_ALL, T_STEP)
+        check(a, "A before the remap")
+        # the same virtual range, new physical pages, B's inputs at A's addresses
+        again = libc.mmap(addr, size, PROT_RW, MAP_PRIVATE_ANON | MAP_FIXED, -1, 0)
+        assert again == addr
+        assert rehome(b.lf, view, 8 * 3) == end_a
+        for key in a.lf.field:  # one layout: A's arrays are B's arrays now
+            assert a.lf.field[key].ctypes.data == b.lf.field[key].ctypes.data
+        eb = engine_for(b)
+        eb.step(PHASE_ALL, T_STEP)
+        check(b, "B at the recycled addresses")
+        reset_outputs(b)
+        ea.step(PHASE_ALL, T_STEP)  # A reads the new contents too
+        check(b, "A after the remap")
+        ea.close()
+        reset_outputs(b)
+        eb.step(PHASE_ALL, T_STEP)
+        check(b, "B after A closed")
+        eb.close()
+    finally:
+        libc.munmap(addr, size)

@@ -46,6 +46,29 @@ def test_task_ranges_slot_rule():
     assert [r for _, _, r in task_ranges(np.repeat(np.arange(4), 3), 4)] == [0, 1, 2, 3]
 
 
+@pytest.mark.parametrize("mapcls", ["PeriodicAtmosMap", "BlockedRandomAtmosMap"])
+def test_structured_maps_take_the_task_slot_rule(mapcls):
+    """The O(size) structured maps of the bench build the same local views as local_atmos on
+    their global map, with the task_ranges slot rule when a middle rank is empty."""
+    import fcx.parallel as par
+
+    mk = getattr(par, mapcls)()
+    n = 30_001
+    g = mk.global_map(n)
+    t = np.repeat(np.array([0, 2, 3], np.int32), [12_007, 9_001, n - 21_008])  # rank 1 empty
+    for rank, (off, size, right_slot) in enumerate(task_ranges(t, 4)):
+        a = mk.local(off, size, rank, 4, n, right_slot=right_slot)
+        b = local_atmos(g, rank, 4, off, size, right_slot=right_slot)
+        assert (a.left, a.right, a.n_atmos) == (b.left, b.right, b.n_atmos), rank
+        np.testing.assert_array_equal(a.atmos_index, b.atmos_index)
+        np.testing.assert_allclose(a.weight, b.weight, rtol=1e-14)
+    # rank 0's right boundary and rank 2's left one are the same slot
+    r0 = mk.local(0, 12_007, 0, 4, n, right_slot=1)
+    r2 = mk.local(12_007, 9_001, 2, 4, n, right_slot=2)
+    if r0.right >= 0:
+        assert r0.right == r2.left == 1
+
+
 def test_synthetic_map_is_conservative_and_sorted():
     m = synthetic_atmos_map(100_003)
     assert np.all(np.diff(m.atmos_index) >= 0)
