@@ -55,6 +55,9 @@ def parse():
     p.add_argument("--cpu-cells", type=int, default=1_000_000)
     p.add_argument("--cpu-cells-mt", type=int, default=4_000_000, help="all-cores CPU sample")
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--e2e", type=int, default=1,
+                   help="N=1: also time the end-to-end host-array step at 10M and 32,768 cells (an 'e2e' "
+                        "sub-object; never the `value`)")
     p.add_argument("--atmos", type=int, default=1,
                    help="exchange->atmosphere accumulation (+ one RCCL all-reduce when N>1)")
     p.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL)")
@@ -166,6 +169,122 @@ def cpu_all_cores(args, variants):
                            else "every CPU of the process affinity set"),
             "sample": f"{reps} coupling steps x {len(variants)} variants over {n} cells, OpenMP "
                       f"APPLE ranges on {threads} threads, {el:.1f} s"}
+
+
+def multi_gpu_check(wl, world, rank, dist, samples=2000):
+    """After the timed steps (outside the timed region): the atmosphere cells of the last step
+    checked against the sequential SCRIP sum (fcx.parallel maps, oracle/fco.c order).
+
+    * shared cells (a rank's first / last atmosphere cell, completed by the one all-reduce):
+      every rank sends its partial cells (weights, fluxes) and its finished values to rank 0,
+      which sums each boundary's cells in global exchange order from 0.0 and compares both
+      neighbours' finished values (mixed error; association differs from the sequential sum
+      only by the split into two partial sums);
+    * a sample of interior cells of every rank: bit-identical to the sequential sum of the
+      rank's own fluxes.
+    The sequential sum is restated here (the oracle serves only the CPU baseline leg of this
+    file): acc = acc + w * x from 0.0 in link order, in IEEE double without contraction.
+    Returns the JSON sub-object on rank 0 (None elsewhere)."""
+    from fcx.workload import ATM_FIELDS
+
+    def seq_sum(w, x):
+        acc = 0.0
+        for wk, xk in zip(w, x):
+            acc = acc + float(wk) * float(xk)
+        return acc
+
+    wl.download()
+    la = wl.la
+    rng = np.random.default_rng(7 + rank)
+    idx = la.atmos_index
+    starts = np.searchsorted(idx, np.arange(la.n_atmos + 1))  # CSR of the local map
+    lo = 1 if la.left >= 0 else 0
+    hi = la.n_atmos - (1 if la.right >= 0 else 0)
+    pick = np.unique(rng.integers(lo, max(hi, lo + 1), min(samples, max(hi - lo, 0)))) if hi > lo else np.zeros(0, int)
+    interior_bad, edge = 0, []
+    for i, (case, outs) in enumerate(zip(wl.cases, wl.atm_outs)):
+        for name, g in ATM_FIELDS:
+            flux = np.asarray(case.lf.field[(1 if wl.types == 1 else 0, g, name)])
+            got = np.asarray(outs[name])
+            for a in pick:
+                x0, x1 = starts[a], starts[a + 1]
+                interior_bad += int(got[a] != seq_sum(la.weight[x0:x1], flux[x0:x1]))
+            for side, a, slot in (("left", 0, la.left), ("right", la.n_atmos - 1, la.right)):
+                if slot >= 0:
+                    x0, x1 = starts[a], starts[a + 1]
+                    edge.append({"variant": i, "field": name, "slot": int(slot), "side": side, "rank": rank,
+                                 "x0": int(wl.offset + x0), "w": la.weight[x0:x1].tolist(),
+                                 "x": flux[x0:x1].tolist(), "got": float(got[a])})
+    mine = {"rank": rank, "interior": int(pick.size) * len(wl.cases) * len(ATM_FIELDS),
+            "interior_bad": interior_bad, "edge": edge}
+    if world > 1:
+        allv = [None] * world
+        dist.all_gather_object(allv, mine)
+    else:
+        allv = [mine]
+    if rank != 0:
+        return None
+    by = {}
+    for r in allv:
+        for e in r["edge"]:
+            by.setdefault((e["variant"], e["field"], e["slot"]), []).append(e)
+    worst, cells = 0.0, 0
+    for key, parts in by.items():
+        parts.sort(key=lambda e: e["x0"])  # the boundary's exchange cells in global order
+        w = np.concatenate([np.asarray(e["w"]) for e in parts])
+        x = np.concatenate([np.asarray(e["x"]) for e in parts])
+        want = seq_sum(w, x)
+        for e in parts:
+            err = abs(e["got"] - want) / max(abs(want), 1e-300)
+            worst = max(worst, err)
+        cells += 1
+    return {"max_mixed_err": worst, "shared_cells": cells, "ranks_seen": len(allv),
+            "interior_sampled": sum(r["interior"] for r in allv),
+            "interior_bit_identical": all(r["interior_bad"] == 0 for r in allv),
+            "rule": "shared boundary cells vs the sequential sum over both neighbours' exchange cells "
+                    "(relative error); sampled interior cells bit-identical to the rank's own sequential sum"}
+
+
+def e2e_host(args, variants, sizes=(10_000_000, 32_768)):
+    """SURVEY.md 8d end-to-end rate (never `value`): the fields in caller heap arrays (numpy,
+    as a Fortran host's ALLOCATEd local_field arrays), every coupling step fcx_step = inputs
+    host -> device, the fused kernels, outputs device -> host, synchronised, with the default
+    transport (the engine's staging arena, pipelined over chunks on large grids).  Wall time
+    per step, one engine per variant at a time."""
+    from fcx.basic import PHASE_ALL
+    from fcx.engine import Engine
+    from fcx.synthetic import build_case, inputs_for_bench
+
+    out = {"transport": "default: caller heap arrays through the engine's page-locked staging arena "
+                        "(FCX_OPT_HOST_STAGING), pipelined H2D/kernel/D2H chunks from 2 x 256K cells",
+           "unit": "Mcells/s", "sizes": {}}
+    for n in sizes:
+        data = inputs_for_bench(n)
+        steps = 10 if n >= 1_000_000 else 500
+        per = {}
+        for v in variants:
+            case = build_case(v, n=n, T=args.types, bias=args.bias, data=data if args.types == 1 else None)
+            eng = Engine(case.lf, case.num_surface_types, case.methods, corrections=case.corrections,
+                         averages=case.averages)
+            for k in range(3 if n >= 1_000_000 else 50):  # first touch, plans, arena, clocks
+                eng.step(PHASE_ALL, k * 3600)
+            ts = []
+            for k in range(steps):
+                t0 = time.perf_counter()
+                eng.step(PHASE_ALL, k * 3600)
+                ts.append(time.perf_counter() - t0)
+            staging = eng.staging_bytes()
+            eng.close()
+            med = float(np.median(ts))
+            per[v] = {"us_per_step_median": round(med * 1e6, 1),
+                      "us_per_step_p90": round(float(np.percentile(ts, 90)) * 1e6, 1),
+                      "Mcells_per_s": round(n / med / 1e6, 1), "staging_MB": round(staging / 1e6, 1)}
+            del case
+        tot = sum(x["us_per_step_median"] for x in per.values()) * 1e-6
+        out["sizes"][str(n)] = {"variants": per, "steps": steps,
+                                "value": round(n * len(per) / tot / 1e6, 1),
+                                "value_rule": "cells x variants / sum of the variants' median step times"}
+    return out
 
 
 def relaunch(n):
@@ -337,6 +456,8 @@ def main():
         except Exception:
             traffic = None
 
+    mg = multi_gpu_check(wl, world, rank, dist) if la is not None else None
+
     out = {
         "metric": METRIC,
         "value": round(value, 1),
@@ -394,6 +515,8 @@ def main():
         },
         "kernels": per_variant,
     }
+    if mg is not None:
+        out["multi_gpu_check"] = mg
     wl.close()
     del wl
     torch.cuda.synchronize()
@@ -448,6 +571,8 @@ def main():
         del w4, wl
         torch.cuda.synchronize()
 
+    if rank == 0 and world == 1 and args.e2e:
+        out["e2e"] = e2e_host(args, variants)
     if rank == 0 and world == 1 and not args.no_cpu:
         cb = cpu_baseline(args, variants)
         out["cpu_baseline"] = cb

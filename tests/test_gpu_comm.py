@@ -109,3 +109,74 @@ def test_one_allreduce_for_three_variants():
             np.testing.assert_array_equal(outs[name].cpu().numpy(), want, err_msg=name)
         e.close()
     c.close()
+
+
+@pytest.mark.parametrize("layout", ["separate_buffers", "gapped_buffer", "reversed_adjacent"])
+@pytest.mark.parametrize("streams", ["one", "per_engine"])
+def test_atmos_allreduce_regions_and_streams(layout, streams):
+    """fcx_atmos_allreduce over three engines whose boundary-slot regions are NOT adjacent in
+    one buffer (separate buffers, or one buffer with gaps: one all-reduce per engine inside one
+    RCCL group) or adjacent in reverse engine order (one call from the lowest address), with
+    the engines on one stream or each on its own stream (the all-reduce on the first engine's
+    stream waits for the others' accumulations, and each engine's finish waits for it).  One
+    rank: every atmosphere cell bit-identical to the sequential sum, every slot re-zeroed."""
+    import torch
+    from fcx.comm import Comm, unique_id
+    from fcx.engine import Engine
+
+    n = 40_003
+    amap = synthetic_atmos_map(n)
+    # both boundary slots in use: the first and the last atmosphere cell go through the exchange
+    la = dataclasses.replace(local_atmos(amap, 0, 1), left=0, right=1, n_boundaries=2)
+    stride, nb = len(FIELDS), 2
+    region = nb * stride
+    if layout == "separate_buffers":
+        bufs = [torch.zeros(region, dtype=torch.float64, device="cuda:0") for _ in range(3)]
+        slots = bufs
+    elif layout == "gapped_buffer":
+        big = torch.zeros(3 * region + 2 * 7, dtype=torch.float64, device="cuda:0")
+        bufs = [big]
+        slots = [big[i * (region + 7):] for i in range(3)]
+    else:
+        big = torch.zeros(3 * region, dtype=torch.float64, device="cuda:0")
+        bufs = [big]
+        slots = [big[(2 - i) * region:] for i in range(3)]
+    own = [torch.cuda.Stream() for _ in range(3)] if streams == "per_engine" else [torch.cuda.current_stream()] * 3
+    c = Comm(0, 1, 0, unique_id())
+    engines, cases, outs_all = [], [], []
+    for i, v in enumerate(("CCLM", "MOM5", "RCO")):
+        case = build_case(v, n=n, T=1, seed=31 + i)
+        outs = {name: torch.full((la.n_atmos,), float("nan"), dtype=torch.float64, device="cuda:0")
+                for name, _ in FIELDS}
+        atmos = {"local": la, "fields": [(PHASE_NORMAL, 1, g, name, outs[name]) for name, g in FIELDS],
+                 "shared": (slots[i], stride)}
+        e = Engine(case.lf, 1, case.methods, atmos=atmos, stream=own[i].cuda_stream,
+                   options={"atmos_in_run": 0})
+        e.upload(PHASE_ALL)
+        engines.append(e)
+        cases.append(case)
+        outs_all.append(outs)
+    torch.cuda.synchronize()
+    for step in range(2):
+        for outs in outs_all:
+            for o in outs.values():
+                o.fill_(float("nan"))
+        torch.cuda.synchronize()
+        for e in engines:
+            e.run(PHASE_ALL, 3600 * step)
+            e.run_atmos(PHASE_ALL)
+        c.atmos_allreduce(engines)
+        for e in engines:
+            e.download(PHASE_ALL)
+            e.synchronize()
+        torch.cuda.synchronize()
+        for b in bufs:
+            assert float(b.abs().sum()) == 0.0  # every slot re-zeroed by the finishes
+        for case, outs in zip(cases, outs_all):
+            for name, g in FIELDS:
+                flux = np.asarray(case.lf.field[(1, g, name)])
+                want = oracle_lib.atmos_accumulate(amap.atmos_index, amap.weight, flux, amap.n_atmos)
+                np.testing.assert_array_equal(outs[name].cpu().numpy(), want, err_msg=f"{name} step {step}")
+    for e in engines:
+        e.close()
+    c.close()
