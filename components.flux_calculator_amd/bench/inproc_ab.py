@@ -43,6 +43,9 @@ def main():
     ap.add_argument("--opts", action="append", default=[],
                     help="NAME:key=val[,key=val] -- another engine set of the main build with these "
                          "fcx_set_option values (e.g. split0:type_split=0)")
+    ap.add_argument("--precision", choices=("f64", "f32"), default="f64")
+    ap.add_argument("--atmos-map", choices=("periodic", "random"), default="random",
+                    help="exchange->atmosphere map (bench.py's default: random runs crossing the wave tiles)")
     ap.add_argument("--host", action="store_true",
                     help="bind host arrays: every build's engines own their (tile-blocked) device "
                          "mirrors, uploaded once -- the bench's layout; builds then differ in placement")
@@ -52,8 +55,8 @@ def main():
     from fcx import _lib
     from fcx.basic import PHASE_ALL, PHASE_NORMAL
     from fcx.engine import Engine
-    from fcx.parallel import PeriodicAtmosMap
-    from fcx.synthetic import build_case, inputs_for_bench
+    from fcx.parallel import BlockedRandomAtmosMap, PeriodicAtmosMap
+    from fcx.synthetic import as_dtype, build_case, inputs_for_bench
 
     libs, no_atmos, extra_opts = {"ref": None}, set(), {}
     for spec in a.opts:
@@ -79,12 +82,15 @@ def main():
         data, cdev = {k: torch.as_tensor(v).to(dev) for k, v in host.items()}, dev
         del host
     stream = torch.cuda.current_stream(dev)
-    la = PeriodicAtmosMap().local(0, n, 0, 1, n)
+    la = (BlockedRandomAtmosMap() if a.atmos_map == "random" else PeriodicAtmosMap()).local(0, n, 0, 1, n)
     cases, outs = [], []
+    f32 = a.precision == "f32"
     for v in variants:
-        cases.append(build_case(v, n=n, T=a.types, device=cdev, data=data if a.types == 1 else None))
-        outs.append({name: (np.empty(max(la.n_atmos, 1)) if a.host else
-                            torch.empty(max(la.n_atmos, 1), dtype=torch.float64, device=dev))
+        c = build_case(v, n=n, T=a.types, device=cdev, data=data if a.types == 1 else None)
+        cases.append(as_dtype(c, "float32") if f32 else c)
+        outs.append({name: (np.empty(max(la.n_atmos, 1), dtype=np.float32 if f32 else np.float64) if a.host else
+                            torch.empty(max(la.n_atmos, 1), dtype=torch.float32 if f32 else torch.float64,
+                                        device=dev))
                      for name, _ in FIELDS})
     s0 = 0 if a.types >= 2 else 1
     engines = {}
@@ -128,7 +134,8 @@ def main():
             torch.cuda.synchronize()
             wall[lname].append((time.perf_counter() - t0) / a.steps * 1e3)
             kern[lname].append([[x.elapsed_time(y) for x, y in row] for row in ev])
-    out = {"cells": n, "types": a.types, "atmos": a.atmos, "rounds": a.rounds, "steps": a.steps, "builds": {}}
+    out = {"cells": n, "types": a.types, "precision": a.precision, "atmos": a.atmos, "atmos_map": a.atmos_map, "rounds": a.rounds,
+           "steps": a.steps, "builds": {}}
     for lname in names:
         km = np.array(kern[lname]).reshape(-1, len(variants)).mean(axis=0)
         out["builds"][lname] = {

@@ -2124,7 +2124,10 @@ static int step_pipelined(fcx_engine *e, int phase, int32_t t, Plan *pl) {
           HIP_TRY(get_atm(e, f.out_host, f.out_dev, e->s_out));
       }
   if (int r = download_remaps(e, phase, e->s_out, &xa)) return r;
-  if (!xa.empty()) HIP_TRY(stage_dma(e, xa, 0, -1, false, e->s_out));
+  if (!xa.empty()) {  // (the arena may hold only these: fields in library memory)
+    if (int r = stage_alloc(e)) return r;
+    HIP_TRY(stage_dma(e, xa, 0, -1, false, e->s_out));
+  }
   if (e->timing) HIP_TRY(hipEventRecord(e->ev1, e->s_out));
   e->timed = e->timing;
   if (!xout.empty())

@@ -351,6 +351,30 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
 #define HOLD(var, grp, member) HOLDX(var, grp, member, false)
 #define HOLDA(var, grp, member, bit) HOLDX(var, grp, member, true)
   constexpr bool kHoldWind = kHoldAtm;
+  // FCX_PREFETCH_TYPE (multi-type kernels): the bottom-side inputs of type s+1 (TSUR FICE
+  // CMOI CHEA CMOM and the FARE of the averages) are loaded when type s starts, so that the
+  // wave does not stall on memory between two types; they cost VGPRs only while type s runs.
+#ifndef FCX_PREFETCH_TYPE
+#define FCX_PREFETCH_TYPE 0
+#endif
+  constexpr bool kPrefetch = kReload && FCX_PREFETCH_TYPE;
+  Vec<C, R> n_ts = {}, n_fi = {}, n_cmoi = {}, n_chea = {}, n_cmom = {}, n_fare = {};
+  auto prefetch = [&](int s2) {
+    const TypeParams &q = P->type[s2];
+    if (q.t.tsur) n_ts = LD(q.t.tsur, j0, nt);
+    if (q.t.fice) n_fi = LD(q.t.fice, j0, nt);
+    if (q.t.cmoi) n_cmoi = LD(q.t.cmoi, j0, nt);
+    if (q.t.chea) n_chea = LD(q.t.chea, j0, nt);
+    if constexpr (MERGED) {
+      if (q.uv[0].cmom) n_cmom = LD(q.uv[0].cmom, j0, nt);
+    }
+    if constexpr (RAVG) {
+      if (P->ravg_on) n_fare = LD(P->ravg.fare[s2], j0, nt);
+    }
+  };
+  if constexpr (kPrefetch) {
+    if (do_t) prefetch(0);
+  }
 
   for (int s = 0; s < T; ++s) {
     if constexpr (kReload) {  // no bottom-side input of the previous type stays live
@@ -369,8 +393,18 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
     if (do_t) {
       // ---- every t-grid input this type needs (before any store of this type)
       Vec<C, R> qs = {}, me = {};
-      HOLD(ts, t, tsur)
-      HOLD(fi, t, fice)
+      if constexpr (kPrefetch) {
+        ts = n_ts;
+        fi = n_fi;
+        cmoi = n_cmoi;
+        chea = n_chea;
+        cmom = n_cmom;
+        if constexpr (RAVG) sink.fare = n_fare;
+        if (s + 1 < T) prefetch(s + 1);
+      } else {
+        HOLD(ts, t, tsur)
+        HOLD(fi, t, fice)
+      }
       HOLDA(ps, t, psur, 0)
       HOLDA(pa, t, patm, 1)
       HOLDA(qa, t, qatm, 2)
@@ -379,17 +413,21 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
       HOLDA(u, t, uatm, 4)
       HOLDA(v, t, vatm, 5)
       HOLDA(amoi, t, amoi, 6)
-      HOLD(cmoi, t, cmoi)
-      HOLD(chea, t, chea)
+      if constexpr (!kPrefetch) {
+        HOLD(cmoi, t, cmoi)
+        HOLD(chea, t, chea)
+      }
       if (g.qsur_in) qs = LD(g.qsur_in, j0, nt);  // may be written by this pass: never held
       if (g.meva_in) me = LD(g.meva_in, j0, nt);
       if constexpr (MERGED) {
         HOLDA(amom, uv[0], amom, 7)
-        HOLD(cmom, uv[0], cmom)
+        if constexpr (!kPrefetch) HOLD(cmom, uv[0], cmom)
       }
       if (wind_new) FOR_C vel.v[i] = wind(u.v[i], v.v[i]);
       if constexpr (RAVG) {
-        if (P->ravg_on) sink.fare = LD(P->ravg.fare[s], j0, nt);
+        if constexpr (!kPrefetch) {
+          if (P->ravg_on) sink.fare = LD(P->ravg.fare[s], j0, nt);
+        }
         sink(A_TSUR, ts);
       }
 
@@ -666,6 +704,11 @@ __device__ __forceinline__ void segment_done(const AtmosFused &af, int64_t tile,
 #ifndef FCX_T1_ATMOS_BLOCKS
 #define FCX_T1_ATMOS_BLOCKS 1
 #endif
+// ... and the fp32 T=1 fused kernels (4 cells per lane): 1 = no register cap (CCLM 132, MOM5
+// 137 VGPRs: 3 waves per SIMD), 4 = at most 128 VGPRs (4 waves per SIMD)
+#ifndef FCX_F32_ATMOS_BLOCKS
+#define FCX_F32_ATMOS_BLOCKS 1
+#endif
 // waves per block of the fused kernel (the fp32 kernel's as an A/B knob)
 #ifndef FCX_F32_ATMOS_WAVES  // A/B: 2 paid while the fp32 rows held fp64 products (13.8 KB/wave)
 #define FCX_F32_ATMOS_WAVES 4
@@ -674,7 +717,7 @@ template <int C>
 constexpr int atmos_waves() { return C == 4 ? FCX_F32_ATMOS_WAVES : 4; }
 template <int C, class R, int VAR, bool NT, int TM, bool RAVG, bool REC = false>
 // (REC: the record stores took CCLM to 129 VGPRs and 3 waves per SIMD; capped at 4 blocks = 4 waves)
-__global__ __launch_bounds__(64 * atmos_waves<C>(), RAVG ? FCX_RAVG_ATMOS_BLOCKS : REC ? 4 : FCX_T1_ATMOS_BLOCKS) void cells_atmos_kernel(const Params *__restrict__ P,
+__global__ __launch_bounds__(64 * atmos_waves<C>(), RAVG ? FCX_RAVG_ATMOS_BLOCKS : REC ? 4 : C == 4 ? FCX_F32_ATMOS_BLOCKS : FCX_T1_ATMOS_BLOCKS) void cells_atmos_kernel(const Params *__restrict__ P,
                                                           const double *__restrict__ corr_m,
                                                           const AtmosFused af, int64_t lo, int64_t hi) {
   static_assert(!RAVG || (C == 2 && sizeof(R) == 8), "register averages: fp64 engine only");

@@ -237,8 +237,10 @@ int fcx_add_remap_field(fcx_engine *e, int32_t remap_id, int phase, int surface_
                         int var, double *out, int flags);
 /* after fcx_commit: the map's gather scatter (distinct 64-B field segments per link over a
  * sample of 256-destination blocks) and whether its launches gather packed records
- * (FCX_OPT_REMAP_PACK): 0 no, 1 packed by a packing pass, 2 written by the flux launch of
- * the last run (T=1 fluxes of surface type 1; no packing pass) */
+ * (FCX_OPT_REMAP_PACK): 0 no, 1 packed by a packing pass, 2 the flux launch of the last
+ * fcx_run / fcx_step wrote the records of one launch group of this remap (T=1 fluxes of
+ * surface type 1; that group needs no packing pass -- a remap of more than 16 fields has
+ * further groups, which pack their own).  Per-call runs do not change the answer. */
 int fcx_remap_info(const fcx_engine *e, int32_t remap_id, double *scatter, int32_t *packed);
 
 /* launch tuning of the fused cells kernel (defaults are the measured best on MI355X) */
