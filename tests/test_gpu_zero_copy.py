@@ -240,6 +240,7 @@ def test_recycled_virtual_address_between_engines(variant):
     libc = _libc()
     a = build_case(variant, n=10_007, T=1, bias=True, seed=3)
     b = build_case(variant, n=10_007, T=1, bias=True, seed=4)
+    b.corrections = a.corrections  # engine state (copied at set-up), not memory at the addresses
     size = 2 * 1024 * 1024
     addr = libc.mmap(None, size, PROT_RW, MAP_PRIVATE_ANON, -1, 0)
     assert addr not in (None, ctypes.c_void_p(-1).value)
