@@ -133,13 +133,16 @@ def main():
 
     # ---- host-bound: fcx_step per variant (upload, run, download, synchronise)
     # host_heap_staged: caller heap arrays (a Fortran host's ALLOCATEd fields) through the
-    # engine's staging arena (the default transport); host_heap_runtime_copies: the same with
-    # one runtime copy per array (FCX_OPT_HOST_STAGING=0, round 2's default);
+    # engine's staging arena, which the kernels use in place at this size (the default);
+    # host_heap_staged_dma: the arena moved by one DMA per pool and direction
+    # (FCX_OPT_ZERO_COPY=0); host_heap_runtime_copies: one runtime copy per array
+    # (FCX_OPT_HOST_STAGING=0, round 2's default);
     # host_library_arrays: arrays from fcx_host_malloc, used in place by default (auto
     # zero-copy); host_library_mirrors: the same arrays through mirrors (FCX_OPT_ZERO_COPY=0)
     from fcx.host_alloc import Arena
 
     for mode, opts, lib_arrays in (("host_heap_staged", {}, False),
+                                   ("host_heap_staged_dma", {"zero_copy": 0}, False),
                                    ("host_heap_runtime_copies", {"host_staging": 0}, False),
                                    ("host_library_arrays", {}, True),
                                    ("host_library_mirrors", {"zero_copy": 0}, True)):

@@ -12,6 +12,9 @@
 #include <mutex>
 #include <thread>
 #include <vector>
+#if defined(__x86_64__)
+#include <emmintrin.h>
+#endif
 
 namespace fcx {
 
@@ -20,6 +23,35 @@ inline void cpu_relax() {
   __builtin_ia32_pause();
 #else
   std::this_thread::yield();
+#endif
+}
+
+// memcpy with non-temporal stores (x86-64: 16-B streaming stores once the destination is
+// aligned): the destination is not read back by this CPU soon (the arena is read by the DMA
+// engine, the caller's arrays by the host program later), so the stores skip the
+// read-for-ownership of every line and leave the caches alone
+inline void copy_nt(char *dst, const char *src, size_t n) {
+#if defined(__x86_64__)
+  const size_t head = std::min(n, (size_t)((16 - (reinterpret_cast<uintptr_t>(dst) & 15)) & 15));
+  std::memcpy(dst, src, head);
+  dst += head;
+  src += head;
+  n -= head;
+  size_t i = 0;
+  for (; i + 64 <= n; i += 64) {
+    const __m128i a = _mm_loadu_si128(reinterpret_cast<const __m128i *>(src + i));
+    const __m128i b = _mm_loadu_si128(reinterpret_cast<const __m128i *>(src + i + 16));
+    const __m128i c = _mm_loadu_si128(reinterpret_cast<const __m128i *>(src + i + 32));
+    const __m128i d = _mm_loadu_si128(reinterpret_cast<const __m128i *>(src + i + 48));
+    _mm_stream_si128(reinterpret_cast<__m128i *>(dst + i), a);
+    _mm_stream_si128(reinterpret_cast<__m128i *>(dst + i + 16), b);
+    _mm_stream_si128(reinterpret_cast<__m128i *>(dst + i + 32), c);
+    _mm_stream_si128(reinterpret_cast<__m128i *>(dst + i + 48), d);
+  }
+  std::memcpy(dst + i, src + i, n - i);
+  _mm_sfence();  // the streamed lines are globally visible before the batch is reported done
+#else
+  std::memcpy(dst, src, n);
 #endif
 }
 
@@ -39,15 +71,16 @@ class CopyPool {
     static CopyPool *p = new CopyPool();  // never destroyed: workers may outlive static dtors
     return *p;
   }
-  // every job done when this returns; `threads` counts the caller
-  void run(const std::vector<CopyJob> &jobs, int threads) {
+  // every job done when this returns; `threads` counts the caller; nt: non-temporal stores
+  void run(const std::vector<CopyJob> &jobs, int threads, bool nt = false) {
     if (jobs.empty()) return;
     std::lock_guard<std::mutex> one(batch_mu_);
     const int helpers = std::max(0, std::min<int>({threads - 1, (int)jobs.size() - 1, 63}));
     if (helpers == 0) {
-      for (const auto &j : jobs) std::memcpy(j.dst, j.src, j.bytes);
+      for (const auto &j : jobs) nt ? copy_nt(j.dst, j.src, j.bytes) : (void)std::memcpy(j.dst, j.src, j.bytes);
       return;
     }
+    nt_ = nt;
     grow(helpers);
     jobs_ = jobs.data();
     njobs_ = jobs.size();
@@ -67,8 +100,12 @@ class CopyPool {
 
  private:
   void work() {
-    for (size_t i; (i = next_.fetch_add(1, std::memory_order_relaxed)) < njobs_;)
-      std::memcpy(jobs_[i].dst, jobs_[i].src, jobs_[i].bytes);
+    for (size_t i; (i = next_.fetch_add(1, std::memory_order_relaxed)) < njobs_;) {
+      if (nt_)
+        copy_nt(jobs_[i].dst, jobs_[i].src, jobs_[i].bytes);
+      else
+        std::memcpy(jobs_[i].dst, jobs_[i].src, jobs_[i].bytes);
+    }
   }
   // new workers start from the generation before the batch about to be published, so a
   // worker created for a batch always takes part in it
@@ -107,6 +144,7 @@ class CopyPool {
   std::vector<std::thread> workers_;
   const CopyJob *jobs_ = nullptr;
   size_t njobs_ = 0;
+  bool nt_ = false;
   std::atomic<size_t> next_{0};
   std::atomic<int> busy_{0}, sleepers_{0};
   std::atomic<uint64_t> gen_{0};  // (batch counter << 8) | helpers of the batch

@@ -84,6 +84,7 @@ struct StagePool {
   size_t bytes = 0;
   bool tiled = false;
   size_t slot = 0, pitch = 0;  // tiled: bytes of one slot's tile, bytes of one row
+  bool mapped = false;         // the image IS the kernels' buffer (device-mapped): no DMA
 };
 
 // One host array <-> its mirror through the staging arena: `n` elements of `es` bytes.
@@ -119,7 +120,7 @@ struct Plan {
 
 int var0(int var) { return var - 1; }
 
-// threads of the host copies: FCX_OPT_HOST_THREADS, else min(8, OMP_NUM_THREADS if set, else
+// threads of the host copies: FCX_OPT_HOST_THREADS, else min(16, OMP_NUM_THREADS if set, else
 // the CPUs this process may run on) -- an MPI rank pinned to one core copies alone
 int default_host_threads() {
   static const int n = [] {
@@ -130,7 +131,7 @@ int default_host_threads() {
       const int t = std::atoi(omp);
       if (t > 0) cpus = std::min(cpus, t);
     }
-    return std::max(1, std::min(cpus, 8));
+    return std::max(1, std::min(cpus, 16));
   }();
   return n;
 }
@@ -1346,19 +1347,22 @@ static void stage_setup(fcx_engine *e) {
       if (!f.external && heap(f.out_host, rm.n_dst)) f.st = stage_ref(e, f.out_dev);
 }
 
-static int stage_alloc(fcx_engine *e) {
-  for (auto &p : e->spools)
-    if (!p.host) {
-      hipError_t err = hipHostMalloc((void **)&p.host, std::max<size_t>(p.bytes, 1), hipHostMallocDefault);
-      if (err != hipSuccess)
-        return fail(FCX_E_NOMEM, "hipHostMalloc(%zu) for the staging arena: %s", p.bytes, hipGetErrorString(err));
-    }
+// the host images of the pools these transfers use (allocated at first use: pools that are
+// never transferred -- e.g. arrays bound but not used by any launch -- get none)
+static int stage_alloc(fcx_engine *e, const std::vector<Xfer> &xs) {
+  for (const Xfer &x : xs) {
+    StagePool &p = e->spools[(size_t)x.sp];
+    if (p.host) continue;
+    hipError_t err = hipHostMalloc((void **)&p.host, std::max<size_t>(p.bytes, 1), hipHostMallocDefault);
+    if (err != hipSuccess)
+      return fail(FCX_E_NOMEM, "hipHostMalloc(%zu) for the staging arena: %s", p.bytes, hipGetErrorString(err));
+  }
   return FCX_OK;
 }
 
 static void stage_free(fcx_engine *e) {
   for (auto &p : e->spools)
-    if (p.host) (void)hipHostFree(p.host);
+    if (p.host) (void)hipHostFree(p.host);  // (a mapped pool's image is its device buffer too)
   e->spools.clear();
   if (e->ev_stage_in) (void)hipEventDestroy(e->ev_stage_in);
   e->ev_stage_in = nullptr;
@@ -1391,7 +1395,11 @@ static void stage_copy(fcx_engine *e, const std::vector<Xfer> &xs, int64_t a, in
       t0 = t1;
     }
   }
-  CopyPool::get().run(jobs, e->host_threads > 0 ? e->host_threads : default_host_threads());
+  // batches beyond the caches stream their stores (no read-for-ownership of the destination);
+  // Baltic-size batches stay cache-resident and copy plainly
+  size_t total = 0;
+  for (const auto &j : jobs) total += j.bytes;
+  CopyPool::get().run(jobs, e->host_threads > 0 ? e->host_threads : default_host_threads(), total >= (size_t(32) << 20));
 }
 
 // DMAs of elements [a, z) of the transfers' mirrors between arena and device: per pool,
@@ -1410,7 +1418,9 @@ static hipError_t stage_dma(fcx_engine *e, std::vector<Xfer> xs, int64_t a, int6
     const StagePool &p = e->spools[(size_t)xs[i].sp];
     size_t j = i + 1;
     int64_t hi = z < 0 ? xs[i].n : std::min(z, xs[i].n);
-    if (p.tiled) {
+    if (p.mapped) {  // the kernels use the image in place
+      while (j < xs.size() && xs[j].sp == xs[i].sp) ++j;
+    } else if (p.tiled) {
       size_t end = xs[i].soff + p.slot;
       while (j < xs.size() && xs[j].sp == xs[i].sp && (xs[j].soff == end || xs[j].soff + p.slot == end)) {
         end = std::max(end, xs[j].soff + p.slot);
@@ -1454,9 +1464,11 @@ static int stage_flush(fcx_engine *e);
 // outputs still waiting for their host copies are completed first
 static int stage_in(fcx_engine *e, const std::vector<Xfer> &xs, hipStream_t s) {
   if (xs.empty()) return FCX_OK;
-  if (int r = stage_alloc(e)) return r;
-  if (!e->pending_out.empty()) {
-    HIP_TRY(hipStreamSynchronize(e->stream));
+  if (int r = stage_alloc(e, xs)) return r;
+  bool mapped = false;
+  for (const Xfer &x : xs) mapped = mapped || e->spools[(size_t)x.sp].mapped;
+  if (!e->pending_out.empty() || mapped) {  // a mapped image is read by the kernels in place:
+    HIP_TRY(hipStreamSynchronize(e->stream));  // the last launch must be done with it
     if (int r = stage_flush(e)) return r;
   }
   if (e->stage_in_live) HIP_TRY(hipEventSynchronize(e->ev_stage_in));
@@ -1471,7 +1483,7 @@ static int stage_in(fcx_engine *e, const std::vector<Xfer> &xs, hipStream_t s) {
 // download through the arena: the DMAs now, the host copies at the next synchronisation
 static int stage_out(fcx_engine *e, const std::vector<Xfer> &xs, hipStream_t s) {
   if (xs.empty()) return FCX_OK;
-  if (int r = stage_alloc(e)) return r;
+  if (int r = stage_alloc(e, xs)) return r;
   HIP_TRY(stage_dma(e, xs, 0, -1, false, s));
   e->pending_out.insert(e->pending_out.end(), xs.begin(), xs.end());
   return FCX_OK;
@@ -1487,6 +1499,65 @@ static int stage_flush(fcx_engine *e) {
 
 static Xfer xfer_of(const StageRef &st, void *host, int64_t n) {
   return Xfer{st.sp, st.soff, reinterpret_cast<char *>(host), n};
+}
+
+// Zero-copy for caller heap arrays (FCX_OPT_ZERO_COPY with staging): their images live in
+// one device-mapped page-locked arena (plain layout, 256-B aligned) that the kernels use in
+// place -- the library's own memory, as fcx_host_malloc blocks are -- so a small step makes
+// no copy call at all: the host copies the inputs into the arena, the launch reads and
+// writes it over the host link, the host copies the outputs back after the synchronisation.
+static int map_staged(fcx_engine *e, int *count) {
+  *count = 0;
+  const size_t es = e->esize;
+  auto heap = [&](const void *h, int64_t n) { return h && !lib_block_device_ptr(h, (size_t)std::max<int64_t>(n, 1) * es); };
+  auto span = [&](int64_t n) { return ((size_t)std::max<int64_t>(n, 1) * es + 255) / 256 * 256; };
+  struct Item {
+    double **dev;
+    bool *ext;
+    StageRef *st;
+    int64_t n;
+    size_t off;
+  };
+  std::vector<Item> items;
+  size_t total = 0;
+  auto add = [&](double **dev, bool *ext, StageRef *st, int64_t n) {
+    items.push_back(Item{dev, ext, st, n, total});
+    total += span(n);
+  };
+  for (auto &bf : e->bufs)
+    if (!bf.external && heap(bf.host, bf.n)) add(&bf.dev, &bf.external, &bf.st, bf.n);
+  for (auto &f : e->atm_fields)
+    if (!f.external && heap(f.out_host, e->n_atmos)) add(&f.out_dev, &f.external, &f.st, std::max<int64_t>(e->n_atmos, 0));
+  for (auto &rm : e->remaps)
+    for (auto &f : rm.fields)
+      if (!f.external && heap(f.out_host, rm.n_dst)) add(&f.out_dev, &f.external, &f.st, rm.n_dst);
+  if (items.empty()) return FCX_OK;
+  StagePool p;
+  void *h = nullptr, *d = nullptr;
+  hipError_t err = hipHostMalloc(&h, total, hipHostMallocMapped);
+  if (err != hipSuccess) return fail(FCX_E_NOMEM, "hipHostMalloc(%zu) for the mapped staging arena: %s", total, hipGetErrorString(err));
+  err = hipHostGetDevicePointer(&d, h, 0);
+  if (err != hipSuccess || !d) {
+    (void)hipHostFree(h);
+    return fail(FCX_E_HIP, "hipHostGetDevicePointer: %s", hipGetErrorString(err));
+  }
+  p.dev = reinterpret_cast<char *>(d);
+  p.host = reinterpret_cast<char *>(h);
+  p.bytes = total;
+  p.mapped = true;
+  const int sp = (int)e->spools.size();
+  e->spools.push_back(p);
+  for (const Item &it : items) {
+    *it.dev = reinterpret_cast<double *>(p.dev + it.off);
+    *it.ext = true;  // no engine mirror: the kernels use the image
+    it.st->sp = sp;
+    it.st->soff = it.off;
+    e->zc_bytes += it.n * (int64_t)es;
+  }
+  for (auto &bf : e->bufs)
+    if (bf.st.sp == sp) bf.in_place = true;
+  *count = (int)items.size();
+  return FCX_OK;
 }
 
 extern "C" int fcx_set_precision(fcx_engine *e, int precision) {
@@ -1551,7 +1622,13 @@ extern "C" int fcx_commit(fcx_engine *e) {
   // dominate it); 1: at any size; 0: never.  Caller heap arrays always take mirrors.
   const int64_t n_big = std::max(e->n[0], std::max(e->n[1], e->n[2]));
   const bool small = n_big < 2 * e->min_chunk;
-  if (e->zero_copy == 1 || (e->zero_copy == 2 && small)) e->zc_active = map_host_arrays(e) > 0;
+  if (e->zero_copy == 1 || (e->zero_copy == 2 && small)) {
+    e->zc_active = map_host_arrays(e) > 0;
+    int staged = 0;
+    if (e->staging)
+      if (int r = map_staged(e, &staged)) return r;
+    e->zc_active = e->zc_active || staged > 0;
+  }
   bool any_external = false;
   for (auto &bf : e->bufs) any_external = any_external || bf.external;
   if (e->tiled_opt && !any_external && !e->bufs.empty()) {
@@ -1735,11 +1812,12 @@ static int copy_bufs(fcx_engine *e, const std::vector<int> &ids, bool h2d, std::
   if (more) xs.swap(*more);
   for (int b : ids) {
     const Buffer &bf = e->bufs[b];
-    if (bf.external || bf.n == 0) continue;
-    if (bf.st.sp >= 0) {
+    if (bf.n == 0) continue;
+    if (bf.st.sp >= 0) {  // (also a heap array whose mirror is a mapped arena image)
       xs.push_back(xfer_of(bf.st, bf.host, bf.n));
       continue;
     }
+    if (bf.external) continue;
     HIP_TRY(copy_cells(e, bf, 0, bf.n, h2d, e->stream));
   }
   return h2d ? stage_in(e, xs, e->stream) : stage_out(e, xs, e->stream);
@@ -1824,10 +1902,10 @@ extern "C" int fcx_download(fcx_engine *e, int phase) {
   std::vector<Xfer> xs;  // every staged download of the phase in one set of DMAs
   std::vector<int> ids = pl->writes;
   for (auto &f : e->atm_fields)
-    if ((f.phase & phase) && !f.external && e->n_atmos > 0) {
+    if ((f.phase & phase) && e->n_atmos > 0) {
       if (f.st.sp >= 0)
         xs.push_back(xfer_of(f.st, f.out_host, e->n_atmos));
-      else
+      else if (!f.external)
         HIP_TRY(get_atm(e, f.out_host, f.out_dev, e->stream));
     }
   if (int r = download_remaps(e, phase, e->stream, &xs)) return r;
@@ -1952,10 +2030,10 @@ static int run_remaps(fcx_engine *e, int phase) {
 static int download_remaps(fcx_engine *e, int phase, hipStream_t s, std::vector<Xfer> *xs) {
   for (auto &rm : e->remaps)
     for (auto &f : rm.fields)
-      if ((f.phase & phase) && !f.external && rm.n_dst > 0) {
+      if ((f.phase & phase) && rm.n_dst > 0) {
         if (f.st.sp >= 0)
           xs->push_back(xfer_of(f.st, f.out_host, rm.n_dst));
-        else
+        else if (!f.external)
           HIP_TRY(hipMemcpyAsync(f.out_host, f.out_dev, rm.n_dst * e->esize, hipMemcpyDeviceToHost, s));
       }
   return FCX_OK;
@@ -2048,18 +2126,19 @@ static int step_pipelined(fcx_engine *e, int phase, int32_t t, Plan *pl) {
   std::vector<int> din, dout;
   for (int b : pl->reads) {
     const Buffer &bf = e->bufs[b];
-    if (bf.external || bf.n == 0) continue;
+    if (bf.n == 0) continue;
     if (bf.st.sp >= 0) xin.push_back(xfer_of(bf.st, bf.host, bf.n));
-    else din.push_back(b);
+    else if (!bf.external) din.push_back(b);
   }
   for (int b : pl->writes) {
     const Buffer &bf = e->bufs[b];
-    if (bf.external || bf.n == 0) continue;
+    if (bf.n == 0) continue;
     if (bf.st.sp >= 0) xout.push_back(xfer_of(bf.st, bf.host, bf.n));
-    else dout.push_back(b);
+    else if (!bf.external) dout.push_back(b);
   }
   if (!xin.empty() || !xout.empty()) {
-    if (int r = stage_alloc(e)) return r;
+    if (int r = stage_alloc(e, xin)) return r;
+    if (int r = stage_alloc(e, xout)) return r;
     if (!e->pending_out.empty()) {  // earlier downloads still owe their host copies
       HIP_TRY(hipStreamSynchronize(e->stream));
       if (int r = stage_flush(e)) return r;
@@ -2117,15 +2196,15 @@ static int step_pipelined(fcx_engine *e, int phase, int32_t t, Plan *pl) {
   std::vector<Xfer> xa;  // atmosphere and remap outputs
   if (e->atmos_in_run || e->atm_done_fused)
     for (auto &f : e->atm_fields)
-      if ((f.phase & phase) && !f.external && e->n_atmos > 0) {
+      if ((f.phase & phase) && e->n_atmos > 0) {
         if (f.st.sp >= 0)
           xa.push_back(xfer_of(f.st, f.out_host, e->n_atmos));
-        else
+        else if (!f.external)
           HIP_TRY(get_atm(e, f.out_host, f.out_dev, e->s_out));
       }
   if (int r = download_remaps(e, phase, e->s_out, &xa)) return r;
-  if (!xa.empty()) {  // (the arena may hold only these: fields in library memory)
-    if (int r = stage_alloc(e)) return r;
+  if (!xa.empty()) {
+    if (int r = stage_alloc(e, xa)) return r;
     HIP_TRY(stage_dma(e, xa, 0, -1, false, e->s_out));
   }
   if (e->timing) HIP_TRY(hipEventRecord(e->ev1, e->s_out));
@@ -2140,9 +2219,9 @@ static int step_pipelined(fcx_engine *e, int phase, int32_t t, Plan *pl) {
 
 static bool host_bound(const fcx_engine *e, const Plan *pl) {
   for (int b : pl->reads)
-    if (!e->bufs[b].external) return true;
+    if (!e->bufs[b].external || e->bufs[b].st.sp >= 0) return true;
   for (int b : pl->writes)
-    if (!e->bufs[b].external) return true;
+    if (!e->bufs[b].external || e->bufs[b].st.sp >= 0) return true;
   return false;
 }
 

@@ -353,9 +353,13 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
   constexpr bool kHoldWind = kHoldAtm;
   // FCX_PREFETCH_TYPE (multi-type kernels): the bottom-side inputs of type s+1 (TSUR FICE
   // CMOI CHEA CMOM and the FARE of the averages) are loaded when type s starts, so that the
-  // wave does not stall on memory between two types; they cost VGPRs only while type s runs.
+  // wave does not stall on memory between two types.  The fused T = 2 kernels then hold
+  // 162 / 166 / 124 VGPRs (CCLM / MOM5 / RCO, was 150 / 144 / 116): still 3 / 3 / 4 waves per
+  // SIMD, no spills.  In one process over the same arrays (profiles/r03/ab_t2_prefetch.json,
+  // random map): T = 2 step 1.672 -> 1.625 ms, CCLM 5.14 -> 5.26 TB/s, MOM5 5.54 -> 5.67,
+  // RCO 5.26 -> 5.50.  0 (A/B): load each type's inputs when it starts.
 #ifndef FCX_PREFETCH_TYPE
-#define FCX_PREFETCH_TYPE 0
+#define FCX_PREFETCH_TYPE 1
 #endif
   constexpr bool kPrefetch = kReload && FCX_PREFETCH_TYPE;
   Vec<C, R> n_ts = {}, n_fi = {}, n_cmoi = {}, n_chea = {}, n_cmom = {}, n_fare = {};
@@ -704,10 +708,13 @@ __device__ __forceinline__ void segment_done(const AtmosFused &af, int64_t tile,
 #ifndef FCX_T1_ATMOS_BLOCKS
 #define FCX_T1_ATMOS_BLOCKS 1
 #endif
-// ... and the fp32 T=1 fused kernels (4 cells per lane): 1 = no register cap (CCLM 132, MOM5
-// 137 VGPRs: 3 waves per SIMD), 4 = at most 128 VGPRs (4 waves per SIMD)
+// ... and the fp32 T=1 fused CCLM / MOM5 kernels (4 cells per lane): 4 = at most 128 VGPRs,
+// 4 waves per SIMD, no spills (uncapped they take 132 / 137 VGPRs and 3 waves); in one
+// process over the same arrays (profiles/r03/ab_f32_4waves.json) CCLM 4.81 -> 5.19 TB/s,
+// MOM5 4.73 -> 5.08.  The fp32 RCO kernel (105 VGPRs, 4 waves either way) lost 5 % under the
+// cap and keeps none.  1 (A/B): no cap.
 #ifndef FCX_F32_ATMOS_BLOCKS
-#define FCX_F32_ATMOS_BLOCKS 1
+#define FCX_F32_ATMOS_BLOCKS 4
 #endif
 // waves per block of the fused kernel (the fp32 kernel's as an A/B knob)
 #ifndef FCX_F32_ATMOS_WAVES  // A/B: 2 paid while the fp32 rows held fp64 products (13.8 KB/wave)
@@ -717,7 +724,10 @@ template <int C>
 constexpr int atmos_waves() { return C == 4 ? FCX_F32_ATMOS_WAVES : 4; }
 template <int C, class R, int VAR, bool NT, int TM, bool RAVG, bool REC = false>
 // (REC: the record stores took CCLM to 129 VGPRs and 3 waves per SIMD; capped at 4 blocks = 4 waves)
-__global__ __launch_bounds__(64 * atmos_waves<C>(), RAVG ? FCX_RAVG_ATMOS_BLOCKS : REC ? 4 : C == 4 ? FCX_F32_ATMOS_BLOCKS : FCX_T1_ATMOS_BLOCKS) void cells_atmos_kernel(const Params *__restrict__ P,
+__global__ __launch_bounds__(64 * atmos_waves<C>(), RAVG  ? FCX_RAVG_ATMOS_BLOCKS
+                                                  : REC ? 4
+                                                  : (C == 4 && VAR != 3) ? FCX_F32_ATMOS_BLOCKS
+                                                                         : FCX_T1_ATMOS_BLOCKS) void cells_atmos_kernel(const Params *__restrict__ P,
                                                           const double *__restrict__ corr_m,
                                                           const AtmosFused af, int64_t lo, int64_t hi) {
   static_assert(!RAVG || (C == 2 && sizeof(R) == 8), "register averages: fp64 engine only");

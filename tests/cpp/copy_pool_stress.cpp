@@ -28,7 +28,7 @@ int main(int argc, char **argv) {
       off += bytes;
     }
     if (b % 997 == 0) usleep(300);  // workers go to sleep in between
-    fcx::CopyPool::get().run(jobs, threads);
+    fcx::CopyPool::get().run(jobs, threads, (b & 1) != 0);
     if (std::memcmp(dst.data(), src.data(), off) != 0) {
       std::printf("batch %d: wrong bytes\n", b);
       return 1;

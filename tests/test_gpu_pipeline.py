@@ -93,12 +93,14 @@ def test_pipeline_generic_kernel_separate_grids_and_averages():
 
 @pytest.mark.parametrize("n", [3_000, 32_768])
 @pytest.mark.parametrize("atmos", [False, True])
-def test_staging_matches_runtime_copies(n, atmos):
+@pytest.mark.parametrize("zero_copy", [0, 1])
+def test_staging_matches_runtime_copies(n, atmos, zero_copy):
     """The Baltic-size step (32,768 cells) and small arrays several to a heap page (3,000
-    cells, T = 2): the staging arena gives the bits of one runtime copy per array, with the
-    atmosphere outputs staged too; only the staged engine holds an arena."""
+    cells, T = 2): the staging arena -- moved by DMA (zero_copy 0) or used by the kernels in
+    place (zero_copy 1, the small-grid default) -- gives the bits of one runtime copy per
+    array, with the atmosphere outputs staged too; only the staged engine holds an arena."""
     case = build_case("CCLM", n=n, T=2 if n < 10_000 else 1, bias=True)
-    a = run(case, {"pipeline_chunks": 2}, atmos_n=n if atmos else None)
+    a = run(case, {"pipeline_chunks": 2, "zero_copy": zero_copy}, atmos_n=n if atmos else None)
     b = run(case, {"pipeline_chunks": 1, "host_staging": 0}, atmos_n=n if atmos else None)
     same_bits(a, b)
     eng = Engine(case.lf, case.num_surface_types, case.methods, corrections=case.corrections,

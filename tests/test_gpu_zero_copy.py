@@ -205,13 +205,20 @@ def test_library_pinned_arrays_zero_copy(variant, n):
 
 
 @pytest.mark.parametrize("zero_copy", [0, 1, 2])
-def test_heap_arrays_never_used_in_place(zero_copy):
-    """Caller heap arrays take device mirrors whatever FCX_OPT_ZERO_COPY says."""
+@pytest.mark.parametrize("staging", [0, 1])
+def test_heap_arrays_never_used_in_place(zero_copy, staging):
+    """Caller heap arrays are never what a kernel addresses, whatever FCX_OPT_ZERO_COPY says:
+    with zero-copy and the staging arena the kernels use the library's mapped arena image of
+    them in place (the small-grid default), otherwise device mirrors."""
     c = build_case("CCLM", n=4097, T=1)
-    e = engine_for(c, zero_copy=zero_copy)
-    assert not e.zero_copy_active()
-    e.step(PHASE_ALL, T_STEP)
-    check(c, "mirrors")
+    e = engine_for(c, zero_copy=zero_copy, host_staging=staging)
+    assert e.zero_copy_active() == bool(zero_copy and staging)
+    for (s, g, name), a in c.lf.field.items():
+        assert e.device_ptr(s, g, name) != a.ctypes.data, (s, g, name)
+    for k in range(3):
+        reset_outputs(c)
+        e.step(PHASE_ALL, T_STEP)
+        check(c, f"step {k}")
     e.close()
 
 
