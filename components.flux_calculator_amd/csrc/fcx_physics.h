@@ -102,38 +102,6 @@ __device__ __forceinline__ R hsen_cclm(R a, R pa, R ps, R qs, R ta, R ts, R vel)
   return fa * R(kCp) * (ts - ta * ef);
 }
 
-// The same three CCLM/MOM5 formulas split at their type-independent factors, for kernels that
-// run several surface types over one set of atmosphere inputs (the operations and their order
-// are those above, so the results are bit-identical):
-//   fa_num = (a * max(vel, u_min)) * ps     (meva_cclm / hsen_cclm numerator, a = AMOI)
-//   taef   = ta * (ps / pa)**(Rd / cp)       (hsen_cclm)
-//   mom_num = (a * vel) * ps                 (mom_cclm_rate numerator, a = AMOM)
-template <class R>
-__device__ __forceinline__ R fa_num(R a, R ps, R vel) {
-  return a * fmax(vel, R(kUmin)) * ps;
-}
-template <class R>
-__device__ __forceinline__ R ta_exner(R pa, R ps, R ta) {
-  return ta * pow_exner(ps / pa, R(kRd / kCp));
-}
-template <class R>
-__device__ __forceinline__ R meva_cclm_pre(R num, R qa, R qs, R ta) {
-  FCX_TRIVIAL(num + qa + qs + ta)
-  const R fa = num / (R(kRd) * t_tilde(ta, qs));
-  return fa * (qs - qa);
-}
-template <class R>
-__device__ __forceinline__ R hsen_cclm_pre(R num, R qa, R ts, R taef) {
-  FCX_TRIVIAL(num + qa + ts + taef)
-  const R fa = num / (R(kRd) * t_tilde(ts, qa));
-  return fa * R(kCp) * (ts - taef);
-}
-template <class R>
-__device__ __forceinline__ R mom_cclm_rate_pre(R num, R qs, R ts) {
-  FCX_TRIVIAL(num + qs + ts)
-  return num / (R(kRd) * t_tilde(ts, qs));
-}
-
 // flux_lib/heat/flux_heat_sensible.F90:136-165 (flux_heat_sensible_rco)
 template <class R>
 __device__ __forceinline__ R hsen_rco(R ta, R ts, R vel) {
