@@ -2139,8 +2139,10 @@ static int step_pipelined(fcx_engine *e, int phase, int32_t t, Plan *pl) {
   if (!xin.empty() || !xout.empty()) {
     if (int r = stage_alloc(e, xin)) return r;
     if (int r = stage_alloc(e, xout)) return r;
-    if (!e->pending_out.empty()) {  // earlier downloads still owe their host copies
-      HIP_TRY(hipStreamSynchronize(e->stream));
+    bool mapped = false;  // (FCX_OPT_ZERO_COPY = 1 on a large grid: the kernels read the arena)
+    for (const Xfer &x : xin) mapped = mapped || e->spools[(size_t)x.sp].mapped;
+    if (!e->pending_out.empty() || mapped) {  // earlier downloads still owe their host copies,
+      HIP_TRY(hipStreamSynchronize(e->stream));  // or an earlier launch may still read the image
       if (int r = stage_flush(e)) return r;
     }
     if (e->stage_in_live) HIP_TRY(hipEventSynchronize(e->ev_stage_in));

@@ -68,6 +68,8 @@ def test_pipeline_chunkings_bit_identical(variant):
     for chunks in (2, 3, 8, 97):
         same_bits(run(case, {"pipeline_chunks": chunks}), seq)
         same_bits(run(case, {"pipeline_chunks": chunks, "host_staging": 0}), seq)
+    # the heap arrays' arena used in place by every chunk launch (zero-copy forced)
+    same_bits(run(case, {"pipeline_chunks": 8, "zero_copy": 1}), seq)
     ref = oracle_lib.run_case(case, "c", current_step_time=STEP_T)
     assert_parity(seq, ref, label=variant)
 
