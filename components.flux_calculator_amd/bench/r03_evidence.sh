@@ -1,0 +1,20 @@
+#!/bin/bash
+# Round-3 evidence of one build: GPU suite, smoke, the default bench line with the driver's
+# arguments, the T = 2 / fp32 / bias lines, and the two-rank rehearsal of the bench's N > 1
+# path (gloo, both ranks on GPU 0).  Output under gpurun_out/$1.
+set -uo pipefail
+export TMPDIR=/tmp
+O=gpurun_out/${1:-r03_evidence}
+mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/gpu_tests.log 2>&1
+rc=$?
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "gpu tests rc=$rc: stopping"; exit $rc; fi
+timeout -k 10 120 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit $?
+/usr/bin/time -f "%e s wall" -o $O/bench_w5_wall.txt timeout -k 10 400 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_w5.json || exit $?
+timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 --no-cpu --e2e 0 --types 2 > $O/bench_T2.json || exit $?
+timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 --no-cpu --e2e 0 --precision f32 > $O/bench_f32.json || exit $?
+timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 --no-cpu --e2e 0 --bias > $O/bench_bias.json || exit $?
+timeout -k 10 300 python3 -m torch.distributed.run --nnodes 1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+  --master-port 29533 bench.py --gpus 2 --backend gloo --same-device --steps 10 --warmup 5 --no-cpu --e2e 0 \
+  --other-map 0 --config4 0 > $O/bench_rehearsal_2ranks_gloo.json 2> $O/rehearsal.err || exit $?
+exit $rc
