@@ -186,6 +186,7 @@ struct fcx_engine {
   int32_t atm_maxseg = 0;
   double *d_atm_xrec = nullptr;    // [tiles][kXRec] crossing records (fix-up kernel)
   int64_t atm_crossings = 0;       // 128-cell tile boundaries inside a segment of the map
+  bool atm_halo = true;            // FCX_OPT_ATMOS_HALO: halo tiles where they apply
   double *d_atm_w = nullptr;
   std::vector<AtmosField> atm_fields;
   double *atm_shared = nullptr;
@@ -1847,10 +1848,20 @@ static int launch_plan(fcx_engine *e, Plan *pl, const double *corr_m, int64_t lo
     pl->af.stride = e->atm_stride;
     pl->af.left = e->atm_left;
     pl->af.right = e->atm_right;
+    // halo tiles instead of crossing records + fix-up: a launch over the whole grid (not a
+    // pipelined chunk) of one surface type, on a map whose segments are short enough that
+    // `halo` lanes of the next tile's head (at most 1/16 of a wave) cover every crossing
+    lc.halo = 0;
+    const int cpl = e->f32 ? 4 : 2;
+    const int h = (e->atm_maxseg - 1 + cpl - 1) / cpl;
+    if (e->atm_halo && e->atm_crossings > 0 && lo == 0 && (hi < 0 || hi >= pl->host.n_max) &&
+        pl->host.num_types == 1 && h >= 1 && h <= (e->f32 ? 2 : 4))
+      lc.halo = h;
+    pl->af.halo = lc.halo;
   }
   const int r = launch_cells(&pl->host, pl->dev, corr_m, lc, e->stream, fused ? &pl->af : nullptr);
   if (r) return fail(FCX_E_HIP, "cells_kernel launch: %s", hipGetErrorString((hipError_t)r));
-  if (fused && fixup && e->atm_crossings > 0) {
+  if (fused && fixup && e->atm_crossings > 0 && !lc.halo) {
     const int r2 = launch_atmos_fixup(pl->af, pl->host.n_max, lc.f32, e->stream);
     if (r2) return fail(FCX_E_HIP, "atmos_fixup launch: %s", hipGetErrorString((hipError_t)r2));
   }
@@ -2486,6 +2497,9 @@ extern "C" int fcx_set_option(fcx_engine *e, int option, int64_t value) {
     case FCX_OPT_PIPELINE_CHUNKS:
       if (value < 1 || value > 1024) return fail(FCX_E_ARG, "pipeline chunks %lld outside 1..1024", (long long)value);
       e->chunks = (int)value;
+      return FCX_OK;
+    case FCX_OPT_ATMOS_HALO:
+      e->atm_halo = value != 0;
       return FCX_OK;
     case FCX_OPT_HOST_STAGING:
       if (e->committed) return fail(FCX_E_STATE, "host_staging is applied at fcx_commit");

@@ -135,6 +135,7 @@ struct LaunchConfig {
                              // hi < 0: to n_max) -- the pipelined host-bound step
   bool rec = false;          // Params::rec set: the launch also writes remap records
                              // (T=1 specialised fp64 kernels, 2 cells per lane)
+  int halo = 0;              // fused accumulation with halo tiles (AtmosFused::halo lanes)
 };
 constexpr int64_t kChunkAlign = 1024;  // chunk boundaries: whole wave tiles and vectors
 
@@ -193,7 +194,11 @@ struct AtmosFused {
                        // and {head cells, their atmosphere cell} of tile t (int2 at double 30);
                        // fp32 engines index the records by their 256-cell tiles
   int32_t xrec_on;     // some segment crosses a tile boundary: the launch fills the records
-  int32_t pad0;
+  int32_t halo;        // > 0: halo tiles (no records, no fix-up): a wave owns the cells of its
+                       // first 64 - halo lanes and computes the fluxes of the last `halo`
+                       // lanes' cells -- the head of the next tile -- for its products only,
+                       // so every segment that starts in its own cells ends inside the wave
+                       // (needs halo * C >= the longest segment - 1; full-range launches)
   int64_t n_atmos;
   double *shared;
   int32_t stride, left, right;

@@ -290,22 +290,26 @@ struct RecEmit {
 // by the pass, so a held value is the array's value.
 // TM: 1 = one surface type, fixed at compile time (the held inputs and the type loop
 // vanish); 0 = T from the parameter block.  RAVG (register averages) needs TM = 0.
+// HALO: cells at or past st_end are a halo tile's head cells -- their fluxes are computed for
+// the fused accumulation's products, nothing of them is stored (the next tile's wave stores).
 template <int C, bool MERGED, int VAR, bool NT, class R = double, int TM = 1, bool RAVG = false,
-          class Emit = NoEmit, bool REC = false>
+          class Emit = NoEmit, bool REC = false, bool HALO = false>
 __device__ __forceinline__ void process(const Params *__restrict__ P, const double *__restrict__ corr_m,
                                         int64_t j0, const Emit &emit_in = Emit(),
-                                        AccLds<C, R> acc_lds = AccLds<C, R>{nullptr, 0}) {
+                                        AccLds<C, R> acc_lds = AccLds<C, R>{nullptr, 0}, int64_t st_end = 0) {
   static_assert(!(RAVG && TM), "register averages need more than one surface type");
   static_assert(!REC || (TM == 1 && !RAVG), "remap records: the T=1 launch");
+  static_assert(!HALO || (TM == 1 && !RAVG), "halo tiles: the T=1 launch");
   const uint32_t stages = P->stages;
   const int T = TM ? 1 : P->num_types;
   const int64_t nt = P->n[0];
+  const int64_t ns = HALO ? min(nt, st_end) : nt;  // stores of the t-grid (and merged u/v) cells
   const bool do_t = j0 < nt;
   using SinkEmit = typename std::conditional<REC, RecEmit<C, R, Emit>, const Emit &>::type;
   SinkEmit emit = [&]() -> SinkEmit {
     if constexpr (REC)
       return RecEmit<C, R, Emit>{emit_in, reinterpret_cast<R *>(P->rec) + j0 * P->rec_p, P->rec_p, P->rec_pos,
-                                 (int)min((int64_t)C, nt - j0)};
+                                 (int)max((int64_t)0, min((int64_t)C, ns - j0))};
     else
       return emit_in;
   }();
@@ -441,17 +445,17 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
         Vec<C, R> r;
         if (tp.m_rbbr == FCX_STBO) {
           FOR_C r.v[i] = rbbr_stbo(ts.v[i]);
-          ST(g.rbbr, j0, nt, r);
+          ST(g.rbbr, j0, ns, r);
           sink(A_RBBR, r);
         } else if (tp.m_rbbr == FCX_ZERO) {
-          ST(g.rbbr, j0, nt, splat<C, R>(R(0)));
+          ST(g.rbbr, j0, ns, splat<C, R>(R(0)));
           sink(A_RBBR, splat<C, R>(R(0)));
         }
       }
       // ---- calc_spec_vapor_surface(t) (calc:37-49)
       if ((stages & S_QSUR_T) && m_q == FCX_CCLM) {
         FOR_C qs.v[i] = qsur_cclm(fi.v[i], ps.v[i], ts.v[i]);
-        if (g.qsur) ST(g.qsur, j0, nt, qs);
+        if (g.qsur) ST(g.qsur, j0, ns, qs);
       }
       // ---- calc_flux_mass_evap (calc:75-118), P2: TATM in the T_s slot
       if (stages & S_MEVA) {
@@ -471,7 +475,7 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
           for (int b = 0; b < tp.bias_adds; ++b) {
             FOR_C me.v[i] = me.v[i] + corr.v[i];
           }
-          if (g.meva) ST(g.meva, j0, nt, me);
+          if (g.meva) ST(g.meva, j0, ns, me);
           sink(A_MEVA, me);
         }
       }
@@ -480,13 +484,13 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
         Vec<C, R> h;
         if (tp.m_hlat == FCX_WATER) {
           FOR_C h.v[i] = me.v[i] * R(kLv);
-          ST(g.hlat, j0, nt, h);
+          ST(g.hlat, j0, ns, h);
         } else if (tp.m_hlat == FCX_ICE) {
           FOR_C h.v[i] = me.v[i] * R(kLs);
-          ST(g.hlat, j0, nt, h);
+          ST(g.hlat, j0, ns, h);
         } else if (tp.m_hlat == FCX_ZERO) {
           h = splat<C, R>(R(0));
-          ST(g.hlat, j0, nt, h);
+          ST(g.hlat, j0, ns, h);
         }
         if (tp.m_hlat == FCX_WATER || tp.m_hlat == FCX_ICE || tp.m_hlat == FCX_ZERO) sink(A_HLAT, h);
       }
@@ -497,13 +501,13 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
         if (m == FCX_CCLM || m == FCX_MOM5) {
           const Vec<C, R> &a = (m == FCX_CCLM) ? amoi : chea;
           FOR_C h.v[i] = hsen_cclm(a.v[i], pa.v[i], ps.v[i], qa.v[i], ta.v[i], ts.v[i], vel.v[i]);
-          ST(g.hsen, j0, nt, h);
+          ST(g.hsen, j0, ns, h);
         } else if (m == FCX_RCO) {
           FOR_C h.v[i] = hsen_rco(ta.v[i], ts.v[i], vel.v[i]);
-          ST(g.hsen, j0, nt, h);
+          ST(g.hsen, j0, ns, h);
         } else if (m == FCX_ZERO) {
           h = splat<C, R>(R(0));
-          ST(g.hsen, j0, nt, h);
+          ST(g.hsen, j0, ns, h);
         }
         if (m == FCX_CCLM || m == FCX_MOM5 || m == FCX_RCO || m == FCX_ZERO) sink(A_HSEN, h);
       }
@@ -517,19 +521,19 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
             if (!((stages & S_QSUR_T) && m_q == FCX_CCLM)) {
               FOR_C qs.v[i] = qsur_cclm(fi.v[i], ps.v[i], ts.v[i]);
             }
-            ST(gk.qsur, j0, nt, qs);
+            ST(gk.qsur, j0, ns, qs);
           }
         }
         const bool do_u = (stages & S_UMOM) && tp.uv[0].mom;
         const bool do_v = (stages & S_VMOM) && tp.uv[1].mom;
         if (do_u || do_v) {
           const Vec<C, R> &a = (m_mo == FCX_MOM5) ? cmom : amom;
-          if (do_u) momentum<C, NT, R>(m_mo, false, tp.uv[0], ts, ps, u, v, vel, qs, a, j0, nt, D_, sink, A_UMOM);
-          if (do_v) momentum<C, NT, R>(m_mo, true, tp.uv[1], ts, ps, u, v, vel, qs, a, j0, nt, D_, sink, A_VMOM);
+          if (do_u) momentum<C, NT, R>(m_mo, false, tp.uv[0], ts, ps, u, v, vel, qs, a, j0, ns, D_, sink, A_UMOM);
+          if (do_v) momentum<C, NT, R>(m_mo, true, tp.uv[1], ts, ps, u, v, vel, qs, a, j0, ns, D_, sink, A_VMOM);
         }
       }
       // ---- distribute_shortwave_radiation_flux (calc:355-362): RSDR_s = RSDD_0
-      if ((stages & S_RSDR) && g.rsdr) ST(g.rsdr, j0, nt, rsdd);
+      if ((stages & S_RSDR) && g.rsdr) ST(g.rsdr, j0, ns, rsdd);
     }
     if constexpr (!MERGED) {
       if (j0 < P->n[1]) uv_grid<C, NT, R>(tp, 0, stages, j0, P->n[1], D_);
@@ -548,7 +552,7 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
       for (int k = 0; k < kAvgSlots; ++k) {
         if (!P->ravg.out[k]) continue;
         const Vec<C, R> avg = sink.acc.get(k);
-        ST(P->ravg.out[k], j0, nt, avg);
+        ST(P->ravg.out[k], j0, ns, avg);
         if (k < kFusedFields) emit(k, avg);  // the type-0 field OASIS sends on
       }
     }
@@ -564,7 +568,7 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
         const Vec<C, R> f = LD(ae.fare[s], j0, n);
         FOR_C acc.v[i] = acc.v[i] + x.v[i] * f.v[i];
       }
-      ST(ae.x0, j0, n, acc);
+      ST(ae.x0, j0, HALO ? min(n, st_end) : n, acc);
     }
   }
 }
@@ -722,7 +726,12 @@ __device__ __forceinline__ void segment_done(const AtmosFused &af, int64_t tile,
 #endif
 template <int C>
 constexpr int atmos_waves() { return C == 4 ? FCX_F32_ATMOS_WAVES : 4; }
-template <int C, class R, int VAR, bool NT, int TM, bool RAVG, bool REC = false>
+// HALO (T = 1, full-range launches, maps whose segments are at most halo * C + 1 cells): a
+// wave owns the first 64 - halo lanes' cells of its tile and computes the last `halo` lanes'
+// cells -- the head of the next tile -- only for their products (nothing of them is stored),
+// so every segment that starts in its own cells is summed inside the wave: no crossing
+// records, no fix-up launch.  Tiles are (64 - halo) * C cells apart.
+template <int C, class R, int VAR, bool NT, int TM, bool RAVG, bool REC = false, bool HALO = false>
 // (REC: the record stores took CCLM to 129 VGPRs and 3 waves per SIMD; capped at 4 blocks = 4 waves)
 __global__ __launch_bounds__(64 * atmos_waves<C>(), RAVG  ? FCX_RAVG_ATMOS_BLOCKS
                                                   : REC ? 4
@@ -739,16 +748,19 @@ __global__ __launch_bounds__(64 * atmos_waves<C>(), RAVG  ? FCX_RAVG_ATMOS_BLOCK
   constexpr bool kXF = sizeof(R) == 4;  // LDS holds fp32 fluxes + fp64 weights
   static_assert(!kXF || C == 4, "fp32 flux rows: 4 cells per lane");
   __shared__ double s_p[atmos_waves<C>()][wave_lds_doubles<R, C>(kRows)];
+  static_assert(!HALO || (TM == 1 && !RAVG), "halo tiles: the T=1 launch");
   const int64_t n = P->n_max;
-  const int64_t n_tiles = (hi + kT - 1) / kT;  // tiles [lo/kT, n_tiles) of this launch
+  const int own_lanes = HALO ? 64 - af.halo : 64;
+  const int64_t kO = (int64_t)C * own_lanes;  // cells a tile owns (HALO: lo == 0)
+  const int64_t n_tiles = (hi + kO - 1) / kO;  // tiles [lo/kT, n_tiles) of this launch
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   double *wp = s_p[wv];
   const int64_t waves = (int64_t)gridDim.x * (blockDim.x >> 6);
   const int64_t wave0 = (int64_t)xcd_block(blockIdx.x, gridDim.x) * (blockDim.x >> 6) + wv;
   const uint64_t at_or_above = ~0ull << lane;
   const uint64_t above = lane == 63 ? 0ull : (~0ull << (lane + 1));
-  for (int64_t tile = lo / kT + wave0; tile < n_tiles; tile += waves) {
-    const int64_t t0 = tile * kT;
+  for (int64_t tile = lo / kO + wave0; tile < n_tiles; tile += waves) {
+    const int64_t t0 = tile * kO;
     const int64_t j0 = t0 + C * lane;
     LdsEmitT<C> emit{wp, {}, lds_slot(C * lane)};
     int32_t a[C];  // -1: past the grid end
@@ -784,8 +796,8 @@ __global__ __launch_bounds__(64 * atmos_waves<C>(), RAVG  ? FCX_RAVG_ATMOS_BLOCK
     const int64_t tend = t0 + kT;
     const int32_t next_a = (tend < n) ? af.idx[tend] : -3;
     if (j0 < n)
-      process<C, true, VAR, NT, R, TM, RAVG, LdsEmitT<C>, REC>(P, corr_m, j0, emit,
-                                             AccLds<C, R>{reinterpret_cast<R *>(wp + emit.s), kR});
+      process<C, true, VAR, NT, R, TM, RAVG, LdsEmitT<C>, REC, HALO>(
+          P, corr_m, j0, emit, AccLds<C, R>{reinterpret_cast<R *>(wp + emit.s), kR}, t0 + kO);
     if constexpr (kXF) {  // the weights row of the fp32 fluxes (dead cells: weight 0)
 #pragma unroll
       for (int h = 0; h < C / 2; ++h)
@@ -829,10 +841,10 @@ __global__ __launch_bounds__(64 * atmos_waves<C>(), RAVG  ? FCX_RAVG_ATMOS_BLOCK
       // theirs hold only values of segments that start in this tile (FCX_ATM_NT_STORE 2)
       const int32_t a_lo = __shfl(a[0], 0), a_hi = __shfl(a[C - 1], 63);
       constexpr int kLineCells = 128 / (int)sizeof(R);
-      uint32_t rem = 0;  // bit i: cell C*lane+i starts a segment not summed yet
+      uint32_t rem = 0;  // bit i: cell C*lane+i starts a segment not summed yet (an own cell)
 #pragma unroll
       for (int i = 0; i < C; ++i)
-        if (st[i] && a[i] >= 0) rem |= 1u << i;
+        if (st[i] && a[i] >= 0 && (!HALO || lane < own_lanes)) rem |= 1u << i;
       while (__ballot(rem != 0)) {
         if (rem) {
           const int i = __builtin_ctz(rem);
@@ -852,13 +864,14 @@ __global__ __launch_bounds__(64 * atmos_waves<C>(), RAVG  ? FCX_RAVG_ATMOS_BLOCK
           for (int k = 0; k < kFusedFields; ++k) acc[k] = 0.0;
           for (int e = c; e < end; ++e) add_cell(acc, e);
           const bool own = a_hi >= 0 && ai / kLineCells > a_lo / kLineCells && ai / kLineCells < a_hi / kLineCells;
-          segment_done<R>(af, tile, ai, acc, end == kT && next_a == ai, own);
+          // (HALO: the segment ends inside the wave's own + halo cells by the engine's rule)
+          segment_done<R>(af, tile, ai, acc, !HALO && end == kT && next_a == ai, own);
         }
       }
     } else {
 #pragma unroll
       for (int i = 0; i < C; ++i) {
-        if (!st[i] || a[i] < 0) continue;
+        if (!st[i] || a[i] < 0 || (HALO && lane >= own_lanes)) continue;
         const int c = C * lane + i;
         int e_end = kT;
 #pragma unroll
@@ -868,12 +881,12 @@ __global__ __launch_bounds__(64 * atmos_waves<C>(), RAVG  ? FCX_RAVG_ATMOS_BLOCK
 #pragma unroll
         for (int k = 0; k < kFusedFields; ++k) acc[k] = 0.0;
         for (int e = c; e < end; ++e) add_cell(acc, e);
-        segment_done<R>(af, tile, a[i], acc, end == kT && next_a == a[i]);
+        segment_done<R>(af, tile, a[i], acc, !HALO && end == kT && next_a == a[i]);
       }
     }
     // the number of head cells (continuing the previous tile's segment) for
     // atmos_fixup_kernel; 0 when the tile starts a segment
-    if (af.xrec_on) {  // (a map whose segments never cross a tile needs no records)
+    if (!HALO && af.xrec_on) {  // (a map whose segments never cross a tile needs no records)
       int head = kT;
 #pragma unroll
       for (int q = 0; q < C; ++q) head = min(head, C * first_bit(m[q]) + q);
@@ -1196,15 +1209,15 @@ static void launch_r(const Params *hp, const LaunchConfig &lc, int blocks, hipSt
     launch_c<C, R, 0, false>(lc, blocks, s, dp, corr_m, lo, hi);
 }
 
-template <int C, class R, int VAR, int TM, bool RAVG, bool REC = false>
+template <int C, class R, int VAR, int TM, bool RAVG, bool REC = false, bool HALO = false>
 static void launch_atm(bool nt, int blocks, hipStream_t s, const Params *dp, const double *corr_m,
                        const AtmosFused &af, int64_t lo, int64_t hi) {
   if (nt)
-    hipLaunchKernelGGL((cells_atmos_kernel<C, R, VAR, true, TM, RAVG, REC>), dim3(blocks), dim3(64 * atmos_waves<C>()),
-                       0, s, dp, corr_m, af, lo, hi);
+    hipLaunchKernelGGL((cells_atmos_kernel<C, R, VAR, true, TM, RAVG, REC, HALO>), dim3(blocks),
+                       dim3(64 * atmos_waves<C>()), 0, s, dp, corr_m, af, lo, hi);
   else
-    hipLaunchKernelGGL((cells_atmos_kernel<C, R, VAR, false, TM, RAVG, REC>), dim3(blocks), dim3(64 * atmos_waves<C>()),
-                       0, s, dp, corr_m, af, lo, hi);
+    hipLaunchKernelGGL((cells_atmos_kernel<C, R, VAR, false, TM, RAVG, REC, HALO>), dim3(blocks),
+                       dim3(64 * atmos_waves<C>()), 0, s, dp, corr_m, af, lo, hi);
 }
 
 // fused accumulation: one surface type (its fluxes), or several with the type-0 averages in
@@ -1212,14 +1225,26 @@ static void launch_atm(bool nt, int blocks, hipStream_t s, const Params *dp, con
 template <int VAR>
 static int launch_atm_r(const Params *hp, const LaunchConfig &lc, int blocks, hipStream_t s, const Params *dp,
                         const double *corr_m, const AtmosFused &af, int64_t lo, int64_t hi) {
-  if (hp->num_types == 1 && lc.f32)  // fp32 engine: 4 cells per lane, T = 1 only
-    launch_atm<4, float, VAR, 1, false>(lc.nontemporal, blocks, s, dp, corr_m, af, lo, hi);
-  else if (lc.f32)
+  const bool halo = lc.halo > 0;
+  if (halo && (hp->num_types != 1 || lo != 0)) return (int)hipErrorInvalidValue;
+  if (hp->num_types == 1 && lc.f32) {  // fp32 engine: 4 cells per lane, T = 1 only
+    if (halo)
+      launch_atm<4, float, VAR, 1, false, false, true>(lc.nontemporal, blocks, s, dp, corr_m, af, lo, hi);
+    else
+      launch_atm<4, float, VAR, 1, false>(lc.nontemporal, blocks, s, dp, corr_m, af, lo, hi);
+  } else if (lc.f32) {
     return (int)hipErrorInvalidValue;
-  else if (hp->num_types == 1 && lc.rec)
-    launch_atm<2, double, VAR, 1, false, true>(lc.nontemporal, blocks, s, dp, corr_m, af, lo, hi);
-  else if (hp->num_types == 1)
-    launch_atm<2, double, VAR, 1, false>(lc.nontemporal, blocks, s, dp, corr_m, af, lo, hi);
+  } else if (hp->num_types == 1 && lc.rec) {
+    if (halo)
+      launch_atm<2, double, VAR, 1, false, true, true>(lc.nontemporal, blocks, s, dp, corr_m, af, lo, hi);
+    else
+      launch_atm<2, double, VAR, 1, false, true>(lc.nontemporal, blocks, s, dp, corr_m, af, lo, hi);
+  } else if (hp->num_types == 1) {
+    if (halo)
+      launch_atm<2, double, VAR, 1, false, false, true>(lc.nontemporal, blocks, s, dp, corr_m, af, lo, hi);
+    else
+      launch_atm<2, double, VAR, 1, false>(lc.nontemporal, blocks, s, dp, corr_m, af, lo, hi);
+  }
   else if (lc.ravg)
     launch_atm<2, double, VAR, 0, true>(lc.nontemporal, blocks, s, dp, corr_m, af, lo, hi);
   else
@@ -1236,7 +1261,7 @@ int launch_cells(const Params *hp, const Params *dp, const double *corr_m, const
   if (atm) {  // fused accumulation: T=1 specialised merged kernel, 2 cells per lane
     // four waves per block (fp32: two), one 128-cell (fp32: 256-cell) tile per wave and trip.  Default: one trip (full
     // grid) -- +2 % per T=1 step over the 8192-block cap, equal at T=2 (profiles/r01/grid_ab)
-    const int64_t kt = lc.f32 ? tile_cells<4>() : tile_cells<2>();
+    const int64_t kt = (lc.f32 ? 4 : 2) * (64 - lc.halo);  // cells a wave tile owns
     const int64_t kw = lc.f32 ? atmos_waves<4>() : atmos_waves<2>();
     const int64_t tiles = (hi - lo + kt - 1) / kt;
     const int64_t full = (tiles + kw - 1) / kw;

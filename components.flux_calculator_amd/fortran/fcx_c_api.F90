@@ -23,7 +23,8 @@ MODULE fcx_c_api
   INTEGER(c_int), PARAMETER :: FCX_OPT_NONTEMPORAL = 3, FCX_OPT_ATMOS_IN_RUN = 5, &
                                FCX_OPT_PIPELINE_CHUNKS = 7, FCX_OPT_ZERO_COPY = 9, FCX_OPT_TIMING = 10, &
                                FCX_OPT_TILED_LAYOUT = 11, FCX_OPT_REMAP_PACK = 13, &
-                               FCX_OPT_HOST_STAGING = 15, FCX_OPT_HOST_THREADS = 16
+                               FCX_OPT_HOST_STAGING = 15, FCX_OPT_HOST_THREADS = 16, &
+                               FCX_OPT_ATMOS_HALO = 17
   ! the RCCL unique id travels between the ranks as these many bytes (MPI_Bcast)
   INTEGER, PARAMETER :: FCX_COMM_ID_BYTES = 128
 

@@ -272,8 +272,14 @@ enum fcx_option {
                                    Nothing of the caller's memory is ever page-locked or
                                    mapped.  Applied at fcx_commit                          */
   FCX_OPT_HOST_THREADS = 16,    /* host threads of those copies (the calling thread
-                                   included); 0 (default): min(8, OMP_NUM_THREADS if set,
+                                   included); 0 (default): min(16, OMP_NUM_THREADS if set,
                                    else the CPUs of the process affinity set)              */
+  FCX_OPT_ATMOS_HALO = 17,      /* fused accumulation of one surface type, launched over the
+                                   whole grid, on a map whose segments are at most 9 cells:
+                                   1 (default) halo tiles -- each wave also computes the
+                                   head cells of the next tile for their products, so every
+                                   segment completes inside the launch (no crossing records,
+                                   no fix-up launch); 0: crossing records + fix-up launch  */
   FCX_OPT_REMAP_PACK = 13,      /* exchange -> model remaps: the fields of a launch packed
                                    cell-major into one record per exchange cell before the
                                    gather, so a link reads one record instead of nf

@@ -195,16 +195,18 @@ def test_fp32_engine_rejects_fp64_outputs():
         Engine(c32.lf, 1, c32.methods, atmos={"local": la, "fields": [(2, 1, 1, "MEVA", np.zeros(la.n_atmos))]})
 
 
-# run lengths: 1..7 and 40..64 (the fp32 fused kernel, 256-cell wave tiles: segments within
-# a tile or crossing one boundary), 1..400 (longer than half a 128-cell tile: atmos_kernel)
-@pytest.mark.parametrize("lengths", [(1, 5), (1, 7), (40, 64), (1, 400)])
-@pytest.mark.parametrize("mode", ["fixup", "capped", "pipelined", "pipelined_runtime"])
+# run lengths: 1..5, 1..9 (the fp32 fused kernel's halo tiles: 1 and 2 halo lanes of 4 cells),
+# 1..10 and 40..64 (256-cell wave tiles crossed: records + fix-up), 1..400 (longer than half a
+# 128-cell tile: atmos_kernel)
+@pytest.mark.parametrize("lengths", [(1, 5), (1, 9), (1, 10), (40, 64), (1, 400)])
+@pytest.mark.parametrize("mode", ["default", "nohalo", "capped", "pipelined", "pipelined_runtime"])
 @pytest.mark.parametrize("variant", ["CCLM", "MOM5", "RCO"])
 def test_fp32_fused_accumulation(variant, mode, lengths):
     """The fp32 engine's flux kernel with the accumulation fused in (4 cells per lane,
-    products and sums in fp64, outputs rounded once): carries between 256-cell tiles completed
-    by the fix-up kernel, across the chunk launches of the pipelined step (staging arena, and
-    one runtime copy per array), and the separate kernel under a grid-stride cap.  Bit-identical to the sequential fp64 sum of the GPU's own
+    products and sums in fp64, outputs rounded once): segments across 256-cell tiles completed
+    by halo tiles (default) or by the fix-up kernel (FCX_OPT_ATMOS_HALO 0, long segments, the
+    chunk launches of the pipelined step through the staging arena and through runtime copies),
+    and under a grid-stride cap.  Bit-identical to the sequential fp64 sum of the GPU's own
     fp32 fluxes, rounded once; the fluxes within the fp32 gate of the oracle."""
     from fcx.parallel import local_atmos
     from test_gpu_multirank import random_run_map
@@ -216,7 +218,7 @@ def test_fp32_fused_accumulation(variant, mode, lengths):
     la = local_atmos(amap, 0, 1)
     outs = {k: np.full(la.n_atmos, np.nan, np.float32) for k, _ in ATM_FIELDS}
     pipe = {"pipeline_chunks": 4, "pipeline_min_chunk": 65536, "zero_copy": 0}
-    opts = {"fixup": {}, "capped": {"max_blocks": 64}, "pipelined": pipe,
+    opts = {"default": {}, "nohalo": {"atmos_halo": 0}, "capped": {"max_blocks": 64}, "pipelined": pipe,
             "pipelined_runtime": {**pipe, "host_staging": 0}}[mode]
     eng = Engine(c32.lf, 1, c32.methods, corrections=c32.corrections,
                  atmos={"local": la, "fields": [(2, 1, g, k, outs[k]) for k, g in ATM_FIELDS]}, options=opts)

@@ -79,17 +79,19 @@ def random_run_map(n, lengths, seed):
     return AtmosMap(np.ascontiguousarray(idx, dtype=np.int32), np.ascontiguousarray(w), n_atmos)
 
 
-# run lengths: 1..7 and 20..64 (the fused kernel: segments within a tile or crossing one
-# boundary; heads longer than the fix-up's kHeadCells = 16 kept products are recomputed);
-# 130..140 and 1..400 (longer than half a tile: the engine runs atmos_kernel instead)
-@pytest.mark.parametrize("lengths", [(1, 5), (1, 7), (20, 64), (130, 140), (1, 400)])
-@pytest.mark.parametrize("mode", ["fixup", "capped", "pipelined", "pipelined_runtime"])
+# run lengths: 1..5, 1..7, 1..9 (halo tiles: 1, 3 and 4 halo lanes), 1..10 (one cell too long
+# for the halo: crossing records + fix-up), 20..64 (the fix-up; heads longer than the records'
+# kRecHead kept products are recomputed); 130..140 and 1..400 (longer than half a tile: the
+# engine runs atmos_kernel instead)
+@pytest.mark.parametrize("lengths", [(1, 5), (1, 7), (1, 9), (1, 10), (20, 64), (130, 140), (1, 400)])
+@pytest.mark.parametrize("mode", ["default", "nohalo", "capped", "pipelined", "pipelined_runtime"])
 def test_fused_accumulation_long_segments(lengths, mode):
-    """The accumulation with segments crossing 128-cell wave tiles: carries left to the fix-up
-    kernel (default one-trip grid, and a grid-stride cap), and across the chunk launches of
-    the pipelined host step (through the staging arena, and with one runtime copy per array);
-    long segments through atmos_kernel.  Bit-identical to the sequential sum of the GPU's own
-    fluxes."""
+    """The accumulation with segments crossing 128-cell wave tiles: completed inside the launch
+    by halo tiles (default, short segments, and under a grid-stride cap), by crossing records
+    and the fix-up kernel (FCX_OPT_ATMOS_HALO 0, or segments too long for the halo), and across
+    the chunk launches of the pipelined host step (through the staging arena, and with one
+    runtime copy per array); long segments through atmos_kernel.  Bit-identical to the
+    sequential sum of the GPU's own fluxes."""
     import torch
     from fcx.engine import Engine
     from fcx.parallel import local_atmos
@@ -102,7 +104,7 @@ def test_fused_accumulation_long_segments(lengths, mode):
             for name, _ in FIELDS}
     atmos = {"local": la, "fields": [(2, 1, g, name, outs[name]) for name, g in FIELDS]}
     pipe = {"pipeline_chunks": 4, "pipeline_min_chunk": 65536, "zero_copy": 0}
-    opts = {"fixup": {}, "capped": {"max_blocks": 64}, "pipelined": pipe,
+    opts = {"default": {}, "nohalo": {"atmos_halo": 0}, "capped": {"max_blocks": 64}, "pipelined": pipe,
             "pipelined_runtime": {**pipe, "host_staging": 0}}[mode]
     eng = Engine(case.lf, 1, case.methods, corrections=case.corrections, atmos=atmos, options=opts)
     for step in range(3):  # later runs reuse the crossing records
