@@ -44,6 +44,9 @@ def main():
                     help="NAME:key=val[,key=val] -- another engine set of the main build with these "
                          "fcx_set_option values (e.g. split0:type_split=0)")
     ap.add_argument("--precision", choices=("f64", "f32"), default="f64")
+    ap.add_argument("--streams", action="append", default=[],
+                    help="NAME: another engine set of the main build with every variant's engine on its "
+                         "own stream (forked from and joined back into the main stream every step)")
     ap.add_argument("--atmos-map", choices=("periodic", "random"), default="random",
                     help="exchange->atmosphere map (bench.py's default: random runs crossing the wave tiles)")
     ap.add_argument("--host", action="store_true",
@@ -59,6 +62,8 @@ def main():
     from fcx.synthetic import as_dtype, build_case, inputs_for_bench
 
     libs, no_atmos, extra_opts = {"ref": None}, set(), {}
+    for name in a.streams:
+        libs[name] = None
     for spec in a.opts:
         name, kv = spec.split(":", 1)
         libs[name] = None
@@ -93,32 +98,44 @@ def main():
                                         device=dev))
                      for name, _ in FIELDS})
     s0 = 0 if a.types >= 2 else 1
-    engines = {}
+    engines, estreams = {}, {}
     for lname, lib in libs.items():
+        estreams[lname] = ([torch.cuda.Stream(dev) for _ in variants] if lname in a.streams else
+                           [stream] * len(variants))
         engines[lname] = [
             Engine(c.lf, c.num_surface_types, c.methods, corrections=c.corrections, averages=c.averages,
-                   device=0, stream=stream.cuda_stream,
+                   device=0, stream=st.cuda_stream,
                    atmos=({"local": la, "fields": [(PHASE_NORMAL, s0, g, name, o[name]) for name, g in FIELDS]}
                           if a.atmos and lname not in no_atmos else None),
                    options={"atmos_in_run": 0, "timing": 0, "host_staging": 0, **extra_opts.get(lname, {})}, lib=lib)
-            for c, o in zip(cases, outs)]
+            for c, o, st in zip(cases, outs, estreams[lname])]
         if a.host:
             for e in engines[lname]:
                 e.upload(PHASE_ALL)
     alg = {k: [es[i].algorithmic_bytes(PHASE_ALL) for i in range(len(variants))] for k, es in engines.items()}
 
-    def step(es, t, ev=None):
+    def step(es, t, ev=None, sts=None):
+        fork = None
+        if sts is not None and sts[0] is not stream:
+            fork = torch.cuda.Event()
+            fork.record(stream)
         for i, e in enumerate(es):
+            st = stream if sts is None else sts[i]
+            if fork is not None:
+                st.wait_event(fork)
             if ev is not None:
-                ev[i][0].record(stream)
+                ev[i][0].record(st)
             e.run(PHASE_ALL, t)
             if ev is not None:
-                ev[i][1].record(stream)
+                ev[i][1].record(st)
+        if fork is not None:
+            for st in sts:
+                stream.wait_stream(st)
 
     names = list(libs)
     for w in range(a.warmup):
         for lname in names:
-            step(engines[lname], w * 3600)
+            step(engines[lname], w * 3600, sts=estreams[lname])
     torch.cuda.synchronize()
     kern = {k: [] for k in names}
     wall = {k: [] for k in names}
@@ -130,7 +147,7 @@ def main():
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             for k in range(a.steps):
-                step(engines[lname], k * 3600, ev[k])
+                step(engines[lname], k * 3600, ev[k], sts=estreams[lname])
             torch.cuda.synchronize()
             wall[lname].append((time.perf_counter() - t0) / a.steps * 1e3)
             kern[lname].append([[x.elapsed_time(y) for x, y in row] for row in ev])
