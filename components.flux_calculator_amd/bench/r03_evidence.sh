@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-3 evidence of one build: GPU suite, smoke, the default bench line with the driver's
 # arguments, the T = 2 / fp32 / bias lines, and the two-rank rehearsal of the bench's N > 1
-# path (gloo, both ranks on GPU 0).  Output under gpurun_out/$1.
+# path (gloo, both ranks on GPU 0), and config 2's latency table (bench/latency.py).  Output under gpurun_out/$1.
 set -uo pipefail
 export TMPDIR=/tmp
 O=gpurun_out/${1:-r03_evidence}
@@ -19,4 +19,5 @@ timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 --no-cpu --e2e 0 --bias
 timeout -k 10 300 python3 -m torch.distributed.run --nnodes 1 --nproc-per-node 2 --master-addr 127.0.0.1 \
   --master-port 29533 bench.py --gpus 2 --backend gloo --same-device --steps 10 --warmup 5 --no-cpu --e2e 0 \
   --other-map 0 --config4 0 > $O/bench_rehearsal_2ranks_gloo.json 2> $O/rehearsal.err || exit $?
+timeout -k 10 300 python3 components.flux_calculator_amd/bench/latency.py --steps 1000 > $O/latency_config2.json || exit $?
 exit $rc
