@@ -33,6 +33,8 @@ def main():
     ap.add_argument("--cells", type=int, default=32_768)
     ap.add_argument("--steps", type=int, default=2000)
     ap.add_argument("--bias", type=int, default=1)
+    ap.add_argument("--mode", action="append", default=[],
+                    help="NAME:key=val[,key=val] -- another host-heap mode with these fcx_set_option values (A/B)")
     a = ap.parse_args()
 
     import torch
@@ -145,7 +147,9 @@ def main():
                                    ("host_heap_staged_dma", {"zero_copy": 0}, False),
                                    ("host_heap_runtime_copies", {"host_staging": 0}, False),
                                    ("host_library_arrays", {}, True),
-                                   ("host_library_mirrors", {"zero_copy": 0}, True)):
+                                   ("host_library_mirrors", {"zero_copy": 0}, True),
+                                   *[(m.split(":", 1)[0], {k: int(v) for k, v in (x.split("=") for x in m.split(":", 1)[1].split(","))},
+                                      False) for m in a.mode]):
         hb = {}
         for v in VARIANTS:
             c = build_case(v, n=n, T=1, bias=bool(a.bias), data=host)
