@@ -1824,6 +1824,10 @@ static int copy_bufs(fcx_engine *e, const std::vector<int> &ids, bool h2d, std::
   return h2d ? stage_in(e, xs, e->stream) : stage_out(e, xs, e->stream);
 }
 
+#ifndef FCX_ZC_ONE_CELL  // A/B builds: 0 keeps 16-B (2-cell) lanes in zero-copy launches
+#define FCX_ZC_ONE_CELL 1
+#endif
+
 static int launch_plan(fcx_engine *e, Plan *pl, const double *corr_m, int64_t lo = 0, int64_t hi = -1,
                        bool fixup = true) {
   if (pl->host.n_max <= 0) return FCX_OK;
@@ -1834,6 +1838,12 @@ static int launch_plan(fcx_engine *e, Plan *pl, const double *corr_m, int64_t lo
   // over the host link it buys nothing, and plain stores are the well-trodden path)
   if (e->zc_active) lc.nontemporal = false;
   if (!e->aligned16) lc.cells_per_thread = 1;
+  // host-mapped fields (small grids): loads over the host link want many requests in flight,
+  // so the grid-stride kernel runs one cell per lane (twice the waves: 32,768 cells are 512
+  // waves), unless this launch also feeds the fused accumulation or writes remap records
+  // (both 2 cells per lane).  Kernel 80.5 -> 72.6-75.2 us per CCLM step at 32,768 cells
+  // (profiles/r03/zc_shape_ab/; one-wave workgroups on top changed nothing)
+  if (FCX_ZC_ONE_CELL && e->zc_active && !pl->atm_fused && pl->host.rec == nullptr) lc.cells_per_thread = 1;
   lc.merged = pl->host.merged_uv != 0;
   lc.variant = (e->specialize && lc.merged) ? pl->variant : 0;
   lc.f32 = e->f32;
