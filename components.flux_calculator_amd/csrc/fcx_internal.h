@@ -24,6 +24,14 @@
 #ifndef FCX_DBG_NO_HEAD  // no crossing-record head stores
 #define FCX_DBG_NO_HEAD 0
 #endif
+// Wave timestamps of the fused kernel (measurement builds only: correct results, but an extra
+// kernel argument and a store per wave; fcx_debug_wave_trace, bench/wave_trace.py)
+#if !defined(FCX_AB_BUILD) && defined(FCX_WAVE_TRACE)
+#error "FCX_WAVE_TRACE is a measurement build (FCX_AB_BUILD)"
+#endif
+#ifndef FCX_WAVE_TRACE
+#define FCX_WAVE_TRACE 0
+#endif
 
 namespace fcx {
 
@@ -205,6 +213,9 @@ struct AtmosFused {
   int64_t tpad;        // layout of x (engine buffers); idx, w are contiguous
   int64_t out_tpad;    // layout of out (tiled atmosphere pool, or 0)
   int32_t scol[kFusedFields];  // shared-slot column of fused field k (AtmosArgs::scol)
+#if FCX_WAVE_TRACE
+  uint64_t *trace;     // per wave (dispatch order): {start, end, HW_ID, XCC_ID}, or nullptr
+#endif
 };
 // the segments carried over a tile boundary: carry of tile t-1 + the head cells of tile t,
 // for every tile of a launch of n_cells (fp32: 256-cell tiles of float fields)

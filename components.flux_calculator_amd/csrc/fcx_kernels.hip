@@ -34,6 +34,9 @@ struct Vec {
 };
 
 typedef double d2 __attribute__((ext_vector_type(2)));
+#if FCX_WAVE_TRACE
+typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+#endif
 typedef float f4 __attribute__((ext_vector_type(4)));
 
 // NT: streamed once -> non-temporal hint (the arrays are read once and written once per
@@ -759,6 +762,9 @@ __global__ __launch_bounds__(64 * atmos_waves<C>(), RAVG  ? FCX_RAVG_ATMOS_BLOCK
   const int64_t wave0 = (int64_t)xcd_block(blockIdx.x, gridDim.x) * (blockDim.x >> 6) + wv;
   const uint64_t at_or_above = ~0ull << lane;
   const uint64_t above = lane == 63 ? 0ull : (~0ull << (lane + 1));
+#if FCX_WAVE_TRACE
+  const uint64_t trace_start = (uint64_t)wall_clock64();
+#endif
   for (int64_t tile = lo / kO + wave0; tile < n_tiles; tile += waves) {
     const int64_t t0 = tile * kO;
     const int64_t j0 = t0 + C * lane;
@@ -913,6 +919,19 @@ __global__ __launch_bounds__(64 * atmos_waves<C>(), RAVG  ? FCX_RAVG_ATMOS_BLOCK
     }
     wave_sync();  // every lane is done reading before the next tile overwrites the region
   }
+#if FCX_WAVE_TRACE
+  if (af.trace) {
+    __builtin_amdgcn_s_waitcnt(0);  // the wave's stores have completed
+    const uint64_t trace_end = (uint64_t)wall_clock64();
+    if (lane == 0) {
+      const uint64_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
+      const uint64_t xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
+      u64x2 *t = reinterpret_cast<u64x2 *>(af.trace + ((int64_t)blockIdx.x * (blockDim.x >> 6) + wv) * 4);
+      t[0] = u64x2{trace_start, trace_end};
+      t[1] = u64x2{hw, xcc};
+    }
+  }
+#endif
 }
 
 // Segments that straddle a tile boundary: the launch leaves, in the crossing record of every tile t, the prefix sum of tile t-1's last
@@ -1252,12 +1271,44 @@ static int launch_atm_r(const Params *hp, const LaunchConfig &lc, int blocks, hi
   return 0;
 }
 
+#if FCX_WAVE_TRACE
+// measurement builds: launch k of the fused kernel writes its wave timestamps into slot
+// k % slots of a device buffer of slots x stride words (bench/wave_trace.py)
+static struct {
+  uint64_t *base = nullptr;
+  int64_t stride = 0;
+  int64_t slots = 1;
+  int64_t launches = 0;
+} g_trace;
+}  // namespace fcx
+extern "C" int fcx_debug_wave_trace(uint64_t *base, int64_t stride_words, int64_t slots, int64_t *wall_khz) {
+  fcx::g_trace.base = base;
+  fcx::g_trace.stride = stride_words;
+  fcx::g_trace.slots = slots > 0 ? slots : 1;
+  fcx::g_trace.launches = 0;
+  int rate = 0, dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&rate, hipDeviceAttributeWallClockRate, dev) != hipSuccess)
+    return 1;
+  if (wall_khz) *wall_khz = rate;
+  return 0;
+}
+namespace fcx {
+#endif
+
 int launch_cells(const Params *hp, const Params *dp, const double *corr_m, const LaunchConfig &lc,
                  void *stream, const AtmosFused *atm) {
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int64_t lo = lc.lo, hi = lc.hi < 0 ? hp->n_max : std::min<int64_t>(lc.hi, hp->n_max);
   if (lo % kChunkAlign || lo < 0) return (int)hipErrorInvalidValue;
   if (hi <= lo) return 0;
+#if FCX_WAVE_TRACE
+  AtmosFused traced;
+  if (atm) {
+    traced = *atm;
+    traced.trace = g_trace.base ? g_trace.base + (g_trace.launches++ % g_trace.slots) * g_trace.stride : nullptr;
+    atm = &traced;
+  }
+#endif
   if (atm) {  // fused accumulation: T=1 specialised merged kernel, 2 cells per lane
     // four waves per block (fp32: two), one 128-cell (fp32: 256-cell) tile per wave and trip.  Default: one trip (full
     // grid) -- +2 % per T=1 step over the 8192-block cap, equal at T=2 (profiles/r01/grid_ab)
