@@ -4,14 +4,17 @@
   tools/build_variant.sh ab/trace -DFCX_WAVE_TRACE=1
   FCX_LIBRARY=ab/trace/libfcx.so python wave_trace.py [--precision f32] [--types 2]
 
-Every wave of cells_atmos_kernel stores {start, end, HW_ID, XCC_ID} (the device's constant
-wall clock; `end` after the wave's own stores completed).  The tool runs the bench workload
+Every wave of cells_atmos_kernel stores {start, end, HW_ID | XCC_ID << 32, loop entry} (the
+device's constant wall clock; `end` after the wave's own stores completed; loop entry = the
+first tile's first instruction, after the scalar set-up).  The tool runs the bench workload
 (3 variants, 10M cells, random-run atmosphere map, caller device arrays) back to back and
 reads the last step's three launches.  Per launch it reports the span, the wave lifetimes,
 the occupancy over time (ramp-up until 90 % of the peak count of resident waves, drain after
 the last time at 90 %) and the wave-time lost against a launch that held its peak count
 from the first to the last timestamp; the gaps between consecutive launches; and how much
-waves that share a SIMD start together (lock-step) early and late in the launch.
+waves that share a SIMD start together (lock-step) early and late in the launch; the gap
+between one wave's end and the next wave's start in the same wave slot; and when each XCD
+finished its share of the workgroups.
 """
 import argparse
 import ctypes
@@ -52,7 +55,8 @@ def analyse(tr, khz, bin_us):
     occ = [float(((np.minimum(end, b + bin_us) - np.maximum(start, b)).clip(0)).sum() / bin_us)
            for b in bins[:-1]]
     # SIMD of every wave: HW_ID simd [5:4], cu [11:8], sh [12], se [15:13]; XCC_ID [3:0]
-    hw, xcc = tr[:, 2].astype(np.int64), tr[:, 3].astype(np.int64) & 0xF
+    hw, xcc = tr[:, 2].astype(np.int64) & 0xFFFFFFFF, (tr[:, 2].astype(np.int64) >> 32) & 0xF
+    setup = (tr[:, 3].astype(np.float64) - tr[:, 0]) * us
     simd = (xcc << 16) | (((hw >> 13) & 7) << 8) | (((hw >> 12) & 1) << 7) | (((hw >> 8) & 0xF) << 3) | ((hw >> 4) & 3)
     # lock-step: per wave, other waves of the same SIMD that started within 0.2 us of it
     close = np.zeros(len(start))
@@ -62,6 +66,19 @@ def analyse(tr, khz, bin_us):
         same = (k_sorted[j:] == k_sorted[:-j]) & (s_sorted[j:] - s_sorted[:-j] < 0.2)
         close[order[j:]] += same
         close[order[:-j]] += same
+    # refill gaps: consecutive waves of one wave slot (SIMD + HW_ID wave_id [3:0]); mid-span
+    slot = (simd << 4) | (hw & 0xF)
+    o2 = np.lexsort((start, slot))
+    same_slot = slot[o2][1:] == slot[o2][:-1]
+    gap = (start[o2][1:] - end[o2][:-1])[same_slot]
+    gmid = gap[(start[o2][1:][same_slot] > 0.2 * span) & (start[o2][1:][same_slot] < 0.8 * span)]
+    # XCD balance: every XCD gets 1/8 of the workgroups (round-robin dispatch)
+    xcds = {}
+    for x in np.unique(xcc):
+        m = xcc == x
+        xcds[int(x)] = {"waves": int(m.sum()), "last_end_us": round(float(end[m].max()), 2),
+                        "mean_lifetime_us": round(float(life[m].mean()), 2)}
+    xe = np.array([v["last_end_us"] for v in xcds.values()])
     early = start < 0.1 * span
     late = (start > 0.3 * span) & (start < 0.7 * span)
     return {
@@ -73,11 +90,18 @@ def analyse(tr, khz, bin_us):
                         "p90": round(float(np.percentile(life, 90)), 2),
                         "first_10pct_of_span": round(float(life[early].mean()), 2),
                         "mid_span": round(float(life[late].mean()), 2)},
+        "setup_us_start_to_loop": {"median": round(float(np.median(setup)), 3),
+                                   "p90": round(float(np.percentile(setup, 90)), 3)},
         "ramp_us_to_90pct": round(ramp, 2),
         "drain_us_from_90pct": round(drain, 2),
         "lost_us_vs_peak_occupancy": round(span - wave_us / peak, 2),
         "same_simd_starts_within_0p2us": {"first_10pct_of_span": round(float(close[early].mean()), 2),
                                           "mid_span": round(float(close[late].mean()), 2)},
+        "slot_refill_gap_us_mid_span": {"median": round(float(np.median(gmid)), 3) if len(gmid) else None,
+                                        "p10": round(float(np.percentile(gmid, 10)), 3) if len(gmid) else None,
+                                        "p90": round(float(np.percentile(gmid, 90)), 3) if len(gmid) else None},
+        "xcd_last_end_spread_us": round(float(xe.max() - xe.min()), 2),
+        "xcds": xcds,
         "occupancy_per_bin": [round(x, 1) for x in occ],
         "_t0": int(t0), "_end": int(tr[:, 1].max()),
     }

@@ -723,12 +723,15 @@ __device__ __forceinline__ void segment_done(const AtmosFused &af, int64_t tile,
 #ifndef FCX_F32_ATMOS_BLOCKS
 #define FCX_F32_ATMOS_BLOCKS 4
 #endif
-// waves per block of the fused kernel (the fp32 kernel's as an A/B knob)
+// waves per block of the fused kernel (A/B knobs)
+#ifndef FCX_ATMOS_WAVES
+#define FCX_ATMOS_WAVES 4
+#endif
 #ifndef FCX_F32_ATMOS_WAVES  // A/B: 2 paid while the fp32 rows held fp64 products (13.8 KB/wave)
 #define FCX_F32_ATMOS_WAVES 4
 #endif
 template <int C>
-constexpr int atmos_waves() { return C == 4 ? FCX_F32_ATMOS_WAVES : 4; }
+constexpr int atmos_waves() { return C == 4 ? FCX_F32_ATMOS_WAVES : FCX_ATMOS_WAVES; }
 // HALO (T = 1, full-range launches, maps whose segments are at most halo * C + 1 cells): a
 // wave owns the first 64 - halo lanes' cells of its tile and computes the last `halo` lanes'
 // cells -- the head of the next tile -- only for their products (nothing of them is stored),
@@ -764,8 +767,12 @@ __global__ __launch_bounds__(64 * atmos_waves<C>(), RAVG  ? FCX_RAVG_ATMOS_BLOCK
   const uint64_t above = lane == 63 ? 0ull : (~0ull << (lane + 1));
 #if FCX_WAVE_TRACE
   const uint64_t trace_start = (uint64_t)wall_clock64();
+  uint64_t trace_loop = 0;
 #endif
   for (int64_t tile = lo / kO + wave0; tile < n_tiles; tile += waves) {
+#if FCX_WAVE_TRACE
+    if (!trace_loop) trace_loop = (uint64_t)wall_clock64();
+#endif
     const int64_t t0 = tile * kO;
     const int64_t j0 = t0 + C * lane;
     LdsEmitT<C> emit{wp, {}, lds_slot(C * lane)};
@@ -928,7 +935,7 @@ __global__ __launch_bounds__(64 * atmos_waves<C>(), RAVG  ? FCX_RAVG_ATMOS_BLOCK
       const uint64_t xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
       u64x2 *t = reinterpret_cast<u64x2 *>(af.trace + ((int64_t)blockIdx.x * (blockDim.x >> 6) + wv) * 4);
       t[0] = u64x2{trace_start, trace_end};
-      t[1] = u64x2{hw, xcc};
+      t[1] = u64x2{hw | (xcc << 32), trace_loop};
     }
   }
 #endif
