@@ -38,6 +38,31 @@ typedef double d2 __attribute__((ext_vector_type(2)));
 typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
 #endif
 typedef float f4 __attribute__((ext_vector_type(4)));
+typedef int i2v __attribute__((ext_vector_type(2)));
+typedef int i4v __attribute__((ext_vector_type(4)));
+
+// Field, map and output pointers reach the kernels through the parameter block as generic
+// pointers, which the compiler lowers to FLAT loads and stores.  A FLAT access counts in
+// both vmcnt and lgkmcnt, so every s_waitcnt lgkmcnt(0) that waits for a scalar load (the
+// next array pointer out of the parameter block) also waits for all of the wave's loads in
+// flight.  These are device (or host-mapped) arrays, never LDS or scratch: addressing them
+// in the global address space gives GLOBAL instructions, counted in vmcnt alone.
+#ifndef FCX_GLOBAL_AS  // A/B builds: 0 = generic pointers (FLAT instructions)
+#define FCX_GLOBAL_AS 1
+#endif
+#if FCX_GLOBAL_AS
+#define FCX_GLOBAL __attribute__((address_space(1)))
+#else
+#define FCX_GLOBAL
+#endif
+template <class T>
+__device__ __forceinline__ const FCX_GLOBAL T *gptr(const T *p) {
+  return (const FCX_GLOBAL T *)p;
+}
+template <class T>
+__device__ __forceinline__ FCX_GLOBAL T *gptr(T *p) {
+  return (FCX_GLOBAL T *)p;
+}
 
 // NT: streamed once -> non-temporal hint (the arrays are read once and written once per
 // step; the 256 MB Infinity Cache cannot hold a 10M-cell step anyway).  Out-of-range lanes
@@ -48,7 +73,7 @@ __device__ __forceinline__ Vec<C, R> ld(const R *__restrict__ p, int64_t j0, int
   if constexpr (C * sizeof(R) == 16) {
     if (j0 + C <= n) {
       using V = typename std::conditional<sizeof(R) == 8, d2, f4>::type;
-      const V *q = reinterpret_cast<const V *>(p + j0);
+      const FCX_GLOBAL V *q = gptr(reinterpret_cast<const V *>(p + j0));
       const V t = NT ? __builtin_nontemporal_load(q) : *q;
 #pragma unroll
       for (int i = 0; i < C; ++i) r.v[i] = t[i];
@@ -56,7 +81,7 @@ __device__ __forceinline__ Vec<C, R> ld(const R *__restrict__ p, int64_t j0, int
     }
   }
 #pragma unroll
-  for (int i = 0; i < C; ++i) r.v[i] = (j0 + i < n) ? p[j0 + i] : R(1);
+  for (int i = 0; i < C; ++i) r.v[i] = (j0 + i < n) ? gptr(p)[j0 + i] : R(1);
   return r;
 }
 
@@ -65,7 +90,7 @@ __device__ __forceinline__ void st(R *__restrict__ p, int64_t j0, int64_t n, con
   if constexpr (C * sizeof(R) == 16) {
     if (j0 + C <= n) {
       using V = typename std::conditional<sizeof(R) == 8, d2, f4>::type;
-      V *q = reinterpret_cast<V *>(p + j0);
+      FCX_GLOBAL V *q = gptr(reinterpret_cast<V *>(p + j0));
       V t;
 #pragma unroll
       for (int i = 0; i < C; ++i) t[i] = x.v[i];
@@ -78,7 +103,7 @@ __device__ __forceinline__ void st(R *__restrict__ p, int64_t j0, int64_t n, con
   }
 #pragma unroll
   for (int i = 0; i < C; ++i)
-    if (j0 + i < n) p[j0 + i] = x.v[i];
+    if (j0 + i < n) gptr(p)[j0 + i] = x.v[i];
 }
 
 template <int C, class R>
@@ -256,7 +281,7 @@ struct RecEmit {
     if (p >= 0) {
 #pragma unroll
       for (int i = 0; i < CC; ++i)
-        if (i < nv) rec[i * P + p] = x.v[i];
+        if (i < nv) gptr(rec)[i * P + p] = x.v[i];
     }
   }
   __device__ __forceinline__ void flush() const {
@@ -278,7 +303,7 @@ struct RecEmit {
             if (pos[k] == q * V + h) v = vals[k][i];
           t[h] = v;
         }
-        *reinterpret_cast<VecT *>(rec + i * P + q * V) = t;
+        *gptr(reinterpret_cast<VecT *>(rec + i * P + q * V)) = t;
       }
     }
   }
@@ -680,7 +705,7 @@ __device__ __forceinline__ void segment_done(const AtmosFused &af, int64_t tile,
   if (cont) {  // the next tile's crossing record: the six prefix sums, 16-B stores
 #pragma unroll
     for (int q = 0; q < kFusedFields / 2; ++q)
-      reinterpret_cast<d2 *>(af.xrec + (tile + 1) * kXRec)[q] = d2{acc[2 * q], acc[2 * q + 1]};
+      gptr(reinterpret_cast<d2 *>(af.xrec + (tile + 1) * kXRec))[q] = d2{acc[2 * q], acc[2 * q + 1]};
     return;
   }
   if (FCX_DBG_ATM_NOSTORE) return;
@@ -696,13 +721,13 @@ __device__ __forceinline__ void segment_done(const AtmosFused &af, int64_t tile,
 #pragma unroll
   for (int k = 0; k < kFusedFields; ++k) {
     if (!af.out[k]) continue;
-    R *o = reinterpret_cast<R *>(af.out[k]) + tiled(a, af.out_tpad);
+    FCX_GLOBAL R *o = gptr(reinterpret_cast<R *>(af.out[k]) + tiled(a, af.out_tpad));
     if (FCX_ATM_NT_STORE == 1 || (FCX_ATM_NT_STORE == 2 && nt_line) || (FCX_ATM_NT_STORE == 3 && sizeof(R) == 8))
       __builtin_nontemporal_store((R)acc[k], o);
     else
       *o = (R)acc[k];
-    if (a == 0 && af.left >= 0) af.shared[(int64_t)af.left * af.stride + af.scol[k]] = acc[k];
-    if (a == af.n_atmos - 1 && af.right >= 0) af.shared[(int64_t)af.right * af.stride + af.scol[k]] = acc[k];
+    if (a == 0 && af.left >= 0) gptr(af.shared)[(int64_t)af.left * af.stride + af.scol[k]] = acc[k];
+    if (a == af.n_atmos - 1 && af.right >= 0) gptr(af.shared)[(int64_t)af.right * af.stride + af.scol[k]] = acc[k];
   }
 }
 
@@ -781,11 +806,11 @@ __global__ __launch_bounds__(64 * atmos_waves<C>(), RAVG  ? FCX_RAVG_ATMOS_BLOCK
     for (int i = 0; i < C; ++i) a[i] = -1;
     if (j0 + C <= n) {
       if constexpr (C == 2) {
-        const int2 ii = *reinterpret_cast<const int2 *>(af.idx + j0);
+        const i2v ii = *gptr(reinterpret_cast<const i2v *>(af.idx + j0));
         a[0] = ii.x;
         a[1] = ii.y;
       } else {
-        const int4 ii = *reinterpret_cast<const int4 *>(af.idx + j0);
+        const i4v ii = *gptr(reinterpret_cast<const i4v *>(af.idx + j0));
         a[0] = ii.x;
         a[1] = ii.y;
         a[2] = ii.z;
@@ -793,7 +818,7 @@ __global__ __launch_bounds__(64 * atmos_waves<C>(), RAVG  ? FCX_RAVG_ATMOS_BLOCK
       }
 #pragma unroll
       for (int h = 0; h < C / 2; ++h) {
-        const d2 ww = __builtin_nontemporal_load(reinterpret_cast<const d2 *>(af.w + j0) + h);
+        const d2 ww = __builtin_nontemporal_load(gptr(reinterpret_cast<const d2 *>(af.w + j0) + h));
         emit.w[2 * h] = ww[0];
         emit.w[2 * h + 1] = ww[1];
       }
@@ -801,13 +826,13 @@ __global__ __launch_bounds__(64 * atmos_waves<C>(), RAVG  ? FCX_RAVG_ATMOS_BLOCK
 #pragma unroll
       for (int i = 0; i < C; ++i)
         if (j0 + i < n) {
-          a[i] = af.idx[j0 + i];
-          emit.w[i] = af.w[j0 + i];
+          a[i] = gptr(af.idx)[j0 + i];
+          emit.w[i] = gptr(af.w)[j0 + i];
         }
     }
-    const int32_t prev_tile = t0 > 0 ? af.idx[t0 - 1] : -2;  // wave-uniform loads
+    const int32_t prev_tile = t0 > 0 ? gptr(af.idx)[t0 - 1] : -2;  // wave-uniform loads
     const int64_t tend = t0 + kT;
-    const int32_t next_a = (tend < n) ? af.idx[tend] : -3;
+    const int32_t next_a = (tend < n) ? gptr(af.idx)[tend] : -3;
     if (j0 < n)
       process<C, true, VAR, NT, R, TM, RAVG, LdsEmitT<C>, REC, HALO>(
           P, corr_m, j0, emit, AccLds<C, R>{reinterpret_cast<R *>(wp + emit.s), kR}, t0 + kO);
@@ -905,7 +930,7 @@ __global__ __launch_bounds__(64 * atmos_waves<C>(), RAVG  ? FCX_RAVG_ATMOS_BLOCK
       for (int q = 0; q < C; ++q) head = min(head, C * first_bit(m[q]) + q);
       if (FCX_DBG_NO_HEAD >= 2) head = 0;
       double *xr0 = af.xrec + tile * kXRec;
-      if (lane == 0 && FCX_DBG_NO_HEAD < 2) *reinterpret_cast<int2 *>(xr0 + 30) = int2{head, a[0]};
+      if (lane == 0 && FCX_DBG_NO_HEAD < 2) *gptr(reinterpret_cast<i2v *>(xr0 + 30)) = i2v{head, a[0]};
       if (FCX_DBG_NO_HEAD) head = 0;
       // the products of the first kRecHead head cells, one lane per cell, 16-B stores
       if (lane < min(head, kRecHead)) {
@@ -921,7 +946,7 @@ __global__ __launch_bounds__(64 * atmos_waves<C>(), RAVG  ? FCX_RAVG_ATMOS_BLOCK
         }
 #pragma unroll
         for (int q = 0; q < kFusedFields / 2; ++q)
-          reinterpret_cast<d2 *>(xr0 + kFusedFields + lane * kFusedFields)[q] = d2{hp[2 * q], hp[2 * q + 1]};
+          gptr(reinterpret_cast<d2 *>(xr0 + kFusedFields + lane * kFusedFields))[q] = d2{hp[2 * q], hp[2 * q + 1]};
       }
     }
     wave_sync();  // every lane is done reading before the next tile overwrites the region
