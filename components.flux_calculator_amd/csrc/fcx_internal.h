@@ -213,6 +213,8 @@ struct AtmosFused {
   int64_t tpad;        // layout of x (engine buffers); idx, w are contiguous
   int64_t out_tpad;    // layout of out (tiled atmosphere pool, or 0)
   int32_t scol[kFusedFields];  // shared-slot column of fused field k (AtmosArgs::scol)
+  int64_t n_tiles;     // tiles [lo / tile cells, n_tiles) of one launch (set per launch, so no
+                       // wave divides by the halo-dependent tile size)
 #if FCX_WAVE_TRACE
   uint64_t *trace;     // per wave (dispatch order): {start, end, HW_ID, XCC_ID}, or nullptr
 #endif

@@ -783,7 +783,7 @@ __global__ __launch_bounds__(64 * atmos_waves<C>(), RAVG  ? FCX_RAVG_ATMOS_BLOCK
   const int64_t n = P->n_max;
   const int own_lanes = HALO ? 64 - af.halo : 64;
   const int64_t kO = (int64_t)C * own_lanes;  // cells a tile owns (HALO: lo == 0)
-  const int64_t n_tiles = (hi + kO - 1) / kO;  // tiles [lo/kT, n_tiles) of this launch
+  const int64_t n_tiles = af.n_tiles;  // (hi + kO - 1) / kO, from the host
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   double *wp = s_p[wv];
   const int64_t waves = (int64_t)gridDim.x * (blockDim.x >> 6);
@@ -1333,14 +1333,16 @@ int launch_cells(const Params *hp, const Params *dp, const double *corr_m, const
   const int64_t lo = lc.lo, hi = lc.hi < 0 ? hp->n_max : std::min<int64_t>(lc.hi, hp->n_max);
   if (lo % kChunkAlign || lo < 0) return (int)hipErrorInvalidValue;
   if (hi <= lo) return 0;
-#if FCX_WAVE_TRACE
-  AtmosFused traced;
+  AtmosFused afl;  // this launch's copy: its tile count (and, in trace builds, its trace slot)
   if (atm) {
-    traced = *atm;
-    traced.trace = g_trace.base ? g_trace.base + (g_trace.launches++ % g_trace.slots) * g_trace.stride : nullptr;
-    atm = &traced;
-  }
+    afl = *atm;
+    const int64_t own = (lc.f32 ? 4 : 2) * (64 - lc.halo);
+    afl.n_tiles = (hi + own - 1) / own;
+#if FCX_WAVE_TRACE
+    afl.trace = g_trace.base ? g_trace.base + (g_trace.launches++ % g_trace.slots) * g_trace.stride : nullptr;
 #endif
+    atm = &afl;
+  }
   if (atm) {  // fused accumulation: T=1 specialised merged kernel, 2 cells per lane
     // four waves per block (fp32: two), one 128-cell (fp32: 256-cell) tile per wave and trip.  Default: one trip (full
     // grid) -- +2 % per T=1 step over the 8192-block cap, equal at T=2 (profiles/r01/grid_ab)
