@@ -682,15 +682,33 @@ __device__ __forceinline__ int first_bit(uint64_t m) { return m ? __builtin_ctzl
 // XCD-aware block order.  Workgroups are dispatched round-robin over the 8 XCDs (block b on
 // XCD b % 8), each XCD with its own L2.  Neighbouring tiles share the 128-B lines of the
 // atmosphere outputs their segments end in; mapped to the same XCD, the two partial lines
-// merge in that L2 before write-back instead of reaching memory as two partial writes.  So
-// XCD x takes one contiguous run of the blocks: b -> x * (nb / 8) + min(x, nb % 8) + b / 8.
+// merge in that L2 before write-back instead of reaching memory as two partial writes.
+// FCX_XCD_MAP 2 (default since round 3): XCD x takes runs of FCX_XCD_CHUNK = 64 consecutive
+// workgroups (256 tiles), the 8 XCDs' runs side by side, so that only one tile edge in 256
+// is shared between two XCDs AND the chip streams from one window of the arrays, as the
+// dispatch order advances.  1 (round 1-2): one contiguous eighth of the grid per XCD,
+// b -> x * (nb / 8) + min(x, nb % 8) + b / 8: eight windows 1/8 of the arrays apart.  In one
+// process over the same arrays, 2 against 1 (profiles/r03/xcd_map_ab/): step -2.4 / -6.1 %
+// fp64 (two boxes), -2.7 / -2.2 % fp32, -3.1 / -0.8 % at T = 2, -5.4 % on the periodic map.
+// 0 (A/B): plain dispatch order.
 #ifndef FCX_XCD_MAP
-#define FCX_XCD_MAP 1
+#define FCX_XCD_MAP 2
 #endif
 constexpr uint32_t kXcds = 8;
+#ifndef FCX_XCD_CHUNK  // FCX_XCD_MAP 2: workgroups per XCD run
+#define FCX_XCD_CHUNK 64
+#endif
 __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb) {
   if (!FCX_XCD_MAP) return b;
-  const uint32_t x = b % kXcds, q = nb / kXcds, r = nb % kXcds;
+  const uint32_t x = b % kXcds;
+  if (FCX_XCD_MAP == 2) {  // runs of FCX_XCD_CHUNK workgroups per XCD, the XCDs side by side
+    constexpr uint32_t K = FCX_XCD_CHUNK, row = K * kXcds;
+    const uint32_t full = nb / row * row;
+    if (b >= full) return b;
+    const uint32_t i = b / kXcds;
+    return i / K * row + x * K + i % K;
+  }
+  const uint32_t q = nb / kXcds, r = nb % kXcds;
   return x * q + min(x, r) + b / kXcds;
 }
 
