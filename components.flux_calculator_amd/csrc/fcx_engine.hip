@@ -1865,7 +1865,7 @@ static int launch_plan(fcx_engine *e, Plan *pl, const double *corr_m, int64_t lo
     const int cpl = e->f32 ? 4 : 2;
     const int h = (e->atm_maxseg - 1 + cpl - 1) / cpl;
     if (e->atm_halo && e->atm_crossings > 0 && lo == 0 && (hi < 0 || hi >= pl->host.n_max) &&
-        pl->host.num_types == 1 && h >= 1 && h <= (e->f32 ? 2 : 4))
+        (pl->host.num_types == 1 || (FCX_HALO_RAVG && pl->host.ravg_on)) && h >= 1 && h <= (e->f32 ? 2 : 4))
       lc.halo = h;
     pl->af.halo = lc.halo;
   }

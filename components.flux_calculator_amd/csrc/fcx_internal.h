@@ -32,6 +32,10 @@
 #ifndef FCX_WAVE_TRACE
 #define FCX_WAVE_TRACE 0
 #endif
+// halo tiles also for the multi-type kernel with register averages (A/B)
+#ifndef FCX_HALO_RAVG
+#define FCX_HALO_RAVG 0
+#endif
 
 namespace fcx {
 

@@ -327,7 +327,7 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
                                         AccLds<C, R> acc_lds = AccLds<C, R>{nullptr, 0}, int64_t st_end = 0) {
   static_assert(!(RAVG && TM), "register averages need more than one surface type");
   static_assert(!REC || (TM == 1 && !RAVG), "remap records: the T=1 launch");
-  static_assert(!HALO || (TM == 1 && !RAVG), "halo tiles: the T=1 launch");
+  static_assert(!HALO || (TM == 1 && !RAVG) || (FCX_HALO_RAVG && RAVG), "halo tiles: the T=1 launch");
   const uint32_t stages = P->stages;
   const int T = TM ? 1 : P->num_types;
   const int64_t nt = P->n[0];
@@ -797,7 +797,7 @@ __global__ __launch_bounds__(64 * atmos_waves<C>(), RAVG  ? FCX_RAVG_ATMOS_BLOCK
   constexpr bool kXF = sizeof(R) == 4;  // LDS holds fp32 fluxes + fp64 weights
   static_assert(!kXF || C == 4, "fp32 flux rows: 4 cells per lane");
   __shared__ double s_p[atmos_waves<C>()][wave_lds_doubles<R, C>(kRows)];
-  static_assert(!HALO || (TM == 1 && !RAVG), "halo tiles: the T=1 launch");
+  static_assert(!HALO || (TM == 1 && !RAVG) || (FCX_HALO_RAVG && RAVG), "halo tiles: the T=1 launch");
   const int64_t n = P->n_max;
   const int own_lanes = HALO ? 64 - af.halo : 64;
   const int64_t kO = (int64_t)C * own_lanes;  // cells a tile owns (HALO: lo == 0)
@@ -1295,7 +1295,7 @@ template <int VAR>
 static int launch_atm_r(const Params *hp, const LaunchConfig &lc, int blocks, hipStream_t s, const Params *dp,
                         const double *corr_m, const AtmosFused &af, int64_t lo, int64_t hi) {
   const bool halo = lc.halo > 0;
-  if (halo && (hp->num_types != 1 || lo != 0)) return (int)hipErrorInvalidValue;
+  if (halo && ((hp->num_types != 1 && !(FCX_HALO_RAVG && lc.ravg)) || lo != 0)) return (int)hipErrorInvalidValue;
   if (hp->num_types == 1 && lc.f32) {  // fp32 engine: 4 cells per lane, T = 1 only
     if (halo)
       launch_atm<4, float, VAR, 1, false, false, true>(lc.nontemporal, blocks, s, dp, corr_m, af, lo, hi);
@@ -1314,9 +1314,15 @@ static int launch_atm_r(const Params *hp, const LaunchConfig &lc, int blocks, hi
     else
       launch_atm<2, double, VAR, 1, false>(lc.nontemporal, blocks, s, dp, corr_m, af, lo, hi);
   }
-  else if (lc.ravg)
+  else if (lc.ravg) {
+    if constexpr (FCX_HALO_RAVG) {
+      if (halo) {
+        launch_atm<2, double, VAR, 0, true, false, true>(lc.nontemporal, blocks, s, dp, corr_m, af, lo, hi);
+        return 0;
+      }
+    }
     launch_atm<2, double, VAR, 0, true>(lc.nontemporal, blocks, s, dp, corr_m, af, lo, hi);
-  else
+  } else
     return (int)hipErrorInvalidValue;
   return 0;
 }

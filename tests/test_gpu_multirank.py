@@ -119,6 +119,41 @@ def test_fused_accumulation_long_segments(lengths, mode):
     eng.close()
 
 
+@pytest.mark.parametrize("lengths", [(1, 5), (1, 9), (1, 10), (20, 64)])
+@pytest.mark.parametrize("mode", ["default", "nohalo", "pipelined"])
+def test_fused_accumulation_of_averages_long_segments(lengths, mode):
+    """Two surface types: the type-0 averages accumulated by the multi-type fused kernel on
+    maps whose segments cross its 128-cell wave tiles (1..5 and 1..9 cells: halo tiles where
+    the kernel takes them, 1..10 and 20..64: crossing records + fix-up), with the crossing
+    records forced (FCX_OPT_ATMOS_HALO 0), and across the pipelined step's chunk launches.
+    Bit-identical to the sequential sum of the GPU's own averages."""
+    import torch
+    from fcx.engine import Engine
+    from fcx.parallel import local_atmos
+
+    n = 300_001 if mode == "pipelined" else 70_001
+    case = build_case("CCLM", n=n, T=2, bias=True, seed=23)
+    amap = random_run_map(n, lengths, seed=lengths[1] + 11)
+    la = local_atmos(amap, 0, 1)
+    outs = {name: torch.full((la.n_atmos,), float("nan"), dtype=torch.float64, device="cuda:0")
+            for name, _ in FIELDS}
+    atmos = {"local": la, "fields": [(2, 0, g, name, outs[name]) for name, g in FIELDS]}
+    opts = {"default": {}, "nohalo": {"atmos_halo": 0},
+            "pipelined": {"pipeline_chunks": 4, "pipeline_min_chunk": 65536, "zero_copy": 0}}[mode]
+    eng = Engine(case.lf, 2, case.methods, corrections=case.corrections, averages=case.averages, atmos=atmos,
+                 options=opts)
+    for step in range(2):
+        for o in outs.values():
+            o.fill_(float("nan"))
+        eng.step(PHASE_ALL, 3600 * step)
+        torch.cuda.synchronize()
+        for name, g in FIELDS:
+            avg = np.asarray(case.lf.field[(0, g, name)])
+            want = oracle_lib.atmos_accumulate(amap.atmos_index, amap.weight, avg, amap.n_atmos)
+            np.testing.assert_array_equal(outs[name].cpu().numpy(), want, err_msg=f"{name} step {step}")
+    eng.close()
+
+
 @pytest.mark.parametrize("fused", [True, False])
 @pytest.mark.parametrize("variant", ["CCLM", "MOM5", "RCO"])
 def test_atmos_accumulation_bit_exact_single_rank(variant, fused):
