@@ -695,14 +695,18 @@ __device__ __forceinline__ int first_bit(uint64_t m) { return m ? __builtin_ctzl
 #define FCX_XCD_MAP 2
 #endif
 constexpr uint32_t kXcds = 8;
-#ifndef FCX_XCD_CHUNK  // FCX_XCD_MAP 2: workgroups per XCD run
+#ifndef FCX_XCD_CHUNK  // FCX_XCD_MAP 2: workgroups per XCD run (fp64 kernels, 128-cell tiles)
 #define FCX_XCD_CHUNK 64
 #endif
+#ifndef FCX_XCD_CHUNK_F32  // ... and of the fp32 kernels (256-cell tiles): 16 against 64,
+#define FCX_XCD_CHUNK_F32 16  // step -0.7 % (shared arrays) / -4.0 % (own mirrors),
+#endif                        // profiles/r03/xcd_map_ab/f32_*
+template <uint32_t K>
 __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb) {
   if (!FCX_XCD_MAP) return b;
   const uint32_t x = b % kXcds;
-  if (FCX_XCD_MAP == 2) {  // runs of FCX_XCD_CHUNK workgroups per XCD, the XCDs side by side
-    constexpr uint32_t K = FCX_XCD_CHUNK, row = K * kXcds;
+  if (FCX_XCD_MAP == 2) {  // runs of K workgroups per XCD, the XCDs side by side
+    constexpr uint32_t row = K * kXcds;
     const uint32_t full = nb / row * row;
     if (b >= full) return b;
     const uint32_t i = b / kXcds;
@@ -805,7 +809,8 @@ __global__ __launch_bounds__(64 * atmos_waves<C>(), RAVG  ? FCX_RAVG_ATMOS_BLOCK
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   double *wp = s_p[wv];
   const int64_t waves = (int64_t)gridDim.x * (blockDim.x >> 6);
-  const int64_t wave0 = (int64_t)xcd_block(blockIdx.x, gridDim.x) * (blockDim.x >> 6) + wv;
+  const int64_t wave0 =
+      (int64_t)xcd_block<C == 4 ? FCX_XCD_CHUNK_F32 : FCX_XCD_CHUNK>(blockIdx.x, gridDim.x) * (blockDim.x >> 6) + wv;
   const uint64_t at_or_above = ~0ull << lane;
   const uint64_t above = lane == 63 ? 0ull : (~0ull << (lane + 1));
 #if FCX_WAVE_TRACE
