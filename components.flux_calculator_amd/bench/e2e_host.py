@@ -65,6 +65,8 @@ SWEEP = [("heap, runtime copies, sequential", {"host_staging": 0, "pipeline_chun
          ("heap, staged, 8 chunks", {"pipeline_chunks": 8}),   # the default transport
          ("heap, staged, 16 chunks", {"pipeline_chunks": 16}),
          ("heap, staged, 32 chunks", {"pipeline_chunks": 32}),
+         ("heap, arena in place, 8 chunks", {"zero_copy": 1, "pipeline_chunks": 8}),
+         ("heap, arena in place, 16 chunks", {"zero_copy": 1, "pipeline_chunks": 16}),
          ("zero-copy", {"zero_copy": 1}),                       # arrays from fcx_host_malloc
          ("library arrays, 8 chunks", {"zero_copy": 0, "pipeline_chunks": 8})]
 LIBRARY_ARRAYS = ("zero-copy", "library arrays, 8 chunks")
