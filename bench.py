@@ -9,10 +9,12 @@ second over the whole job, one variant over N cells counting N cells.
 
 Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): one rank
 per GPU, each owns a contiguous APPLE cell range of its own 10M cells (decomp_def.F90:23-31,
-weak scaling); the flux path has no cross-rank exchange.
+weak scaling); the one cross-rank exchange is the all-reduce of the atmosphere cells shared
+by neighbouring ranks (libfcx's RCCL communicator), once per step.
 
 Also reported:
-  roofline      algorithmic bytes of the dominant kernel / its mean HIP-event duration
+  roofline      algorithmic bytes of the dominant kernel / its mean HIP-event duration in
+                the timed steps (one event pair per step, around that kernel only)
   cpu_baseline  the CPU oracle on a bounded sample of the same workload (rank 0, N=1 only):
                 "reference" = the reference flux_lib compiled from source (oracle/_ref),
                 "port" = the C restatement (oracle/fco.c)
@@ -86,6 +88,9 @@ def parse():
     p.add_argument("--precision", choices=("f64", "f32"), default="f64",
                    help="f32: the fp32 variant (config 5): fp32 cell pass with the accumulation fused in "
                         "(fp32 fluxes, fp64 weights, products and sums, fp32 outputs)")
+    p.add_argument("--kernel-events", choices=("dominant", "all"), default="dominant",
+                   help="HIP event pairs inside the timed steps: around the dominant engine's launch only "
+                        "(picked in an event-timed warm-up block), or around every engine's")
     return p.parse_args()
 
 
@@ -316,10 +321,19 @@ def measure(wl, args, world, dist, comm, steps, warmup, t_base=0, cold=False):
         if comm is not None:
             comm.atmos_allreduce(wl.engines)  # the one collective of the step (RCCL over xGMI)
 
+    def pairs(k):
+        return [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                 for _ in wl.engines] for _ in range(k)]
+
+    nv = len(wl.engines)
+    # event-timed warm-up block: every engine's launch, to pick the dominant one (and report
+    # the others); the timed steps then carry ONE event pair, around the dominant launch --
+    # each pair in the step costs ~2.5 % of it (bench/event_probe.py)
+    probe_steps = max(WARMUP_BLOCK, min(steps, 200))
+    ev_probe = pairs(probe_steps)
     # the timed steps' events exist before the warm-up starts: nothing host-side sits between
     # the warm-up and the timed region (an idle GPU drops its clocks)
-    ev = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in wl.engines] for _ in range(steps)]
+    ev = pairs(steps)
     step(t_base)  # builds the engines' plans
     torch.cuda.synchronize()
     cold_ms = None
@@ -343,6 +357,17 @@ def measure(wl, args, world, dist, comm, steps, warmup, t_base=0, cold=False):
         torch.cuda.synchronize()
         if warm >= warmup and time.perf_counter() - t_w >= MIN_WARMUP_S:
             break
+    for k in range(probe_steps):  # still warm-up: the event-timed block
+        step(t_base + (warm + k) * 3600, ev_probe[k])
+    torch.cuda.synchronize()
+    probe_ms = np.array([[a.elapsed_time(b) for (a, b) in row] for row in ev_probe])  # [steps][variant]
+    dom = int(np.argmax(probe_ms.mean(axis=0)))
+    if args.kernel_events == "dominant":
+        ev = [[p if i == dom else None for i, p in enumerate(row)] for row in ev]
+    for k in range(WARMUP_BLOCK):  # back under load after the host read the probe events
+        step(t_base + (warm + probe_steps + k) * 3600)
+    torch.cuda.synchronize()
+    warm += probe_steps + WARMUP_BLOCK
     warmup_s = time.perf_counter() - t_w
     if world > 1:
         dist.barrier()
@@ -354,14 +379,21 @@ def measure(wl, args, world, dist, comm, steps, warmup, t_base=0, cold=False):
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kern_ms = np.array([[a.elapsed_time(b) for (a, b) in row] for row in ev])  # [steps][variant]
+    # per-variant mean kernel time: the timed steps where they carry events (the dominant
+    # engine; every engine with --kernel-events all), the event-timed warm-up block otherwise
+    kern_mean = probe_ms.mean(axis=0)
+    timed = {i: np.array([row[i][0].elapsed_time(row[i][1]) for row in ev])
+             for i in range(nv) if ev[0][i] is not None}
+    for i, x in timed.items():
+        kern_mean[i] = x.mean()
     t_max = elapsed
     if world > 1:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=wl.dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         t_max = float(tt.item())
     del stream
-    return {"t_max": t_max, "kern_ms": kern_ms, "cold_ms": cold_ms, "warm": warm, "warmup_s": warmup_s}
+    return {"t_max": t_max, "kern_mean": kern_mean, "dom": dom, "timed_events": sorted(timed),
+            "cold_ms": cold_ms, "warm": warm, "warmup_s": warmup_s}
 
 
 def main():
@@ -426,13 +458,13 @@ def main():
     # bias month slice changes inside the timed region (init_date 19610101)
     t_base = 31 * 86400 - 3600 * (args.steps // 2) if args.bias else 0
     m = measure(wl, args, world, dist, coll, args.steps, args.warmup, t_base, cold=True)
-    t_max, kern_ms = m["t_max"], m["kern_ms"]
+    t_max = m["t_max"]
     ms_per_step = t_max / args.steps * 1e3
     cells_per_step = n_global * len(variants)
     value = cells_per_step * args.steps / t_max / 1e6
 
-    mean_ms = kern_ms.mean(axis=0)
-    dom = int(np.argmax(mean_ms))
+    mean_ms = m["kern_mean"]
+    dom = m["dom"]
     achieved = alg_bytes[dom] / (mean_ms[dom] * 1e-3) / 1e9
     per_variant = {
         v: {"kernel_ms": round(float(mean_ms[i]), 4),
@@ -467,7 +499,8 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 4),
         "warmup_run": {"steps": m["warm"], "seconds": round(m["warmup_s"], 3),
-                       "rule": f"at least --warmup steps and at least {MIN_WARMUP_S} s of device work"},
+                       "rule": f"at least --warmup steps and at least {MIN_WARMUP_S} s of device work, then an "
+                               "event-timed block (every engine) and one more block without events"},
         "timed_ms": round(t_max * 1e3, 3),
         "cold_step_ms": round(m["cold_ms"], 4),
         "higher_is_better": True,
@@ -512,8 +545,14 @@ def main():
             "traffic_source": traffic_source,
             "alg_bytes_per_launch": int(alg_bytes[dom]),
             "mean_kernel_ms": round(float(mean_ms[dom]), 4),
+            "events": ("one HIP event pair per timed step, around the dominant engine's launch on its stream "
+                       "(picked in an event-timed warm-up block of every engine)" if args.kernel_events == "dominant"
+                       else "HIP event pairs around every engine's launch in every timed step"),
         },
         "kernels": per_variant,
+        "kernels_rule": ("kernel_ms from the timed steps' events for " + ", ".join(variants[i] for i in m["timed_events"])
+                         + ("; from the event-timed warm-up block for the others" if len(m["timed_events"]) < len(variants)
+                            else "")),
     }
     if mg is not None:
         out["multi_gpu_check"] = mg
@@ -529,8 +568,8 @@ def main():
                       stream=torch.cuda.current_stream(dev), engine_options=engine_options)
         wl = wo
         mo = measure(wo, args, world, dist, coll if comm is None else comm, args.steps, args.warmup)
-        ko = mo["kern_ms"].mean(axis=0)
-        do = int(np.argmax(ko))
+        ko = mo["kern_mean"]
+        do = mo["dom"]
         out["other_map"] = {
             "atmos_map": other,
             "value": round(n_global * len(variants) * args.steps / mo["t_max"] / 1e6, 1),
@@ -550,8 +589,8 @@ def main():
                       engine_options=engine_options, atmos_map=args.atmos_map)
         wl = w4
         m4 = measure(w4, args, world, dist, coll if comm is None else comm, args.steps, args.warmup)
-        k4 = m4["kern_ms"].mean(axis=0)
-        d4 = int(np.argmax(k4))
+        k4 = m4["kern_mean"]
+        d4 = m4["dom"]
         out["config4"] = {
             "workload": "config 4: fixed synthetic grid sharded by APPLE ranges over the ranks (strong scaling), "
                         "CCLM+MOM5+RCO fused kernels + accumulation, one all-reduce of the boundary slots per step, "

@@ -102,13 +102,14 @@ class Workload:
 
     def run(self, t, events=None):
         """One coupling step of every variant (no collective); events[i] = (start, end)
-        recorded around engine i's launch."""
+        recorded around engine i's launch (None: no events around that engine)."""
         for i, e in enumerate(self.engines):
-            if events is not None:
-                events[i][0].record(self.stream)
+            ev = events[i] if events is not None else None
+            if ev is not None:
+                ev[0].record(self.stream)
             e.run(PHASE_ALL, t)
-            if events is not None:
-                events[i][1].record(self.stream)
+            if ev is not None:
+                ev[1].record(self.stream)
             if self.la is not None:
                 e.run_atmos(PHASE_ALL)
 
