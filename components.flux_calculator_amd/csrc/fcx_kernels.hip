@@ -94,6 +94,8 @@ __device__ __forceinline__ void st(R *__restrict__ p, int64_t j0, int64_t n, con
       V t;
 #pragma unroll
       for (int i = 0; i < C; ++i) t[i] = x.v[i];
+      // (write-through sc1 / sc1 nt stores instead of nt: step +9 to +27 %,
+      // profiles/r03/store_wt_ab/ -- the L2 write-back merges the output lines)
       if (NT)
         __builtin_nontemporal_store(t, q);
       else
