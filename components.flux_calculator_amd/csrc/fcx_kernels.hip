@@ -47,14 +47,8 @@ typedef int i4v __attribute__((ext_vector_type(4)));
 // next array pointer out of the parameter block) also waits for all of the wave's loads in
 // flight.  These are device (or host-mapped) arrays, never LDS or scratch: addressing them
 // in the global address space gives GLOBAL instructions, counted in vmcnt alone.
-#ifndef FCX_GLOBAL_AS  // A/B builds: 0 = generic pointers (FLAT instructions)
-#define FCX_GLOBAL_AS 1
-#endif
-#if FCX_GLOBAL_AS
+// (Round 3: step -0.4 % fp64, -0.7 % fp32, -1.0 % at T = 2 against FLAT, profiles/r03/global_as_ab/.)
 #define FCX_GLOBAL __attribute__((address_space(1)))
-#else
-#define FCX_GLOBAL
-#endif
 template <class T>
 __device__ __forceinline__ const FCX_GLOBAL T *gptr(const T *p) {
   return (const FCX_GLOBAL T *)p;
@@ -365,17 +359,12 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
   // the per-type reloads of the shared fields cost 8 % of the step; holding them costs 36
   // VGPRs, so the multi-type fused kernels run 3 instead of 4 waves per SIMD and still gain
   // 6-7 % per step.  Holding every input (round 1) kept ~56 VGPRs live and lost.
-  // FCX_HOLD_SHARED = 0 (A/B): the atmosphere-side inputs are reloaded per type too.
-#ifndef FCX_HOLD_SHARED
-#define FCX_HOLD_SHARED 1
-#endif
   constexpr bool kReload = TM == 0;  // bottom-side inputs: loaded per type
-  constexpr bool kHoldAtm = TM == 1 || FCX_HOLD_SHARED;
-  // grp.member names the pointer in TypeParams.  ATM: an atmosphere-side input.
+  // grp.member names the pointer in TypeParams.  ATM: an atmosphere-side input (held).
 #define HOLDX(var, grp, member, ATM)                  \
   {                                                   \
     const double *ptr_ = tp.grp.member;               \
-    if constexpr (kReload && !(kHoldAtm && ATM)) {    \
+    if constexpr (kReload && !ATM) {                  \
       if (ptr_) var = LD(ptr_, j0, nt);               \
     } else if (ptr_ && ptr_ != h_##var) {             \
       var = LD(ptr_, j0, nt);                         \
@@ -383,19 +372,15 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
     }                                                 \
   }
 #define HOLD(var, grp, member) HOLDX(var, grp, member, false)
-#define HOLDA(var, grp, member, bit) HOLDX(var, grp, member, true)
-  constexpr bool kHoldWind = kHoldAtm;
-  // FCX_PREFETCH_TYPE (multi-type kernels): the bottom-side inputs of type s+1 (TSUR FICE
+#define HOLDA(var, grp, member) HOLDX(var, grp, member, true)
+  // Next-type prefetch (multi-type kernels): the bottom-side inputs of type s+1 (TSUR FICE
   // CMOI CHEA CMOM and the FARE of the averages) are loaded when type s starts, so that the
   // wave does not stall on memory between two types.  The fused T = 2 kernels then hold
   // 162 / 166 / 124 VGPRs (CCLM / MOM5 / RCO, was 150 / 144 / 116): still 3 / 3 / 4 waves per
   // SIMD, no spills.  In one process over the same arrays (profiles/r03/ab_t2_prefetch.json,
   // random map): T = 2 step 1.672 -> 1.625 ms, CCLM 5.14 -> 5.26 TB/s, MOM5 5.54 -> 5.67,
-  // RCO 5.26 -> 5.50.  0 (A/B): load each type's inputs when it starts.
-#ifndef FCX_PREFETCH_TYPE
-#define FCX_PREFETCH_TYPE 1
-#endif
-  constexpr bool kPrefetch = kReload && FCX_PREFETCH_TYPE;
+  // RCO 5.26 -> 5.50.
+  constexpr bool kPrefetch = kReload;
   Vec<C, R> n_ts = {}, n_fi = {}, n_cmoi = {}, n_chea = {}, n_cmom = {}, n_fare = {};
   auto prefetch = [&](int s2) {
     const TypeParams &q = P->type[s2];
@@ -417,7 +402,6 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
   for (int s = 0; s < T; ++s) {
     if constexpr (kReload) {  // no bottom-side input of the previous type stays live
       ts = fi = cmoi = chea = cmom = Vec<C, R>{};
-      if constexpr (!kHoldAtm) ps = pa = qa = ta = u = v = amoi = amom = vel = Vec<C, R>{};
     }
     const TypeParams &tp = P->type[s];
     const TGridPtrs &g = tp.t;
@@ -443,14 +427,14 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
         HOLD(ts, t, tsur)
         HOLD(fi, t, fice)
       }
-      HOLDA(ps, t, psur, 0)
-      HOLDA(pa, t, patm, 1)
-      HOLDA(qa, t, qatm, 2)
-      HOLDA(ta, t, tatm, 3)
-      const bool wind_new = !kHoldWind ? (g.uatm || g.vatm) : ((g.uatm && g.uatm != h_u) || (g.vatm && g.vatm != h_v));
-      HOLDA(u, t, uatm, 4)
-      HOLDA(v, t, vatm, 5)
-      HOLDA(amoi, t, amoi, 6)
+      HOLDA(ps, t, psur)
+      HOLDA(pa, t, patm)
+      HOLDA(qa, t, qatm)
+      HOLDA(ta, t, tatm)
+      const bool wind_new = (g.uatm && g.uatm != h_u) || (g.vatm && g.vatm != h_v);
+      HOLDA(u, t, uatm)
+      HOLDA(v, t, vatm)
+      HOLDA(amoi, t, amoi)
       if constexpr (!kPrefetch) {
         HOLD(cmoi, t, cmoi)
         HOLD(chea, t, chea)
@@ -458,7 +442,7 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
       if (g.qsur_in) qs = LD(g.qsur_in, j0, nt);  // may be written by this pass: never held
       if (g.meva_in) me = LD(g.meva_in, j0, nt);
       if constexpr (MERGED) {
-        HOLDA(amom, uv[0], amom, 7)
+        HOLDA(amom, uv[0], amom)
         if constexpr (!kPrefetch) HOLD(cmom, uv[0], cmom)
       }
       if (wind_new) FOR_C vel.v[i] = wind(u.v[i], v.v[i]);
@@ -685,19 +669,15 @@ __device__ __forceinline__ int first_bit(uint64_t m) { return m ? __builtin_ctzl
 // XCD b % 8), each XCD with its own L2.  Neighbouring tiles share the 128-B lines of the
 // atmosphere outputs their segments end in; mapped to the same XCD, the two partial lines
 // merge in that L2 before write-back instead of reaching memory as two partial writes.
-// FCX_XCD_MAP 2 (default since round 3): XCD x takes runs of FCX_XCD_CHUNK = 64 consecutive
-// workgroups (256 tiles), the 8 XCDs' runs side by side, so that only one tile edge in 256
-// is shared between two XCDs AND the chip streams from one window of the arrays, as the
-// dispatch order advances.  1 (round 1-2): one contiguous eighth of the grid per XCD,
-// b -> x * (nb / 8) + min(x, nb % 8) + b / 8: eight windows 1/8 of the arrays apart.  In one
-// process over the same arrays, 2 against 1 (profiles/r03/xcd_map_ab/): step -2.4 / -6.1 %
-// fp64 (two boxes), -2.7 / -2.2 % fp32, -3.1 / -0.8 % at T = 2, -5.4 % on the periodic map.
-// 0 (A/B): plain dispatch order.
-#ifndef FCX_XCD_MAP
-#define FCX_XCD_MAP 2
-#endif
+// XCD runs (round 3): XCD x takes runs of FCX_XCD_CHUNK = 64 consecutive workgroups (256
+// tiles), the 8 XCDs' runs side by side, so that only one tile edge in 256 is shared between
+// two XCDs AND the chip streams from one window of the arrays, as the dispatch order
+// advances.  Rounds 1-2 gave each XCD one contiguous eighth of the grid, b -> x * (nb / 8) +
+// min(x, nb % 8) + b / 8: eight windows 1/8 of the arrays apart.  In one process over the
+// same arrays, runs against eighths (profiles/r03/xcd_map_ab/): step -2.4 / -6.1 % fp64 (two
+// boxes), -2.7 / -2.2 % fp32, -3.1 / -0.8 % at T = 2, -5.4 % on the periodic map.
 constexpr uint32_t kXcds = 8;
-#ifndef FCX_XCD_CHUNK  // FCX_XCD_MAP 2: workgroups per XCD run (fp64 kernels, 128-cell tiles)
+#ifndef FCX_XCD_CHUNK  // workgroups per XCD run (fp64 kernels, 128-cell tiles)
 #define FCX_XCD_CHUNK 64
 #endif
 #ifndef FCX_XCD_CHUNK_F32  // ... and of the fp32 kernels (256-cell tiles): 16 against 64,
@@ -705,17 +685,11 @@ constexpr uint32_t kXcds = 8;
 #endif                        // profiles/r03/xcd_map_ab/f32_*
 template <uint32_t K>
 __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb) {
-  if (!FCX_XCD_MAP) return b;
-  const uint32_t x = b % kXcds;
-  if (FCX_XCD_MAP == 2) {  // runs of K workgroups per XCD, the XCDs side by side
-    constexpr uint32_t row = K * kXcds;
-    const uint32_t full = nb / row * row;
-    if (b >= full) return b;
-    const uint32_t i = b / kXcds;
-    return i / K * row + x * K + i % K;
-  }
-  const uint32_t q = nb / kXcds, r = nb % kXcds;
-  return x * q + min(x, r) + b / kXcds;
+  constexpr uint32_t row = K * kXcds;  // runs of K workgroups per XCD, the XCDs side by side
+  const uint32_t full = nb / row * row;
+  if (b >= full) return b;
+  const uint32_t x = b % kXcds, i = b / kXcds;
+  return i / K * row + x * K + i % K;
 }
 
 // Where a finished segment sum goes: a segment that continues into the next tile leaves its
@@ -725,7 +699,7 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb) {
 // R: the engine's output type (an fp32 engine's atmosphere outputs are float, rounded once)
 template <class R>
 __device__ __forceinline__ void segment_done(const AtmosFused &af, int64_t tile, int32_t a, const double *acc,
-                                             bool cont, bool nt_line = false) {
+                                             bool cont) {
   if (cont) {  // the next tile's crossing record: the six prefix sums, 16-B stores
 #pragma unroll
     for (int q = 0; q < kFusedFields / 2; ++q)
@@ -733,20 +707,17 @@ __device__ __forceinline__ void segment_done(const AtmosFused &af, int64_t tile,
     return;
   }
   if (FCX_DBG_ATM_NOSTORE) return;
-// Non-temporal atmosphere-output stores: 3 (default) for fp64 outputs, 1 all, 0 none, 2 only
-// the lines a tile owns whole.  Since the segment sums run in rounds, a round writes the
-// tile's values of a field with one instruction, and for fp64 outputs NT stores gained
-// 3.4-4.4 % per step (periodic / random map); fp32 outputs lost 7 % with them
+// Non-temporal atmosphere-output stores for fp64 outputs.  Since the segment sums run in
+// rounds, a round writes the tile's values of a field with one instruction, and for fp64
+// outputs NT stores gained 3.4-4.4 % per step (periodic / random map); fp32 outputs lost 7 %
+// with them, and NT only for the lines a tile owns whole changed nothing
 // (profiles/r02/nt_atm_ab/; round 1, with one store instruction per cell position, all-NT
 // had lost 6.8 %).
-#ifndef FCX_ATM_NT_STORE
-#define FCX_ATM_NT_STORE 3
-#endif
 #pragma unroll
   for (int k = 0; k < kFusedFields; ++k) {
     if (!af.out[k]) continue;
     FCX_GLOBAL R *o = gptr(reinterpret_cast<R *>(af.out[k]) + tiled(a, af.out_tpad));
-    if (FCX_ATM_NT_STORE == 1 || (FCX_ATM_NT_STORE == 2 && nt_line) || (FCX_ATM_NT_STORE == 3 && sizeof(R) == 8))
+    if constexpr (sizeof(R) == 8)
       __builtin_nontemporal_store((R)acc[k], o);
     else
       *o = (R)acc[k];
@@ -892,50 +863,25 @@ __global__ __launch_bounds__(64 * atmos_waves<C>(), RAVG  ? FCX_RAVG_ATMOS_BLOCK
       m[i] = __ballot(st[i]);
     }
     wave_sync();  // the wave's LDS products are visible to all its lanes
-#ifndef FCX_SEG_ROUNDS  // A/B: 0 = one pass per cell position i (the round-1 loop)
-#define FCX_SEG_ROUNDS 1
-#endif
-    if (FCX_SEG_ROUNDS) {
-      // Rounds of one segment start per lane: every lane with a start sums its segment and
-      // stores the six values in the same round, so a tile's atmosphere stores are six
-      // store instructions per round (one round when every run is >= C cells long, as on an
-      // intersection grid), not six per cell position of the lane.
-      // atmosphere cells of the tile's first and last cell: the output lines strictly between
-      // theirs hold only values of segments that start in this tile (FCX_ATM_NT_STORE 2)
-      const int32_t a_lo = __shfl(a[0], 0), a_hi = __shfl(a[C - 1], 63);
-      constexpr int kLineCells = 128 / (int)sizeof(R);
-      uint32_t rem = 0;  // bit i: cell C*lane+i starts a segment not summed yet (an own cell)
+    // Rounds of one segment start per lane (round 2): every lane with a start sums its
+    // segment and stores the six values in the same round, so a tile's atmosphere stores are
+    // six store instructions per round (one round when every run is >= C cells long, as on an
+    // intersection grid), not six per cell position of the lane as in round 1
+    // (profiles/r02/seg_rounds_ab/).
+    uint32_t rem = 0;  // bit i: cell C*lane+i starts a segment not summed yet (an own cell)
 #pragma unroll
-      for (int i = 0; i < C; ++i)
-        if (st[i] && a[i] >= 0 && (!HALO || lane < own_lanes)) rem |= 1u << i;
-      while (__ballot(rem != 0)) {
-        if (rem) {
-          const int i = __builtin_ctz(rem);
-          rem &= rem - 1;
-          int32_t ai = a[0];
+    for (int i = 0; i < C; ++i)
+      if (st[i] && a[i] >= 0 && (!HALO || lane < own_lanes)) rem |= 1u << i;
+    while (__ballot(rem != 0)) {
+      if (rem) {
+        const int i = __builtin_ctz(rem);
+        rem &= rem - 1;
+        int32_t ai = a[0];
 #pragma unroll
-          for (int q = 1; q < C; ++q)
-            if (q == i) ai = a[q];
-          const int c = C * lane + i;
-          // next start after cell c: cell C*j+i' with j > l, or j == l and i' > i
-          int e_end = kT;
-#pragma unroll
-          for (int q = 0; q < C; ++q) e_end = min(e_end, C * first_bit(m[q] & (q > i ? at_or_above : above)) + q);
-          const int end = min(e_end, kT);
-          double acc[kFusedFields];
-#pragma unroll
-          for (int k = 0; k < kFusedFields; ++k) acc[k] = 0.0;
-          for (int e = c; e < end; ++e) add_cell(acc, e);
-          const bool own = a_hi >= 0 && ai / kLineCells > a_lo / kLineCells && ai / kLineCells < a_hi / kLineCells;
-          // (HALO: the segment ends inside the wave's own + halo cells by the engine's rule)
-          segment_done<R>(af, tile, ai, acc, !HALO && end == kT && next_a == ai, own);
-        }
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < C; ++i) {
-        if (!st[i] || a[i] < 0 || (HALO && lane >= own_lanes)) continue;
+        for (int q = 1; q < C; ++q)
+          if (q == i) ai = a[q];
         const int c = C * lane + i;
+        // next start after cell c: cell C*j+i' with j > l, or j == l and i' > i
         int e_end = kT;
 #pragma unroll
         for (int q = 0; q < C; ++q) e_end = min(e_end, C * first_bit(m[q] & (q > i ? at_or_above : above)) + q);
@@ -944,7 +890,8 @@ __global__ __launch_bounds__(64 * atmos_waves<C>(), RAVG  ? FCX_RAVG_ATMOS_BLOCK
 #pragma unroll
         for (int k = 0; k < kFusedFields; ++k) acc[k] = 0.0;
         for (int e = c; e < end; ++e) add_cell(acc, e);
-        segment_done<R>(af, tile, a[i], acc, !HALO && end == kT && next_a == a[i]);
+        // (HALO: the segment ends inside the wave's own + halo cells by the engine's rule)
+        segment_done<R>(af, tile, ai, acc, !HALO && end == kT && next_a == ai);
       }
     }
     // the number of head cells (continuing the previous tile's segment) for
