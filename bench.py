@@ -383,7 +383,7 @@ def measure(wl, args, world, dist, comm, steps, warmup, t_base=0, cold=False):
     # engine; every engine with --kernel-events all), the event-timed warm-up block otherwise
     kern_mean = probe_ms.mean(axis=0)
     timed = {i: np.array([row[i][0].elapsed_time(row[i][1]) for row in ev])
-             for i in range(nv) if ev[0][i] is not None}
+             for i in range(nv) if ev and ev[0][i] is not None}
     for i, x in timed.items():
         kern_mean[i] = x.mean()
     t_max = elapsed
