@@ -727,7 +727,9 @@ __device__ __forceinline__ void segment_done(const AtmosFused &af, int64_t tile,
 }
 
 // blocks per CU the multi-type (RAVG) fused kernel is compiled for: 3 -> <= 168 VGPRs, room
-// for the held atmosphere-side inputs (4 -> <= 128 spilled them)
+// for the held atmosphere-side inputs (4 -> <= 128 spills them: T = 2 step +24 %).  2 gives
+// the same 3 waves per SIMD (+1 VGPR): -0.7 % in one process over shared arrays, +0.5 % in
+// alternating bench processes on one box (profiles/r03/ravg_blocks_ab/): 3 stays.
 #ifndef FCX_RAVG_ATMOS_BLOCKS
 #define FCX_RAVG_ATMOS_BLOCKS 3
 #endif
