@@ -215,6 +215,8 @@ def multi_gpu_check(wl, world, rank, dist, samples=2000):
                 x0, x1 = starts[a], starts[a + 1]
                 interior_bad += int(got[a] != seq_sum(la.weight[x0:x1], flux[x0:x1]))
             for side, a, slot in (("left", 0, la.left), ("right", la.n_atmos - 1, la.right)):
+                if side == "right" and la.n_atmos == 1 and la.right == la.left:
+                    continue  # one cell shared on both sides: one slot, its part sent once
                 if slot >= 0:
                     x0, x1 = starts[a], starts[a + 1]
                     edge.append({"variant": i, "field": name, "slot": int(slot), "side": side, "rank": rank,
@@ -423,10 +425,11 @@ def main():
 
     f32 = args.precision == "f32"
     # the library's own RCCL communicator for the boundary exchange (N > 1); the unique id is
-    # broadcast over torch.distributed.  --backend gloo (same-device rehearsals on one GPU,
-    # where RCCL refuses two ranks per device) keeps torch's all-reduce of the slots instead.
+    # broadcast over torch.distributed.  Same-device rehearsals on one GPU (RCCL refuses two
+    # ranks per device) keep torch's all-reduce of the slots, unless FCX_RCCL_LIBRARY names a
+    # stand-in that allows it (tests/cpp/mock_rccl.cpp: the libfcx exchange code itself runs)
     comm = None
-    if world > 1 and args.collective == "rccl" and not args.same_device:
+    if world > 1 and args.collective == "rccl" and (not args.same_device or os.environ.get("FCX_RCCL_LIBRARY")):
         from fcx.comm import Comm
 
         comm = Comm.from_torch(gpu)
@@ -530,7 +533,9 @@ def main():
             "atmos_accumulation": (f"6 fluxes -> {la.n_atmos} atmosphere cells per GPU (1 per ~4 "
                                    f"exchange cells, {args.atmos_map} runs), one all-reduce of the shared "
                                    "boundary cells per step"
-                                   + (" (libfcx RCCL communicator)" if comm is not None else
+                                   + ((" (libfcx RCCL communicator" + (", FCX_RCCL_LIBRARY stand-in)"
+                                                                         if os.environ.get("FCX_RCCL_LIBRARY") else ")"))
+                                      if comm is not None else
                                       " (torch.distributed, rehearsal)" if world > 1 else " (none needed at N=1)")
                                    if la is not None else "off"),
         },

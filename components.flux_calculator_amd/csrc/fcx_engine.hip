@@ -25,6 +25,7 @@
 #include <vector>
 
 #include <sched.h>
+#include <unistd.h>
 
 #include "fcx_copy_pool.h"
 #include "fcx_internal.h"
@@ -85,6 +86,7 @@ struct StagePool {
   bool tiled = false;
   size_t slot = 0, pitch = 0;  // tiled: bytes of one slot's tile, bytes of one row
   bool mapped = false;         // the image IS the kernels' buffer (device-mapped): no DMA
+  bool disabled = false;       // its image could not be page-locked: members take the direct path
 };
 
 // One host array <-> its mirror through the staging arena: `n` elements of `es` bytes.
@@ -122,11 +124,25 @@ int var0(int var) { return var - 1; }
 
 // threads of the host copies: FCX_OPT_HOST_THREADS, else min(16, OMP_NUM_THREADS if set, else
 // the CPUs this process may run on) -- an MPI rank pinned to one core copies alone
+// an unpinned rank (affinity = every online CPU) shares the node with the other local ranks
+// of its launch (MPI or torchrun environment): its share of the CPUs, so that several ranks'
+// copy threads do not oversubscribe the cores the coupled models run on
+int local_ranks() {
+  for (const char *v : {"OMPI_COMM_WORLD_LOCAL_SIZE", "MPI_LOCALNRANKS", "SLURM_NTASKS_PER_NODE", "LOCAL_WORLD_SIZE"})
+    if (const char *x = std::getenv(v)) {
+      const int k = std::atoi(x);
+      if (k > 0) return k;
+    }
+  return 1;
+}
+
 int default_host_threads() {
   static const int n = [] {
     int cpus = 1;
     cpu_set_t set;
     if (sched_getaffinity(0, sizeof set, &set) == 0) cpus = std::max(1, CPU_COUNT(&set));
+    const long online = sysconf(_SC_NPROCESSORS_ONLN);
+    if (online > 0 && cpus >= online) cpus = std::max(1, cpus / local_ranks());
     if (const char *omp = std::getenv("OMP_NUM_THREADS")) {
       const int t = std::atoi(omp);
       if (t > 0) cpus = std::min(cpus, t);
@@ -245,6 +261,7 @@ struct fcx_engine {
   // staging arena of caller heap arrays (FCX_OPT_HOST_STAGING): page-locked host images of
   // the device pools that hold their mirrors, allocated at the first staged transfer
   bool staging = true;
+  bool deferred_scatter = false;        // FCX_OPT_DEFERRED_SCATTER: downloads scattered at fcx_synchronize
   int host_threads = 0;                 // FCX_OPT_HOST_THREADS (0: default_host_threads)
   std::vector<StagePool> spools;
   std::vector<Xfer> pending_out;        // D2H into the arena whose scatter waits for the stream
@@ -1348,16 +1365,37 @@ static void stage_setup(fcx_engine *e) {
       if (!f.external && heap(f.out_host, rm.n_dst)) f.st = stage_ref(e, f.out_dev);
 }
 
-// the host images of the pools these transfers use (allocated at first use: pools that are
-// never transferred -- e.g. arrays bound but not used by any launch -- get none)
-static int stage_alloc(fcx_engine *e, const std::vector<Xfer> &xs) {
-  for (const Xfer &x : xs) {
-    StagePool &p = e->spools[(size_t)x.sp];
-    if (p.host) continue;
-    hipError_t err = hipHostMalloc((void **)&p.host, std::max<size_t>(p.bytes, 1), hipHostMallocDefault);
-    if (err != hipSuccess)
-      return fail(FCX_E_NOMEM, "hipHostMalloc(%zu) for the staging arena: %s", p.bytes, hipGetErrorString(err));
+// at commit: the host image of every staging pool (page-locked, the pool's size: the pinned
+// footprint is fcx_staging_bytes).  A pool whose image cannot be page-locked (a memory-tight
+// node) falls back to the direct path -- its mirrors are copied one runtime copy per array
+// from the caller's pageable memory, as with FCX_OPT_HOST_STAGING 0 -- so a step never
+// meets an allocation failure.
+static void stage_alloc_all(fcx_engine *e) {
+  // FCX_TEST_PIN_FAIL=1 (tests only): every image fails, as on a node out of lockable memory
+  const char *inject = std::getenv("FCX_TEST_PIN_FAIL");
+  const bool fail_all = inject && *inject == '1';
+  for (size_t i = 0; i < e->spools.size(); ++i) {
+    StagePool &p = e->spools[i];
+    if (p.host) continue;  // (a mapped arena has its image already)
+    if (!fail_all && hipHostMalloc((void **)&p.host, std::max<size_t>(p.bytes, 1), hipHostMallocDefault) == hipSuccess)
+      continue;
+    (void)hipGetLastError();
+    p.host = nullptr;
+    p.disabled = true;
+    auto drop = [&](StageRef &st) {
+      if (st.sp == (int)i) st.sp = -1;
+    };
+    for (auto &bf : e->bufs) drop(bf.st);
+    for (auto &f : e->atm_fields) drop(f.st);
+    for (auto &rm : e->remaps)
+      for (auto &f : rm.fields) drop(f.st);
   }
+}
+
+// the host images of the pools these transfers use (allocated at commit)
+static int stage_alloc(fcx_engine *e, const std::vector<Xfer> &xs) {
+  for (const Xfer &x : xs)
+    if (!e->spools[(size_t)x.sp].host) return fail(FCX_E_STATE, "staging pool %d has no host image", x.sp);
   return FCX_OK;
 }
 
@@ -1481,12 +1519,18 @@ static int stage_in(fcx_engine *e, const std::vector<Xfer> &xs, hipStream_t s) {
   return FCX_OK;
 }
 
-// download through the arena: the DMAs now, the host copies at the next synchronisation
+// download through the arena: the DMAs now; the host copies into the caller's arrays right
+// away (the stream is waited for, so the arrays hold the outputs when fcx_download returns),
+// or with FCX_OPT_DEFERRED_SCATTER at the next fcx_synchronize
 static int stage_out(fcx_engine *e, const std::vector<Xfer> &xs, hipStream_t s) {
   if (xs.empty()) return FCX_OK;
   if (int r = stage_alloc(e, xs)) return r;
   HIP_TRY(stage_dma(e, xs, 0, -1, false, s));
   e->pending_out.insert(e->pending_out.end(), xs.begin(), xs.end());
+  if (!e->deferred_scatter) {
+    HIP_TRY(hipStreamSynchronize(s));
+    return stage_flush(e);
+  }
   return FCX_OK;
 }
 
@@ -1738,8 +1782,9 @@ extern "C" int fcx_commit(fcx_engine *e) {
     const size_t cnt = std::max<size_t>((size_t)e->atm_nb * stride, 1);
     HIP_TRY(hipMalloc(&e->atm_shared_own, cnt * sizeof(double)));
     HIP_TRY(hipMemset(e->atm_shared_own, 0, cnt * sizeof(double)));
-    if (e->atm_left >= 0 && e->atm_right >= 0 && e->n_atmos < 2)
-      return fail(FCX_E_UNSUPPORTED, "one atmosphere cell shared on both sides (shard too small)");
+    if (e->atm_left >= 0 && e->atm_right >= 0 && e->n_atmos < 2 && e->atm_left != e->atm_right)
+      return fail(FCX_E_ARG, "the one atmosphere cell is shared on both sides: it needs one boundary slot for all "
+                             "its ranks (left == right), not %d and %d", e->atm_left, e->atm_right);
     e->atm_shared = e->atm_nb > 0 ? e->atm_shared_own : nullptr;
     e->atm_stride = (int32_t)stride;
   }
@@ -1782,6 +1827,7 @@ extern "C" int fcx_commit(fcx_engine *e) {
   }
   if (e->rec_bytes) HIP_TRY(hipMalloc(&e->d_rec, e->rec_bytes));
   stage_setup(e);
+  stage_alloc_all(e);
   e->committed = true;
   return FCX_OK;
 }
@@ -2386,8 +2432,23 @@ extern "C" int fcx_staging_bytes(fcx_engine *e, int64_t *bytes) {
   if (int r = check(e)) return r;
   if (!bytes) return fail(FCX_E_ARG, "NULL argument");
   int64_t b = 0;
-  for (auto &p : e->spools) b += (int64_t)p.bytes;
+  for (auto &p : e->spools)
+    if (p.host) b += (int64_t)p.bytes;  // page-locked images only (a disabled pool has none)
   *bytes = b;
+  return FCX_OK;
+}
+
+// retired in version 3 (kept as stubs for one release): nothing is page-locked for the
+// caller any more, and the in-launch carry hand-off and its recoveries are gone
+extern "C" int fcx_pinned_bytes(fcx_engine *e, int64_t *bytes) {
+  if (!e || !bytes) return fail(FCX_E_ARG, "NULL argument");
+  *bytes = 0;
+  return FCX_OK;
+}
+
+extern "C" int fcx_handoff_recoveries(fcx_engine *e, int64_t *count) {
+  if (!e || !count) return fail(FCX_E_ARG, "NULL argument");
+  *count = 0;
   return FCX_OK;
 }
 
@@ -2528,6 +2589,15 @@ extern "C" int fcx_set_option(fcx_engine *e, int option, int64_t value) {
       if (e->committed) return fail(FCX_E_STATE, "tiled_layout is applied at fcx_commit");
       e->tiled_opt = value != 0;
       return FCX_OK;
+    case FCX_OPT_DEFERRED_SCATTER:
+      e->deferred_scatter = value != 0;
+      return FCX_OK;
+    case FCX_OPT_RETIRED_PIN_HOST:
+    case FCX_OPT_RETIRED_12:
+    case FCX_OPT_RETIRED_CARRY_HANDOFF:
+      // removed in version 3 (nothing of the caller's memory is page-locked; the in-launch
+      // carry hand-off is gone): accepted and ignored, so hosts that set them still run
+      return FCX_OK;
     default:
       return fail(FCX_E_ARG, "option %d unknown", option);
   }
@@ -2603,8 +2673,9 @@ extern "C" int fcx_set_atmos_shared(fcx_engine *e, double *shared, int32_t nb, i
     return fail(FCX_E_ARG, "bad shared boundary buffer");
   if ((left >= 0 || right >= 0) && stride < (int32_t)e->atm_fields.size())
     return fail(FCX_E_ARG, "stride %d < %zu atmosphere fields", stride, e->atm_fields.size());
-  if (left >= 0 && right >= 0 && e->n_atmos < 2)
-    return fail(FCX_E_UNSUPPORTED, "one atmosphere cell shared on both sides (shard too small)");
+  if (left >= 0 && right >= 0 && e->n_atmos == 1 && left != right)
+    return fail(FCX_E_ARG, "the one atmosphere cell is shared on both sides: it needs one boundary slot for all "
+                           "its ranks (left == right), not %d and %d", left, right);
   if (e->own_shared) return fail(FCX_E_STATE, "boundary slots already owned by the engine (fcx_set_atmos_boundaries)");
   e->atm_shared = shared;
   e->atm_nb = nb;
@@ -2725,17 +2796,24 @@ struct RcclApi {
   ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
   ncclResult_t (*AllReduce)(const void *, void *, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
                             hipStream_t) = nullptr;
-  ncclResult_t (*GroupStart)() = nullptr;
-  ncclResult_t (*GroupEnd)() = nullptr;
   const char *(*GetErrorString)(ncclResult_t) = nullptr;
 };
 
 const RcclApi &rccl() {
   static RcclApi api = [] {
     RcclApi a;
-    void *h = dlopen("librccl.so", RTLD_NOW | RTLD_NOLOAD);  // already in the process (torch)
-    if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
-    if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    void *h = nullptr;
+    // FCX_RCCL_LIBRARY: an explicit library with the same entry points (tests: a host-memory
+    // stand-in that lets several ranks share one GPU, which RCCL refuses, and checks that every
+    // rank issues the same collective sequence)
+    const char *forced = std::getenv("FCX_RCCL_LIBRARY");
+    if (forced && *forced) {
+      h = dlopen(forced, RTLD_NOW | RTLD_LOCAL);
+    } else {
+      h = dlopen("librccl.so", RTLD_NOW | RTLD_NOLOAD);  // already in the process (torch)
+      if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+      if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    }
     if (!h) {
       const char *m = dlerror();
       a.why = m ? m : "librccl.so not found";
@@ -2751,11 +2829,9 @@ const RcclApi &rccl() {
     a.CommInitRank = reinterpret_cast<decltype(a.CommInitRank)>(sym("ncclCommInitRank"));
     a.CommDestroy = reinterpret_cast<decltype(a.CommDestroy)>(sym("ncclCommDestroy"));
     a.AllReduce = reinterpret_cast<decltype(a.AllReduce)>(sym("ncclAllReduce"));
-    a.GroupStart = reinterpret_cast<decltype(a.GroupStart)>(sym("ncclGroupStart"));
-    a.GroupEnd = reinterpret_cast<decltype(a.GroupEnd)>(sym("ncclGroupEnd"));
     a.GetErrorString = reinterpret_cast<decltype(a.GetErrorString)>(sym("ncclGetErrorString"));
     a.ok = all;
-    if (!all) a.why = "librccl.so lacks an nccl* entry point";
+    if (!all) a.why = std::string(forced && *forced ? forced : "librccl.so") + " lacks an nccl* entry point";
     return a;
   }();
   return api;
@@ -2773,6 +2849,13 @@ struct fcx_comm {
   ncclComm_t comm = nullptr;
   int nranks = 0, rank = 0, device = 0;
   std::vector<hipEvent_t> events;  // stream joins of fcx_atmos_allreduce (engines on several streams)
+  // the boundary exchange's collective contract (atmos_exchange): packing scratch for slot
+  // regions that are not one contiguous run in list order, and the exchange signature every
+  // rank has agreed on (checked once per signature by a blocking max-all-reduce)
+  double *scratch = nullptr;
+  size_t scratch_cap = 0;
+  double *agree = nullptr;  // 2 * kSigWords doubles (device)
+  std::vector<double> agreed;
 };
 
 extern "C" int fcx_comm_unique_id(void *id) {
@@ -2806,6 +2889,8 @@ extern "C" int fcx_comm_create(int device, int nranks, int rank, const void *id,
 extern "C" int fcx_comm_destroy(fcx_comm *c) {
   if (!c) return FCX_OK;
   for (hipEvent_t ev : c->events) (void)hipEventDestroy(ev);
+  (void)hipFree(c->scratch);
+  (void)hipFree(c->agree);
   if (c->comm) (void)rccl().CommDestroy(c->comm);
   delete c;
   return FCX_OK;
@@ -2818,17 +2903,75 @@ extern "C" int fcx_comm_allreduce_sum(fcx_comm *c, double *buf, size_t count, vo
   return FCX_OK;
 }
 
-// the boundary exchange of one or several engines of this rank: one all-reduce over their
-// boundary slots on the first engine's stream (one call when the engines' slot regions are
-// adjacent in one buffer, else one per engine inside one RCCL group), then fcx_atmos_finish
-// of each engine.  Engines on other streams are joined with events before and after.
+// The boundary exchange of one or several engines of this rank: ONE all-reduce (sum, fp64)
+// over the boundary slots of the listed engines, in list order, on the first engine's
+// stream, then fcx_atmos_finish of each.  Engines on other streams are joined with events
+// before and after.  The collective contract -- the call sequence is the same on every rank
+// whatever each rank's memory layout or engine state, so no rank is left waiting:
+//  * the count is sum(n_boundaries * stride) over the listed engines that have boundary
+//    slots: configuration, the same on every rank of one decomposition (n_boundaries = P-1);
+//  * the slots are reduced in place when the regions follow each other in list order in one
+//    buffer (the bench's layout), else through the communicator's scratch (device copies each
+//    way): the choice changes copies, never the collective;
+//  * an engine with nothing new in its slots -- already completed in this run by its
+//    attached communicator, or no accumulation since its last exchange -- takes part with
+//    zeros and is not finished; the second case is an error returned AFTER the collective;
+//  * the first exchange of each signature (engines with slots, values, their n_boundaries
+//    and strides in order) is preceded by a blocking max-all-reduce of the signature and its
+//    negation: ranks that disagree all return the same named error instead of entering
+//    all-reduces of different counts (RCCL would hang).
+namespace {
+constexpr int kSigWords = 3;
+}
+
+static int exchange_agree(fcx_comm *c, const std::vector<double> &sig, hipStream_t s) {
+  for (size_t i = 0; i + kSigWords <= c->agreed.size(); i += kSigWords)
+    if (std::equal(sig.begin(), sig.end(), c->agreed.begin() + (std::ptrdiff_t)i)) return FCX_OK;
+  if (!c->agree) HIP_TRY(hipMalloc(&c->agree, 2 * kSigWords * sizeof(double)));
+  double h[2 * kSigWords];
+  for (int i = 0; i < kSigWords; ++i) {
+    h[i] = sig[(size_t)i];
+    h[kSigWords + i] = -sig[(size_t)i];
+  }
+  HIP_TRY(hipMemcpyAsync(c->agree, h, sizeof h, hipMemcpyHostToDevice, s));
+  RCCL_TRY(rccl().AllReduce(c->agree, c->agree, 2 * kSigWords, ncclFloat64, ncclMax, c->comm, s));
+  HIP_TRY(hipMemcpyAsync(h, c->agree, sizeof h, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  bool same = true;
+  for (int i = 0; i < kSigWords; ++i) same = same && h[i] == -h[kSigWords + i];
+  if (!same)
+    return fail(FCX_E_ARG,
+                "ranks disagree on the boundary exchange (rank %d of %d): here %.0f engines with boundary slots, "
+                "%.0f slot values, layout hash %.0f; over the ranks %.0f..%.0f engines, %.0f..%.0f values, hash "
+                "%.0f..%.0f",
+                c->rank, c->nranks, sig[0], sig[1], sig[2], -h[3], h[0], -h[4], h[1], -h[5], h[2]);
+  c->agreed.insert(c->agreed.end(), sig.begin(), sig.end());
+  return FCX_OK;
+}
+
 static int atmos_exchange(fcx_comm *c, fcx_engine *const *es, int n) {
-  std::vector<fcx_engine *> v;
+  std::vector<fcx_engine *> v;  // the engines with boundary slots, in list order
   for (int i = 0; i < n; ++i)
-    if (es[i] && !es[i]->exchanged && es[i]->atm_shared && es[i]->atm_nb > 0 && es[i]->atm_stride > 0)
-      v.push_back(es[i]);
+    if (es[i]->atm_shared && es[i]->atm_nb > 0 && es[i]->atm_stride > 0) v.push_back(es[i]);
+  uint64_t hash = 1469598103ull;
+  size_t total = 0;
+  for (auto *e : v) {
+    total += (size_t)e->atm_nb * e->atm_stride;
+    hash = (hash * 1000003ull + (uint64_t)e->atm_nb * 4099ull + (uint64_t)e->atm_stride) & ((1ull << 48) - 1);
+  }
+  hipStream_t s0 = n > 0 ? es[0]->stream : nullptr;
+  if (int r = exchange_agree(c, {(double)v.size(), (double)total, (double)hash}, s0)) return r;
   if (v.empty()) return FCX_OK;
-  hipStream_t s0 = v[0]->stream;
+  s0 = v[0]->stream;
+  std::vector<char> fresh(v.size());
+  int stale = -1;  // first engine with no accumulation since its last exchange
+  bool inplace = true;
+  for (size_t i = 0; i < v.size(); ++i) {
+    fresh[i] = v[i]->atm_done && !v[i]->exchanged;
+    if (!v[i]->atm_done && stale < 0) stale = (int)i;
+    inplace = inplace && fresh[i] &&
+              (i == 0 || v[i - 1]->atm_shared + (size_t)v[i - 1]->atm_nb * v[i - 1]->atm_stride == v[i]->atm_shared);
+  }
   size_t joins = 0;
   for (auto *e : v) joins += e->stream != s0 ? 2 : 0;
   while (c->events.size() < joins) {
@@ -2842,36 +2985,49 @@ static int atmos_exchange(fcx_comm *c, fcx_engine *const *es, int n) {
       HIP_TRY(hipEventRecord(c->events[k], e->stream));
       HIP_TRY(hipStreamWaitEvent(s0, c->events[k++], 0));
     }
-  std::vector<fcx_engine *> byptr(v);
-  std::sort(byptr.begin(), byptr.end(), [](fcx_engine *a, fcx_engine *b) { return a->atm_shared < b->atm_shared; });
-  bool adjacent = true;
-  for (size_t i = 1; i < byptr.size(); ++i)
-    adjacent = adjacent && byptr[i - 1]->atm_shared + (size_t)byptr[i - 1]->atm_nb * byptr[i - 1]->atm_stride ==
-                               byptr[i]->atm_shared;
-  if (adjacent) {
-    size_t count = 0;
-    for (auto *e : byptr) count += (size_t)e->atm_nb * e->atm_stride;
-    RCCL_TRY(rccl().AllReduce(byptr[0]->atm_shared, byptr[0]->atm_shared, count, ncclFloat64, ncclSum, c->comm, s0));
+  if (inplace) {
+    RCCL_TRY(rccl().AllReduce(v[0]->atm_shared, v[0]->atm_shared, total, ncclFloat64, ncclSum, c->comm, s0));
   } else {
-    RCCL_TRY(rccl().GroupStart());
-    for (auto *e : v) {
-      const ncclResult_t r = rccl().AllReduce(e->atm_shared, e->atm_shared, (size_t)e->atm_nb * e->atm_stride,
-                                              ncclFloat64, ncclSum, c->comm, s0);
-      if (r != ncclSuccess) {
-        (void)rccl().GroupEnd();
-        return fail(FCX_E_HIP, "ncclAllReduce: %s", rccl().GetErrorString(r));
-      }
+    if (c->scratch_cap < total) {
+      (void)hipFree(c->scratch);
+      c->scratch = nullptr;
+      c->scratch_cap = 0;
+      HIP_TRY(hipMalloc(&c->scratch, total * sizeof(double)));
+      c->scratch_cap = total;
     }
-    RCCL_TRY(rccl().GroupEnd());
+    size_t off = 0;
+    for (size_t i = 0; i < v.size(); ++i) {
+      const size_t cnt = (size_t)v[i]->atm_nb * v[i]->atm_stride;
+      if (fresh[i])
+        HIP_TRY(hipMemcpyAsync(c->scratch + off, v[i]->atm_shared, cnt * sizeof(double), hipMemcpyDeviceToDevice, s0));
+      else
+        HIP_TRY(hipMemsetAsync(c->scratch + off, 0, cnt * sizeof(double), s0));
+      off += cnt;
+    }
+    RCCL_TRY(rccl().AllReduce(c->scratch, c->scratch, total, ncclFloat64, ncclSum, c->comm, s0));
+    off = 0;
+    for (size_t i = 0; i < v.size(); ++i) {
+      const size_t cnt = (size_t)v[i]->atm_nb * v[i]->atm_stride;
+      if (fresh[i])
+        HIP_TRY(hipMemcpyAsync(v[i]->atm_shared, c->scratch + off, cnt * sizeof(double), hipMemcpyDeviceToDevice, s0));
+      off += cnt;
+    }
   }
-  for (auto *e : v) {
+  for (size_t i = 0; i < v.size(); ++i) {
+    fcx_engine *e = v[i];
     if (e->stream != s0) {  // the finish of that engine waits for the all-reduce
       HIP_TRY(hipEventRecord(c->events[k], s0));
       HIP_TRY(hipStreamWaitEvent(e->stream, c->events[k++], 0));
     }
+    if (!fresh[i]) continue;
     if (int r = fcx_atmos_finish(e)) return r;
     e->exchanged = true;
   }
+  if (stale >= 0)
+    return fail(FCX_E_STATE,
+                "boundary exchange: engine %d of the list has no accumulation since its last exchange (fcx_run or "
+                "fcx_run_atmos first); it took part with zeros",
+                stale);
   return FCX_OK;
 }
 

@@ -24,7 +24,9 @@ MODULE fcx_c_api
                                FCX_OPT_PIPELINE_CHUNKS = 7, FCX_OPT_ZERO_COPY = 9, FCX_OPT_TIMING = 10, &
                                FCX_OPT_TILED_LAYOUT = 11, FCX_OPT_REMAP_PACK = 13, &
                                FCX_OPT_HOST_STAGING = 15, FCX_OPT_HOST_THREADS = 16, &
-                               FCX_OPT_ATMOS_HALO = 17
+                               FCX_OPT_ATMOS_HALO = 17, FCX_OPT_DEFERRED_SCATTER = 18
+  ! retired in version 3: accepted by fcx_set_option and ignored
+  INTEGER(c_int), PARAMETER :: FCX_OPT_PIN_HOST = 6, FCX_OPT_CARRY_HANDOFF = 14
   ! the RCCL unique id travels between the ranks as these many bytes (MPI_Bcast)
   INTEGER, PARAMETER :: FCX_COMM_ID_BYTES = 128
 
@@ -273,6 +275,19 @@ MODULE fcx_c_api
       TYPE(c_ptr), VALUE :: engine
       INTEGER(c_int64_t), INTENT(OUT) :: bytes
       INTEGER(c_int) :: fcx_zero_copy_bytes
+    END FUNCTION
+    ! retired in version 3 (always 0), kept for one release
+    FUNCTION fcx_pinned_bytes(engine, bytes) BIND(C, name='fcx_pinned_bytes')
+      IMPORT :: c_int, c_int64_t, c_ptr
+      TYPE(c_ptr), VALUE :: engine
+      INTEGER(c_int64_t), INTENT(OUT) :: bytes
+      INTEGER(c_int) :: fcx_pinned_bytes
+    END FUNCTION
+    FUNCTION fcx_handoff_recoveries(engine, count) BIND(C, name='fcx_handoff_recoveries')
+      IMPORT :: c_int, c_int64_t, c_ptr
+      TYPE(c_ptr), VALUE :: engine
+      INTEGER(c_int64_t), INTENT(OUT) :: count
+      INTEGER(c_int) :: fcx_handoff_recoveries
     END FUNCTION
     ! ---- exchange -> model remaps (the OASIS 'S' maps to a bottom model, SURVEY.md 8f rank 3):
     ! src/dst 0-based cells, links in file order; outputs REAL(wp) arrays of n_dst cells

@@ -37,6 +37,12 @@ MODULE flux_calculator_calculate
     PUBLIC fcx_attach, fcx_register_average, fcx_commit_engine, fcx_run_phase, fcx_detach
 
     TYPE(c_ptr), SAVE :: engine = c_null_ptr
+    ! What fcx_attach bound.  The reference subroutines take the bottom model, the type count,
+    ! the method table and grid_size on every call (calc:25-385); the engine takes them once.
+    ! Each per-call subroutine checks its own arguments against these and stops with a named
+    ! error when they differ or when no engine is attached.
+    INTEGER, SAVE :: att_model = -1, att_types = -1, att_grid(3) = -1
+    CHARACTER(len=20), SAVE :: att_methods(0:7, MAX_SURFACE_TYPES)
 
 CONTAINS
 
@@ -49,6 +55,56 @@ CONTAINS
             ERROR STOP 1
         ENDIF
     END SUBROUTINE check
+
+    SUBROUTINE contract_error(where, msg)
+        CHARACTER(len=*), INTENT(IN) :: where, msg
+        WRITE (w_unit, '(4A)') 'flux engine contract violation in ', where, ': ', msg
+        CALL FLUSH(w_unit)
+        ERROR STOP 1
+    END SUBROUTINE contract_error
+
+    ! the per-call subroutine `where` against the attached engine: an engine exists, and
+    ! num_surface_types, grid_size(1:3), my_bottom_model and its method table column are the
+    ! ones fcx_attach bound (flux: FCX_* table id; absent for calls that take no table)
+    SUBROUTINE require(where, num_surface_types, grid_size, my_bottom_model, flux, methods)
+        CHARACTER(len=*),                            INTENT(IN) :: where
+        INTEGER,                                     INTENT(IN) :: num_surface_types
+        INTEGER,           DIMENSION(:),             INTENT(IN) :: grid_size
+        INTEGER,                           OPTIONAL, INTENT(IN) :: my_bottom_model
+        INTEGER(c_int),                    OPTIONAL, INTENT(IN) :: flux
+        CHARACTER(len=20), DIMENSION(:,:), OPTIONAL, INTENT(IN) :: methods
+        CHARACTER(len=256) :: msg
+        INTEGER :: i
+        IF (.NOT. c_associated(engine)) CALL contract_error(where, &
+            'no flux engine attached (call fcx_attach once all fields are allocated, after flux_calculator.F90:761)')
+        IF (num_surface_types /= att_types) THEN
+            WRITE (msg, '(A,I0,A,I0)') 'num_surface_types ', num_surface_types, ' but the engine was attached with ', &
+                att_types
+            CALL contract_error(where, TRIM(msg))
+        ENDIF
+        IF (SIZE(grid_size) < 3) CALL contract_error(where, 'grid_size has fewer than 3 grids')
+        IF (ANY(grid_size(1:3) /= att_grid)) THEN
+            WRITE (msg, '(A,3(1X,I0),A,3(1X,I0))') 'grid_size', grid_size(1:3), ' but the engine was attached with', &
+                att_grid
+            CALL contract_error(where, TRIM(msg))
+        ENDIF
+        IF (PRESENT(my_bottom_model)) THEN
+            IF (my_bottom_model /= att_model) THEN
+                WRITE (msg, '(A,I0,A,I0)') 'my_bottom_model ', my_bottom_model, ' but the engine was attached with ', &
+                    att_model
+                CALL contract_error(where, TRIM(msg))
+            ENDIF
+        ENDIF
+        IF (PRESENT(methods) .AND. PRESENT(flux) .AND. PRESENT(my_bottom_model)) THEN
+            DO i = 1, num_surface_types
+                IF (TRIM(methods(my_bottom_model, i)) /= TRIM(att_methods(flux, i))) THEN
+                    WRITE (msg, '(A,I0,5A)') 'method table differs from the attached one: surface type ', i, &
+                        ' is "', TRIM(methods(my_bottom_model, i)), '", attached "', TRIM(att_methods(flux, i)), '"'
+                    CALL contract_error(where, TRIM(msg))
+                ENDIF
+            ENDDO
+        ENDIF
+    END SUBROUTINE require
 
     SUBROUTINE set_table(flux, methods, my_bottom_model, num_surface_types)
         INTEGER(c_int),                          INTENT(IN) :: flux
@@ -63,6 +119,7 @@ CONTAINS
                 ERROR STOP 1
             ENDIF
             CALL check(fcx_set_method(engine, flux, INT(i, c_int), m), 'fcx_set_method')
+            att_methods(flux, i) = methods(my_bottom_model, i)
         ENDDO
     END SUBROUTINE set_table
 
@@ -96,6 +153,10 @@ CONTAINS
 
         IF (c_associated(engine)) CALL fcx_detach()
         gs = INT(grid_size(1:3), c_int32_t)
+        att_model = my_bottom_model
+        att_types = num_surface_types
+        att_grid = grid_size(1:3)
+        att_methods = ''
         dev = 0
         IF (PRESENT(device)) dev = INT(device, c_int)
         CALL check(fcx_create(dev, INT(num_surface_types, c_int), gs, engine), 'fcx_create')
@@ -193,6 +254,9 @@ CONTAINS
         IF (.NOT. c_associated(engine)) RETURN
         r = fcx_destroy(engine)
         engine = c_null_ptr
+        att_model = -1
+        att_types = -1
+        att_grid = -1
     END SUBROUTINE fcx_detach
 
     !!!!!!!!!! the reference subroutines (flux_calculator_calculate.F90:25-385) !!!!!!!!!!
@@ -204,6 +268,9 @@ CONTAINS
         CHARACTER(len=20),       DIMENSION(:,:),  INTENT(IN)    :: methods
         INTEGER,                 DIMENSION(:),    INTENT(IN)    :: grid_size
         TYPE(local_fields_type), DIMENSION(0:,:), INTENT(INOUT) :: local_field
+        IF (which_grid < 1 .OR. which_grid > 3) CALL contract_error('calc_spec_vapor_surface', 'which_grid outside 1..3')
+        CALL require('calc_spec_vapor_surface', num_surface_types, grid_size, my_bottom_model, &
+                     FCX_SPEC_VAPOR_SURFACE_T + INT(which_grid - 1, c_int), methods)
         CALL check(fcx_calc_spec_vapor_surface(engine, INT(which_grid, c_int)), 'calc_spec_vapor_surface')
     END SUBROUTINE calc_spec_vapor_surface
 
@@ -214,6 +281,7 @@ CONTAINS
         INTEGER,                 DIMENSION(:),    INTENT(IN)    :: grid_size
         TYPE(local_fields_type), DIMENSION(0:,:), INTENT(INOUT) :: local_field
         ! the month of the bias correction comes from current_step_time (basic:125)
+        CALL require('calc_flux_mass_evap', num_surface_types, grid_size, my_bottom_model, FCX_FLUX_MASS_EVAP, methods)
         CALL check(fcx_calc_flux_mass_evap(engine, INT(current_step_time, c_int32_t)), 'calc_flux_mass_evap')
     END SUBROUTINE calc_flux_mass_evap
 
@@ -223,6 +291,8 @@ CONTAINS
         CHARACTER(len=20),       DIMENSION(:,:),  INTENT(IN)    :: methods
         INTEGER,                 DIMENSION(:),    INTENT(IN)    :: grid_size
         TYPE(local_fields_type), DIMENSION(0:,:), INTENT(INOUT) :: local_field
+        CALL require('calc_flux_heat_latent', num_surface_types, grid_size, my_bottom_model, FCX_FLUX_HEAT_LATENT, &
+                     methods)
         CALL check(fcx_calc_flux_heat_latent(engine), 'calc_flux_heat_latent')
     END SUBROUTINE calc_flux_heat_latent
 
@@ -232,6 +302,8 @@ CONTAINS
         CHARACTER(len=20),       DIMENSION(:,:),  INTENT(IN)    :: methods
         INTEGER,                 DIMENSION(:),    INTENT(IN)    :: grid_size
         TYPE(local_fields_type), DIMENSION(0:,:), INTENT(INOUT) :: local_field
+        CALL require('calc_flux_heat_sensible', num_surface_types, grid_size, my_bottom_model, &
+                     FCX_FLUX_HEAT_SENSIBLE, methods)
         CALL check(fcx_calc_flux_heat_sensible(engine), 'calc_flux_heat_sensible')
     END SUBROUTINE calc_flux_heat_sensible
 
@@ -242,6 +314,8 @@ CONTAINS
         CHARACTER(len=20),       DIMENSION(:,:),  INTENT(IN)    :: methods
         INTEGER,                 DIMENSION(:),    INTENT(IN)    :: grid_size
         TYPE(local_fields_type), DIMENSION(0:,:), INTENT(INOUT) :: local_field
+        CALL require('calc_flux_momentum_east', num_surface_types, grid_size, my_bottom_model, FCX_FLUX_MOMENTUM, &
+                     methods)
         CALL check(fcx_calc_flux_momentum_east(engine, INT(which_grid, c_int)), 'calc_flux_momentum_east')
     END SUBROUTINE calc_flux_momentum_east
 
@@ -252,6 +326,8 @@ CONTAINS
         CHARACTER(len=20),       DIMENSION(:,:),  INTENT(IN)    :: methods
         INTEGER,                 DIMENSION(:),    INTENT(IN)    :: grid_size
         TYPE(local_fields_type), DIMENSION(0:,:), INTENT(INOUT) :: local_field
+        CALL require('calc_flux_momentum_north', num_surface_types, grid_size, my_bottom_model, FCX_FLUX_MOMENTUM, &
+                     methods)
         CALL check(fcx_calc_flux_momentum_north(engine, INT(which_grid, c_int)), 'calc_flux_momentum_north')
     END SUBROUTINE calc_flux_momentum_north
 
@@ -261,6 +337,8 @@ CONTAINS
         CHARACTER(len=20),       DIMENSION(:,:),  INTENT(IN)    :: methods
         INTEGER,                 DIMENSION(:),    INTENT(IN)    :: grid_size
         TYPE(local_fields_type), DIMENSION(0:,:), INTENT(INOUT) :: local_field
+        CALL require('calc_flux_radiation_blackbody', num_surface_types, grid_size, my_bottom_model, &
+                     FCX_FLUX_RADIATION_BLACKBODY, methods)
         CALL check(fcx_calc_flux_radiation_blackbody(engine), 'calc_flux_radiation_blackbody')
     END SUBROUTINE calc_flux_radiation_blackbody
 
@@ -269,6 +347,7 @@ CONTAINS
         INTEGER,                                  INTENT(IN)    :: num_surface_types
         INTEGER,                 DIMENSION(:),    INTENT(IN)    :: grid_size
         TYPE(local_fields_type), DIMENSION(0:,:), INTENT(INOUT) :: local_field
+        CALL require('distribute_shortwave_radiation_flux', num_surface_types, grid_size, my_bottom_model)
         CALL check(fcx_distribute_shortwave_radiation_flux(engine), 'distribute_shortwave_radiation_flux')
     END SUBROUTINE distribute_shortwave_radiation_flux
 
@@ -278,6 +357,7 @@ CONTAINS
         INTEGER,                                  INTENT(IN)    :: num_surface_types
         INTEGER,                 DIMENSION(:),    INTENT(IN)    :: grid_size
         TYPE(local_fields_type), DIMENSION(0:,:), INTENT(INOUT) :: local_field
+        CALL require('average_across_surface_types', num_surface_types, grid_size)
         CALL check(fcx_average_across_surface_types(engine, INT(which_grid, c_int), INT(my_idx, c_int)), &
                    'average_across_surface_types')
     END SUBROUTINE average_across_surface_types

@@ -181,7 +181,7 @@ class Engine:
     OPTIONS = {"cells_per_thread": 1, "max_blocks": 2, "nontemporal": 3, "specialize": 4,
                "atmos_in_run": 5, "pipeline_chunks": 7, "pipeline_min_chunk": 8, "zero_copy": 9,
                "timing": 10, "tiled_layout": 11, "remap_pack": 13, "host_staging": 15, "host_threads": 16,
-               "atmos_halo": 17}
+               "atmos_halo": 17, "deferred_scatter": 18}
 
     def run_atmos(self, phase=PHASE_ALL):
         _lib.check(self.lib.fcx_run_atmos(self.h, phase))

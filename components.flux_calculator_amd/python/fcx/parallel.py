@@ -92,22 +92,54 @@ class LocalAtmos:
     n_boundaries: int
 
 
-def local_atmos(amap: AtmosMap, rank, nranks, offset=None, size=None, right_slot=None):
+def boundary_slots(ranges, index_at):
+    """Every rank's (left, right) boundary slots for contiguous exchange ranges in rank order.
+
+    ranges: every rank's (offset, size); index_at(x): global atmosphere cell of exchange cell
+    x.  Boundary m - 1 is the one just before rank m's cells (an empty rank has no boundary
+    of its own: the next rank with cells numbers it).  All ranks that hold part of one
+    atmosphere cell use ONE slot, that of the first rank boundary inside the cell, so a rank
+    whose cells all lie in an atmosphere cell shared with both neighbours gets left == right
+    and the one all-reduce sums the cell over three or more ranks."""
+    left, right = [-1] * len(ranges), [-1] * len(ranges)
+    prev, a0s, a1s = None, {}, {}
+    for k, (off, size) in enumerate(ranges):
+        if size == 0:
+            continue
+        a0, a1 = int(index_at(off)), int(index_at(off + size - 1))
+        if prev is not None and a1s[prev] == a0:  # the boundary before rank k cuts a cell
+            chained = left[prev] >= 0 and a0s[prev] == a1s[prev]  # the cell began before prev
+            slot = left[prev] if chained else k - 1
+            right[prev] = left[k] = slot
+        a0s[k], a1s[k] = a0, a1
+        prev = k
+    return list(zip(left, right))
+
+
+def local_atmos(amap: AtmosMap, rank, nranks, offset=None, size=None, right_slot=None, ranges=None):
     """right_slot: the slot of the boundary after this rank's cells (default `rank`; with
-    empty ranks in between, task_ranges gives it)."""
-    if offset is None:
-        offset, size = apple_range(amap.atmos_index.shape[0], rank, nranks)
+    empty ranks in between, task_ranges gives it).  ranges: every rank's (offset, size); with
+    them (or with APPLE ranges, offset None) the slots come from boundary_slots, which also
+    serves a rank inside one atmosphere cell shared with both neighbours."""
+    n_global = amap.atmos_index.shape[0]
+    if ranges is None and offset is None:
+        ranges = [apple_range(n_global, r, nranks) for r in range(nranks)]
+    if ranges is not None:
+        offset, size = ranges[rank]
     gi = amap.atmos_index[offset: offset + size]
     if size == 0:
         return LocalAtmos(offset, 0, 0, 0, np.zeros(0, np.int32), np.zeros(0), -1, -1, max(nranks - 1, 0))
     a0, a1 = int(gi[0]), int(gi[-1])
-    left = rank - 1 if (offset > 0 and amap.atmos_index[offset - 1] == a0) else -1
-    end = offset + size
-    right_slot = rank if right_slot is None else right_slot
-    right = right_slot if (end < amap.atmos_index.shape[0] and amap.atmos_index[end] == a1) else -1
-    if left >= 0 and right >= 0 and a0 == a1:
-        raise ValueError(f"rank {rank}: its {size} cells lie inside one atmosphere cell shared "
-                         "with both neighbours (shard smaller than an atmosphere cell)")
+    if ranges is not None:
+        left, right = boundary_slots(ranges, lambda x: amap.atmos_index[x])[rank]
+    else:
+        left = rank - 1 if (offset > 0 and amap.atmos_index[offset - 1] == a0) else -1
+        end = offset + size
+        right_slot = rank if right_slot is None else right_slot
+        right = right_slot if (end < n_global and amap.atmos_index[end] == a1) else -1
+        if left >= 0 and right >= 0 and a0 == a1:
+            raise ValueError(f"rank {rank}: its {size} cells lie inside one atmosphere cell shared "
+                             "with both neighbours: pass every rank's ranges to give it one slot")
     return LocalAtmos(offset, size, a0, a1 - a0 + 1, np.ascontiguousarray(gi - a0, dtype=np.int32),
                       np.ascontiguousarray(amap.weight[offset: offset + size]), left, right,
                       max(nranks - 1, 0))
@@ -168,18 +200,22 @@ class PeriodicAtmosMap:
             tot += np.where((k < length) & (y < n_global), self.area(y), 0.0)
         return self.area(x) / tot
 
-    def local(self, offset, size, rank, nranks, n_global, right_slot=None):
+    def local(self, offset, size, rank, nranks, n_global, right_slot=None, ranges=None):
         """right_slot: the boundary slot after this rank's cells (default `rank`; with empty
-        ranks in the decomposition, the next rank with cells minus one, as task_ranges)."""
+        ranks in the decomposition, the next rank with cells minus one, as task_ranges).
+        ranges: every rank's (offset, size): slots from boundary_slots."""
         right_slot = rank if right_slot is None else right_slot
         x = np.arange(offset, offset + size, dtype=np.int64)
         gi = self.index(x)
         if size == 0:
             return LocalAtmos(offset, 0, 0, 0, np.zeros(0, np.int32), np.zeros(0), -1, -1, max(nranks - 1, 0))
         a0, a1 = int(gi[0]), int(gi[-1])
-        left = rank - 1 if (offset > 0 and int(self.index(offset - 1)) == a0) else -1
-        end = offset + size
-        right = right_slot if (end < n_global and int(self.index(end)) == a1) else -1
+        if ranges is not None:
+            left, right = boundary_slots(ranges, lambda c: int(self.index(c)))[rank]
+        else:
+            left = rank - 1 if (offset > 0 and int(self.index(offset - 1)) == a0) else -1
+            end = offset + size
+            right = right_slot if (end < n_global and int(self.index(end)) == a1) else -1
         return LocalAtmos(offset, size, a0, a1 - a0 + 1, np.ascontiguousarray(gi - a0, dtype=np.int32),
                           np.ascontiguousarray(self.weight(x, n_global)), left, right, max(nranks - 1, 0))
 
@@ -226,8 +262,8 @@ class BlockedRandomAtmosMap:
         s = lo - b0 * self.BLOCK
         return idx[s: s + (hi - lo)], w[s: s + (hi - lo)]
 
-    def local(self, offset, size, rank, nranks, n_global, right_slot=None):
-        """right_slot: as PeriodicAtmosMap.local."""
+    def local(self, offset, size, rank, nranks, n_global, right_slot=None, ranges=None):
+        """right_slot, ranges: as PeriodicAtmosMap.local."""
         right_slot = rank if right_slot is None else right_slot
         if size == 0:
             return LocalAtmos(offset, 0, 0, 0, np.zeros(0, np.int32), np.zeros(0), -1, -1, max(nranks - 1, 0))
@@ -236,8 +272,11 @@ class BlockedRandomAtmosMap:
         mine = slice(offset - lo, offset - lo + size)
         g, wm = gi[mine], w[mine]
         a0, a1 = int(g[0]), int(g[-1])
-        left = rank - 1 if (offset > 0 and int(gi[0]) == a0) else -1
-        right = right_slot if (offset + size < n_global and int(gi[-1]) == a1) else -1
+        if ranges is not None:
+            left, right = boundary_slots(ranges, lambda c: int(self._cells(c, c + 1, n_global)[0][0]))[rank]
+        else:
+            left = rank - 1 if (offset > 0 and int(gi[0]) == a0) else -1
+            right = right_slot if (offset + size < n_global and int(gi[-1]) == a1) else -1
         return LocalAtmos(offset, size, a0, a1 - a0 + 1, np.ascontiguousarray(g - a0, dtype=np.int32),
                           np.ascontiguousarray(wm), left, right, max(nranks - 1, 0))
 

@@ -57,10 +57,10 @@ class Workload:
         # segments cross wave tiles as on a real intersection grid
         if not atmos:
             self.la = None
-        elif atmos_map == "random":
-            self.la = BlockedRandomAtmosMap().local(self.offset, self.n, self.rank, self.world, self.n_global)
         else:
-            self.la = PeriodicAtmosMap().local(self.offset, self.n, self.rank, self.world, self.n_global)
+            ranges = [apple_range(self.n_global, r, self.world) for r in range(self.world)]
+            amap = BlockedRandomAtmosMap() if atmos_map == "random" else PeriodicAtmosMap()
+            self.la = amap.local(self.offset, self.n, self.rank, self.world, self.n_global, ranges=ranges)
         self.atmos_map = atmos_map
         nb, stride = max(self.world - 1, 0), len(ATM_FIELDS)
         self.n_boundaries, self.stride = nb, stride

@@ -133,8 +133,9 @@ int fcx_download(fcx_engine *e, int phase); /* D2H of host-bound outputs of the 
 /* the three above; with host-bound fields pipelined over cell chunks (FCX_OPT_PIPELINE_CHUNKS) */
 int fcx_step(fcx_engine *e, int phase, int32_t current_step_time);
 /* waits for the engine's stream; the caller's host arrays hold the downloaded outputs once it
- * returns (caller heap arrays are filled from the engine's staging arena here,
- * FCX_OPT_HOST_STAGING).  fcx_step and the per-call subroutines end with it. */
+ * returns.  fcx_download fills caller heap arrays itself (it waits for the stream); with
+ * FCX_OPT_DEFERRED_SCATTER they are filled from the staging arena here.  fcx_step and the
+ * per-call subroutines end with it. */
 int fcx_synchronize(fcx_engine *e);
 
 /* ---- per call: the reference subroutines one by one (exact drop-in semantics; each
@@ -161,8 +162,15 @@ int fcx_device_layout(fcx_engine *e, int64_t *tile, int64_t *tile_stride);
 /* device time (hipEvents on the engine stream) of the kernels of the last fcx_run;
    needs FCX_OPT_TIMING = 1 */
 int fcx_last_kernel_ms(fcx_engine *e, float *ms);
-/* bytes of the engine's page-locked staging arena for caller heap arrays (0: none) */
+/* bytes of the engine's page-locked staging arena for caller heap arrays (0: none): one host
+ * image per device pool that holds a heap array's mirror, allocated at fcx_commit (the
+ * pinned footprint: ~the mirrors' size, e.g. 2.2-2.6 GB per 10M-cell CCLM engine).  A pool
+ * whose image cannot be page-locked takes the direct path instead and is not counted. */
 int fcx_staging_bytes(fcx_engine *e, int64_t *bytes);
+/* retired in version 3, kept for one release: always 0 (nothing of the caller's memory is
+ * page-locked; the in-launch carry hand-off is gone) */
+int fcx_pinned_bytes(fcx_engine *e, int64_t *bytes);
+int fcx_handoff_recoveries(fcx_engine *e, int64_t *count);
 /* bytes of host arrays the kernels use in place (FCX_OPT_ZERO_COPY) */
 int fcx_zero_copy_bytes(fcx_engine *e, int64_t *bytes);
 /* algorithmic HBM bytes of one fcx_run(phase) (each distinct array read once, written once) */
@@ -185,7 +193,11 @@ int fcx_add_atmos_field(fcx_engine *e, int phase, int surface_type, int grid, in
  * rank's first local atmosphere cell is boundary `left` (-1: not shared), its last one
  * boundary `right`; field f of the accumulation uses column f (f < stride).  Boundary m - 1
  * is the one just before rank m's cells: left = rank - 1, right = (next rank with cells) - 1
- * (a rank with an empty task, io:101-104, sits between two slots' owners without one) */
+ * (a rank with an empty task, io:101-104, sits between two slots' owners without one).
+ * Every rank that holds part of one atmosphere cell uses ONE slot for it, the slot of the
+ * first rank boundary inside the cell: a rank whose cells all lie in one atmosphere cell
+ * shared with both neighbours has left == right (fcx.parallel.boundary_slots).  The slots
+ * are written, never added to, so left == right is safe. */
 int fcx_set_atmos_shared(fcx_engine *e, double *shared, int32_t n_boundaries, int32_t stride,
                          int32_t left, int32_t right);
 /* instead of fcx_set_atmos_shared: the engine allocates the [n_boundaries][fields] slots
@@ -216,11 +228,17 @@ int fcx_comm_allreduce_sum(fcx_comm *c, double *buf, size_t count, void *hip_str
  * boundary slots themselves (all-reduce on the engine's stream, then fcx_atmos_finish);
  * every rank's engine must then run the same steps.  NULL detaches. */
 int fcx_set_comm(fcx_engine *e, fcx_comm *c);
-/* several engines of this rank (e.g. one per bottom-model variant) in ONE all-reduce: the
- * slots of engines whose regions are adjacent in one buffer go in one call (else one call
- * per engine inside one RCCL group), on the first engine's stream; then fcx_atmos_finish of
- * each.  Call after their accumulation (fcx_run, or fcx_run_atmos); engines already
- * completed in this run (fcx_set_comm) are skipped. */
+/* several engines of this rank (e.g. one per bottom-model variant) in ONE all-reduce of
+ * sum(n_boundaries * stride) doubles over their slots in list order, on the first engine's
+ * stream, then fcx_atmos_finish of each.  Regions that follow each other in list order in
+ * one buffer are reduced in place, others through the communicator's scratch; the collective
+ * is the same either way.  Call after their accumulation (fcx_run, or fcx_run_atmos).
+ * Collective contract: every rank passes its engines in the same order with the same
+ * n_boundaries and strides.  The first exchange of each such signature checks it with a
+ * blocking max-all-reduce, and ranks that disagree all return FCX_E_ARG.  An engine already
+ * completed in this run (fcx_set_comm) takes part with zeros and is skipped; one with no
+ * accumulation since its last exchange takes part with zeros and the call returns
+ * FCX_E_STATE after the collective, so no rank is left waiting. */
 int fcx_atmos_allreduce(fcx_comm *c, fcx_engine *const *engines, int n_engines);
 
 /* ---- exchange-grid -> model remaps ----
@@ -273,7 +291,18 @@ enum fcx_option {
                                    mapped.  Applied at fcx_commit                          */
   FCX_OPT_HOST_THREADS = 16,    /* host threads of those copies (the calling thread
                                    included); 0 (default): min(16, OMP_NUM_THREADS if set,
-                                   else the CPUs of the process affinity set)              */
+                                   else the CPUs of the process affinity set -- divided by
+                                   the node's local rank count when the rank is not pinned
+                                   (OMPI_COMM_WORLD_LOCAL_SIZE, MPI_LOCALNRANKS,
+                                   SLURM_NTASKS_PER_NODE or LOCAL_WORLD_SIZE)).  Under MPI,
+                                   pin ranks or set this to each rank's core share        */
+  FCX_OPT_DEFERRED_SCATTER = 18, /* staged downloads: 0 (default) fcx_download waits for the
+                                   stream and fills the caller's heap arrays before it
+                                   returns; 1: the host copies wait for the next
+                                   fcx_synchronize (a host that overlaps engines)         */
+  FCX_OPT_RETIRED_PIN_HOST = 6, /* retired options (version 3): accepted and ignored      */
+  FCX_OPT_RETIRED_12 = 12,
+  FCX_OPT_RETIRED_CARRY_HANDOFF = 14,
   FCX_OPT_ATMOS_HALO = 17,      /* fused accumulation of one surface type, launched over the
                                    whole grid, on a map whose segments are at most 9 cells:
                                    1 (default) halo tiles -- each wave also computes the

@@ -8,7 +8,7 @@
 ! No regridding matrices are set, so the reference's do_regridding calls between the
 ! calc_* calls would be no-ops and are left out.
 !
-!   dropin_host <dir> percall|fused
+!   dropin_host <dir> percall|fused|noattach|badtable|badgrid|badtypes
 !
 ! <dir>/manifest.txt (written by tests/test_fortran.py), one record per line:
 !   N nbufs T nt nu nv          buffer count, surface types, grid sizes
@@ -98,6 +98,11 @@ PROGRAM dropin_host
     ENDDO
     CLOSE (u)
 
+    ! contract checks of the per-call subroutines (no GPU work reaches the engine):
+    ! the reference host loop without fcx_attach, and calls whose arguments differ from the
+    ! attached ones -- each must stop with a named error
+    IF (TRIM(mode) == 'noattach') CALL calc_flux_mass_evap(1, nsurf, tables(:,:,4), grid_size, local_field)
+
     ! after flux_calculator.F90:761: every allocation and alias is final
     IF (lcorr) THEN
         CALL fcx_attach(1, nsurf, grid_size, local_field, tables(:,:,1), tables(:,:,2), tables(:,:,3),   &
@@ -107,6 +112,19 @@ PROGRAM dropin_host
         CALL fcx_attach(1, nsurf, grid_size, local_field, tables(:,:,1), tables(:,:,2), tables(:,:,3),   &
                         tables(:,:,4), tables(:,:,5), tables(:,:,6), tables(:,:,7), tables(:,:,8),    &
                         lcorr, init_date)
+    ENDIF
+
+    IF (TRIM(mode) == 'badtable') THEN
+        IF (TRIM(tables(1, 1, 4)) == 'CCLM') THEN
+            tables(1, 1, 4) = 'MOM5'
+        ELSE
+            tables(1, 1, 4) = 'CCLM'
+        ENDIF
+        CALL calc_flux_mass_evap(1, nsurf, tables(:,:,4), grid_size, local_field)
+    ELSE IF (TRIM(mode) == 'badgrid') THEN
+        CALL calc_flux_heat_latent(1, nsurf, tables(:,:,5), grid_size + [1, 0, 0], local_field)
+    ELSE IF (TRIM(mode) == 'badtypes') THEN
+        CALL average_across_surface_types(1, 22, nsurf + 1, grid_size, local_field)
     ENDIF
 
     IF (TRIM(mode) == 'fused') THEN

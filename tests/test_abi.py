@@ -158,9 +158,10 @@ def test_set_precision_validates():
 
 def test_remap_and_staging_options_before_commit():
     """FCX_OPT_REMAP_PACK (13: 0 never, 1 always, 2 auto), FCX_OPT_HOST_STAGING (15) and
-    FCX_OPT_HOST_THREADS (16: 0..64) are validated without a GPU; the options removed in
-    round 3 (6 page-locking of caller memory, 12/14 the in-launch carry hand-off) are
-    unknown; fcx_remap_info is only answered after fcx_commit."""
+    FCX_OPT_HOST_THREADS (16: 0..64) are validated without a GPU; the options retired in
+    version 3 (6 page-locking of caller memory, 12/14 the in-launch carry hand-off) are
+    accepted and ignored, and their query functions answer 0, so hosts that used them still
+    run; an unknown option is rejected; fcx_remap_info is only answered after fcx_commit."""
     lib = _lib.load()
     h = ctypes.c_void_p()
     gs = (ctypes.c_int32 * 3)(16, 16, 16)
@@ -175,7 +176,17 @@ def test_remap_and_staging_options_before_commit():
     assert lib.fcx_set_option(h, 16, 65) == 1
     assert lib.fcx_set_option(h, 16, -1) == 1
     for gone in (6, 12, 14):
-        assert lib.fcx_set_option(h, gone, 1) == 1
+        _lib.check(lib.fcx_set_option(h, gone, 1))
+        _lib.check(lib.fcx_set_option(h, gone, 0))
+    assert lib.fcx_set_option(h, 19, 1) == 1  # FCX_E_ARG: unknown
+    for v in (0, 1):
+        _lib.check(lib.fcx_set_option(h, 18, v))  # FCX_OPT_DEFERRED_SCATTER
+    b = ctypes.c_int64(7)
+    _lib.check(lib.fcx_pinned_bytes(h, ctypes.byref(b)))
+    assert b.value == 0
+    b.value = 7
+    _lib.check(lib.fcx_handoff_recoveries(h, ctypes.byref(b)))
+    assert b.value == 0
     src = np.arange(16, dtype=np.int32)
     dst = src % 4
     w = np.ones(16)
@@ -186,3 +197,38 @@ def test_remap_and_staging_options_before_commit():
     assert lib.fcx_add_remap(h, 4, 1, src.ctypes.data, (dst + 4).ctypes.data, w.ctypes.data,
                              ctypes.byref(rid)) == 1  # a link outside the target grid
     lib.fcx_destroy(h)
+
+
+def test_mock_rccl_stand_in_exports_the_entry_points_libfcx_binds():
+    """The test-only librccl stand-in (tests/cpp/mock_rccl.cpp, FCX_RCCL_LIBRARY) that runs
+    libfcx's N > 1 exchange with several ranks on one GPU: built by build(), and it exports
+    every nccl* entry point libfcx resolves (fcx_engine.hip, rccl())."""
+    path = os.path.join(ROOT, "components.flux_calculator_amd", "lib", "test", "libmock_rccl.so")
+    assert os.path.exists(path), "make -C components.flux_calculator_amd mock-rccl"
+    lib = ctypes.CDLL(path)
+    for s in ("ncclGetUniqueId", "ncclCommInitRank", "ncclCommDestroy", "ncclAllReduce", "ncclGetErrorString"):
+        assert hasattr(lib, s), s
+    uid = (ctypes.c_char * 128)()
+    assert lib.ncclGetUniqueId(uid) == 0 and bytes(uid).startswith(b"/fcxmock-")
+
+
+def test_one_cell_shared_on_both_sides_takes_one_slot():
+    """A rank whose only atmosphere cell is shared with both neighbours uses the one slot of
+    the cell (left == right, fcx.parallel.boundary_slots); two different slots are rejected
+    with a named error before any collective."""
+    case = build_case("CCLM", n=3, T=1)
+    lib = _lib.load()
+    idx = np.zeros(3, np.int32)
+    w = np.full(3, 1.0 / 3)
+    for left, right, ok in ((0, 0, True), (0, 1, False), (1, -1, True)):
+        h = ctypes.c_void_p()
+        gs = (ctypes.c_int32 * 3)(*case.lf.grid_size)
+        _lib.check(lib.fcx_create(0, 1, gs, ctypes.byref(h)))
+        try:
+            _lib.check(lib.fcx_set_atmos_map(h, 1, ctypes.c_void_p(idx.ctypes.data), ctypes.c_void_p(w.ctypes.data)))
+            rc = lib.fcx_set_atmos_shared(h, ctypes.c_void_p(16), 2, 6, left, right)
+            assert (rc == 0) == ok, (left, right, rc)
+            if not ok:
+                assert b"one boundary slot" in lib.fcx_last_error()
+        finally:
+            lib.fcx_destroy(h)

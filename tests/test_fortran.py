@@ -100,3 +100,27 @@ def test_dropin_module_in_a_fortran_host(tmp_path, mode, variant, T):
     assert "DROPIN_HOST OK" in r.stdout, r.stdout
     got = {key: np.fromfile(os.path.join(tmp_path, f"o{i}.bin"), dtype=np.float64) for i, key in enumerate(outs)}
     assert_parity(got, {k: ref[k] for k in outs}, label=f"{variant} T={T} {mode}")
+
+
+@pytest.mark.skipif(not os.path.exists(DROPIN), reason="Fortran drop-in host not built")
+@pytest.mark.parametrize("mode,message", [
+    ("noattach", "no flux engine attached"),
+    ("badtable", "method table differs from the attached one: surface type 1"),
+    ("badgrid", "grid_size"),
+    ("badtypes", "num_surface_types 3 but the engine was attached with 2"),
+])
+def test_dropin_per_call_checks_its_arguments(tmp_path, mode, message):
+    """The reference subroutines take my_bottom_model, num_surface_types, the method table and
+    grid_size on every call (calc:25-385; called at flux_calculator.F90:902, 972-991).  The
+    drop-in checks them against what fcx_attach bound and stops with a named error --
+    the reference host loop without fcx_attach, a different method table, a different
+    grid_size, a different type count.  Host-side only: no GPU work is reached."""
+    from fcx.synthetic import build_case
+
+    case = build_case("CCLM", n=257, T=2, bias=False)
+    write_manifest(case, str(tmp_path), 3600)
+    r = subprocess.run([DROPIN, str(tmp_path), mode], capture_output=True, text=True, timeout=120)
+    out = r.stdout + r.stderr
+    assert r.returncode != 0, out
+    assert "flux engine contract violation" in out and message in out, out
+    assert "DROPIN_HOST OK" not in out

@@ -309,3 +309,48 @@ def test_pipeline_multi_type_register_averages_and_fused_accumulation():
         g = 2 if name == "UMOM" else 1
         want = oracle_lib.atmos_accumulate(amap.atmos_index, amap.weight, res[0][(0, g, name)], amap.n_atmos)
         np.testing.assert_array_equal(res[0][("atm", name)], want, err_msg=name)
+
+
+@pytest.mark.parametrize("n", [32_768, 600_001])
+def test_download_fills_heap_arrays_without_synchronize(n):
+    """fcx_download through the staging arena fills the caller's heap arrays before it
+    returns: a host that waits with a device-wide sync of its own (torch.cuda.synchronize),
+    never calling fcx_synchronize, reads the outputs.  With FCX_OPT_DEFERRED_SCATTER they
+    arrive at fcx_synchronize instead."""
+    import torch
+
+    case = build_case("MOM5", n=n, T=1, bias=True)
+    ref = oracle_lib.run_case(case, "c", current_step_time=STEP_T)
+    for deferred in (0, 1):
+        for k in case.outputs:
+            case.lf.field[k][:] = np.nan
+        eng = Engine(case.lf, 1, case.methods, corrections=case.corrections,
+                     options={"deferred_scatter": deferred})
+        assert eng.staging_bytes() > 0 or eng.zero_copy_active()
+        eng.upload(PHASE_ALL)
+        eng.run(PHASE_ALL, STEP_T)
+        eng.download(PHASE_ALL)
+        torch.cuda.synchronize()
+        got = {k: np.array(case.lf.field[k], copy=True) for k in case.outputs}
+        if deferred:
+            assert all(np.isnan(v).all() for v in got.values())  # still in the arena
+            eng.synchronize()
+            got = {k: np.array(case.lf.field[k], copy=True) for k in case.outputs}
+        eng.close()
+        assert_parity(got, {k: ref[k] for k in case.outputs}, label=f"n={n} deferred={deferred}")
+
+
+def test_staging_arena_failure_falls_back_to_direct_copies(monkeypatch):
+    """A node that cannot page-lock the staging arena (FCX_TEST_PIN_FAIL=1 makes every image
+    fail at fcx_commit): the pools fall back to one runtime copy per array, the step runs,
+    no pinned bytes are reported, and the outputs are the bits of the staged step."""
+    case = build_case("CCLM", n=600_001, T=2, bias=True)
+    opts = {"pipeline_chunks": 4, "pipeline_min_chunk": 65_536, "zero_copy": 0}
+    want = run(case, opts, atmos_n=600_001)
+    monkeypatch.setenv("FCX_TEST_PIN_FAIL", "1")
+    got = run(case, opts, atmos_n=600_001)
+    same_bits(got, want)
+    eng = Engine(case.lf, case.num_surface_types, case.methods, corrections=case.corrections,
+                 averages=case.averages, options=opts)
+    assert eng.staging_bytes() == 0
+    eng.close()

@@ -9,8 +9,8 @@ import numpy as np
 import pytest
 
 import oracle_lib
-from fcx.parallel import (apple_range, local_atmos, pack_boundaries, synthetic_atmos_map, task_ranges,
-                          task_range, unpack_boundaries)
+from fcx.parallel import (apple_range, boundary_slots, local_atmos, pack_boundaries, synthetic_atmos_map,
+                          task_ranges, task_range, unpack_boundaries)
 from fcx.synthetic import build_case
 from parity import assert_parity, mixed_error
 
@@ -67,6 +67,53 @@ def test_structured_maps_take_the_task_slot_rule(mapcls):
     r2 = mk.local(12_007, 9_001, 2, 4, n, right_slot=2)
     if r0.right >= 0:
         assert r0.right == r2.left == 1
+
+
+def test_boundary_slots_rules():
+    """boundary_slots: slot m - 1 before rank m's cells; an empty rank has none; every rank
+    holding part of one atmosphere cell uses the slot of the first boundary inside it."""
+    idx = np.array([0, 0, 1, 1, 1, 1, 1, 1, 2, 2, 3, 3])  # cell 1 spans 6 exchange cells
+    at = lambda x: idx[x]  # noqa: E731
+    # APPLE-like: cuts at 3, 5, 7 all inside cell 1: ranks 1 and 2 lie inside it
+    assert boundary_slots([(0, 3), (3, 2), (5, 2), (7, 5)], at) == [(-1, 0), (0, 0), (0, 0), (0, -1)]
+    # a cut between two cells shares nothing
+    assert boundary_slots([(0, 2), (2, 10)], at) == [(-1, -1), (-1, -1)]
+    # an empty rank between two ranks that share cell 1: the slot of the next rank with cells
+    assert boundary_slots([(0, 4), (0, 0), (4, 8)], at) == [(-1, 1), (-1, -1), (1, -1)]
+    # a rank inside cell 1 after an empty rank
+    assert boundary_slots([(0, 3), (0, 0), (3, 2), (5, 7)], at) == [(-1, 1), (-1, -1), (1, 1), (1, -1)]
+    # the task_ranges rule for every rank with cells is the same
+    t = np.array([0, 0, 2, 2, 2, 4], np.int32)
+    tr = task_ranges(t, 6)
+    got = boundary_slots([(o, s) for o, s, _ in tr], lambda x: np.array([0, 1, 1, 2, 3, 3])[x])
+    assert got[0] == (-1, 1) and got[2] == (1, 3) and got[4] == (3, -1)
+
+
+@pytest.mark.parametrize("cuts", [(1, 2, 3), (1, 3), (1, 2, 3, 4), (2, 4, 7)])
+def test_one_atmosphere_cell_over_several_ranks(cuts):
+    """A cell spread over three or more ranks: each rank writes its partial sum into the one
+    slot (left == right for the ranks inside it), the slot sum over all ranks completes the
+    cell for every one of them (what fcx_atmos_allreduce does on the device)."""
+    amap = synthetic_atmos_map(64)
+    first = int(np.flatnonzero(np.bincount(amap.atmos_index) >= 5)[0])
+    c0 = int(np.searchsorted(amap.atmos_index, first))
+    bounds = [0] + [c0 + c for c in cuts if c0 + c < 64] + [64]
+    ranges = [(a, b - a) for a, b in zip(bounds[:-1], bounds[1:])]
+    p = len(ranges)
+    x = np.random.default_rng(3).normal(size=64)
+    want = oracle_lib.atmos_accumulate(amap.atmos_index, amap.weight, x, amap.n_atmos)
+    views = [local_atmos(amap, r, p, ranges=ranges) for r in range(p)]
+    total = np.zeros((p - 1, 1))
+    parts = []
+    for la in views:
+        part = oracle_lib.atmos_accumulate(la.atmos_index, la.weight, x[la.offset: la.offset + la.size], la.n_atmos)
+        parts.append(part)
+        total += pack_boundaries(la, [part], 1)
+    for la, part in zip(views, parts):
+        unpack_boundaries(la, total, [part])
+        np.testing.assert_allclose(part, want[la.atmos_offset: la.atmos_offset + la.n_atmos], rtol=1e-13)
+    inside = [la for la in views if la.n_atmos == 1 and la.left >= 0 and la.right >= 0]
+    assert inside and all(la.left == la.right for la in inside)
 
 
 def test_synthetic_map_is_conservative_and_sorted():
