@@ -15,12 +15,14 @@ by neighbouring ranks (libfcx's RCCL communicator), once per step.
 Also reported:
   roofline      algorithmic bytes of the dominant kernel / its mean HIP-event duration in
                 the timed steps (one event pair per step, around that kernel only)
-  cpu_baseline  the CPU oracle on a bounded sample of the same workload (rank 0, N=1 only):
-                "reference" = the reference flux_lib compiled from source (oracle/_ref),
-                "port" = the C restatement (oracle/fco.c)
+  cpu_baseline  the reference path on this box's host cores (rank 0, N=1 only; cpu_legs.py):
+                the reference flux_lib compiled from source (oracle/_ref, kind "reference";
+                the C restatement oracle/fco.c, kind "port", where it was not built) on one
+                core and on the box's CPU share as APPLE-range ranks, at 32,768 cells
+                (configs 1/2) and at this workload's size, on the same inputs
+  baltic_size   the drop-in from host arrays (e2e) against those host cores at 32,768 cells
 """
 import argparse
-import ctypes
 import json
 import os
 import sys
@@ -53,9 +55,8 @@ def parse():
     p.add_argument("--variants", default=",".join(VARIANTS))
     p.add_argument("--types", type=int, default=1, help="surface types")
     p.add_argument("--bias", action="store_true", help="monthly evaporation bias corrections")
-    p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget")
-    p.add_argument("--cpu-cells", type=int, default=1_000_000)
-    p.add_argument("--cpu-cells-mt", type=int, default=4_000_000, help="all-cores CPU sample")
+    p.add_argument("--cpu-seconds", type=float, default=3.0,
+                   help="CPU baselines: seconds per leg (1 core and all cores, at 32,768 cells and --cells)")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--e2e", type=int, default=1,
                    help="N=1: also time the end-to-end host-array step at 10M and 32,768 cells (an 'e2e' "
@@ -94,37 +95,6 @@ def parse():
     return p.parse_args()
 
 
-def cpu_baseline(args, variants):
-    """Oracle timing on the host cores, single thread, bounded sample of the same workload."""
-    import oracle_lib
-    from fcx.synthetic import build_case, inputs_for_bench
-
-    kind = "reference" if oracle_lib.load("ref") is not None else "port"
-    n = args.cpu_cells
-    data = inputs_for_bench(n)
-    cases = [build_case(v, n=n, T=args.types, bias=args.bias, data=data if args.types == 1 else None)
-             for v in variants]
-    states = [oracle_lib.OracleState(c, 0) for c in cases]
-    lib_kind = "ref" if kind == "reference" else "c"
-    cells, t0, reps = 0, time.perf_counter(), 0
-    while True:
-        for st in states:
-            oracle_lib.run_state(st, lib_kind)
-            cells += n
-        reps += 1
-        el = time.perf_counter() - t0
-        if el >= args.cpu_seconds and reps >= 2:
-            break
-    return {
-        "value": cells / el / 1e6,
-        "unit": "Mcells/s",
-        "cores": 1,
-        "kind": kind,
-        "sample": f"{reps} coupling steps x {len(variants)} variants ({'+'.join(variants)}) over "
-                  f"{n} cells, T={args.types}, reference call order, {el:.1f} s on 1 thread",
-    }
-
-
 def host_cpu():
     """lscpu-style model name and the CPUs this process may use (SURVEY.md 8d CPU timing)."""
     model = "unknown"
@@ -136,44 +106,6 @@ def host_cpu():
     except OSError:
         pass
     return {"model": model, "nproc": len(os.sched_getaffinity(0)), "machine_cpus": os.cpu_count()}
-
-
-def cpu_all_cores(args, variants):
-    """SURVEY.md 8d CPU timing (ii): every host core available to this process, OpenMP over
-    contiguous APPLE ranges (the reference's MPI range decomposition), the C port of the
-    path (oracle/fco.c, bit-matched to the reference flux_lib), same workload shape."""
-    import ctypes
-
-    import oracle_lib
-    from fcx.synthetic import build_case, inputs_for_bench
-
-    # the box's CPU share: OMP_NUM_THREADS is set to it on the GPU box (16 of the machine's
-    # cores per GPU); without it, every CPU of this process's affinity set
-    affinity = len(os.sched_getaffinity(0))
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or affinity
-    n = args.cpu_cells_mt
-    data = inputs_for_bench(n)
-    cases = [build_case(v, n=n, T=args.types, bias=args.bias, data=data if args.types == 1 else None)
-             for v in variants]
-    lib, _ = oracle_lib.load("c")
-    states = [oracle_lib.OracleState(c, 0) for c in cases]
-    for st in states:
-        lib.fco_step_threads(ctypes.byref(st.st), threads)
-    cells, t0, reps = 0, time.perf_counter(), 0
-    while True:
-        for st in states:
-            lib.fco_step_threads(ctypes.byref(st.st), threads)
-            cells += n
-        reps += 1
-        el = time.perf_counter() - t0
-        if el >= args.cpu_seconds / 2 and reps >= 2:
-            break
-    return {"value": cells / el / 1e6, "unit": "Mcells/s", "cores": threads, "kind": "port",
-            "cores_note": (f"OMP_NUM_THREADS={threads}: the CPU share of this GPU's box "
-                           f"(process affinity set: {affinity} CPUs)" if threads != affinity
-                           else "every CPU of the process affinity set"),
-            "sample": f"{reps} coupling steps x {len(variants)} variants over {n} cells, OpenMP "
-                      f"APPLE ranges on {threads} threads, {el:.1f} s"}
 
 
 def multi_gpu_check(wl, world, rank, dist, samples=2000):
@@ -460,6 +392,11 @@ def main():
     # config 5 (--bias): hourly steps whose timed half crosses 1961-01-31 -> 02-01, so the
     # bias month slice changes inside the timed region (init_date 19610101)
     t_base = 31 * 86400 - 3600 * (args.steps // 2) if args.bias else 0
+    # fcx_run_group merges the fused T = 1 passes (the accumulation in the flux kernel, no grid
+    # cap); elsewhere the engines would run one by one inside it, so the one-launch roofline
+    # does not apply and the step runs them as fcx_run
+    args.group = int(bool(args.group) and args.types == 1 and la is not None and len(variants) >= 2
+                     and (args.max_blocks is None or args.max_blocks <= 0))
     m = measure(wl, args, world, dist, coll, args.steps, args.warmup, t_base, cold=True)
     t_max = m["t_max"]
     ms_per_step = t_max / args.steps * 1e3
@@ -468,7 +405,13 @@ def main():
 
     mean_ms = m["kern_mean"]
     dom = m["dom"]
-    achieved = alg_bytes[dom] / (mean_ms[dom] * 1e-3) / 1e9
+    grouped = m["group_ms"] is not None
+    if grouped:  # the one launch of the step: every variant's algorithmic bytes
+        dom_bytes, dom_ms = int(sum(alg_bytes)), m["group_ms"]
+        dom_name = f"cells_atmos_group_kernel[{'+'.join(variants)}]"
+    else:
+        dom_bytes, dom_ms = int(alg_bytes[dom]), float(mean_ms[dom])
+    achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
     per_variant = {
         v: {"kernel_ms": round(float(mean_ms[i]), 4),
             "alg_bytes": int(alg_bytes[i]),
@@ -484,10 +427,11 @@ def main():
         try:
             t = json.load(open(tfile))
             # the timed launch carries the accumulation only when it is fused (fp64)
-            traffic = t.get(traffic_key(variants[dom], n, args.types, args.bias, fused, args.precision))
+            tkey = traffic_key("GROUP" if grouped else variants[dom], n, args.types, args.bias, fused,
+                               args.precision)
+            traffic = t.get(tkey)
             if traffic is not None:
-                traffic_source = t.get("_sources", {}).get(
-                    traffic_key(variants[dom], n, args.types, args.bias, fused, args.precision))
+                traffic_source = t.get("_sources", {}).get(tkey)
         except Exception:
             traffic = None
 
@@ -513,7 +457,8 @@ def main():
         "data": "synthetic (SURVEY.md 8d distributions, seeded PCG64)",
         "config": {
             "workload": ("config3/4: synthetic exchange grid, CCLM+MOM5+RCO fused flux kernels "
-                         "back-to-back per coupling step"
+                         + ("in one launch per coupling step (fcx_run_group)" if args.group else
+                            "back-to-back per coupling step")
                          + (" + exchange->atmosphere accumulation" if la is not None else "")
                          + (" (its own kernel after the flux pass)" if la is not None and not fused else "")
                          + (", fp32 variant (config 5)" if f32 else "") + ", inputs HBM-resident"),
@@ -541,21 +486,26 @@ def main():
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": (f"cells_atmos_kernel[{variants[dom]}]" if fused else f"cells_kernel[{variants[dom]}]"),
+            "kernel": (dom_name if grouped else
+                       f"cells_atmos_kernel[{variants[dom]}]" if fused else f"cells_kernel[{variants[dom]}]"),
             "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic,
             "traffic_source": traffic_source,
-            "alg_bytes_per_launch": int(alg_bytes[dom]),
-            "mean_kernel_ms": round(float(mean_ms[dom]), 4),
-            "events": ("one HIP event pair per timed step, around the dominant engine's launch on its stream "
+            "alg_bytes_per_launch": dom_bytes,
+            "mean_kernel_ms": round(dom_ms, 4),
+            "events": ("one HIP event pair per timed step around the step's one launch (fcx_run_group: the "
+                       "variants' fused flux passes in one grid), on its stream" if grouped else
+                       "one HIP event pair per timed step, around the dominant engine's launch on its stream "
                        "(picked in an event-timed warm-up block of every engine)" if args.kernel_events == "dominant"
                        else "HIP event pairs around every engine's launch in every timed step"),
         },
         "kernels": per_variant,
-        "kernels_rule": ("kernel_ms from the timed steps' events for " + ", ".join(variants[i] for i in m["timed_events"])
+        "kernels_rule": ("kernel_ms of each variant's own launch, from the event-timed warm-up block (one launch per "
+                         "engine); the timed steps run them as one group launch" if grouped else
+                         "kernel_ms from the timed steps' events for " + ", ".join(variants[i] for i in m["timed_events"])
                          + ("; from the event-timed warm-up block for the others" if len(m["timed_events"]) < len(variants)
                             else "")),
     }
@@ -583,6 +533,9 @@ def main():
             "dominant_kernel_ms": round(float(ko[do]), 4),
             "frac": round(wo.alg_bytes[do] / (ko[do] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
         }
+        if mo["group_ms"] is not None:
+            out["other_map"]["group_kernel_ms"] = round(mo["group_ms"], 4)
+            out["other_map"]["group_frac"] = round(sum(wo.alg_bytes) / (mo["group_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
         wo.close()
         del wo, wl
         torch.cuda.synchronize()
@@ -611,6 +564,9 @@ def main():
             "dominant_kernel_ms": round(float(k4[d4]), 4),
             "frac": round(w4.alg_bytes[d4] / (k4[d4] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
         }
+        if m4["group_ms"] is not None:
+            out["config4"]["group_kernel_ms"] = round(m4["group_ms"], 4)
+            out["config4"]["group_frac"] = round(sum(w4.alg_bytes) / (m4["group_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
         w4.close()
         del w4, wl
         torch.cuda.synchronize()
@@ -618,10 +574,37 @@ def main():
     if rank == 0 and world == 1 and args.e2e:
         out["e2e"] = e2e_host(args, variants)
     if rank == 0 and world == 1 and not args.no_cpu:
-        cb = cpu_baseline(args, variants)
-        out["cpu_baseline"] = cb
-        out["cpu_baseline_all_cores"] = cpu_all_cores(args, variants)
+        # the reference path on this box's host cores at BASELINE's config sizes: config 1/2's
+        # Baltic-size grid (32,768 cells) and this workload's size, on one core (one MPI rank
+        # of the reference) and on the box's CPU share as APPLE-range ranks (cpu_legs.py)
+        import cpu_legs
+
+        legs = cpu_legs.legs(variants, sizes=(32_768, n), seconds=args.cpu_seconds)
+        mine = legs["sizes"][str(n)]
+        one = mine["one_core"]
+        out["cpu_baseline"] = {
+            "value": one["value"], "unit": "Mcells/s", "cores": 1, "kind": one["kind"],
+            "sample": one["sample"] + " (this workload's size and inputs; the reference's call order)",
+            "sizes": legs["sizes"], "threads_all_cores": legs["threads"],
+            "affinity_cpus": legs["affinity_cpus"], "machine_cpus": legs["machine_cpus"],
+            "rule": "one_core: the reference flux_lib on 1 thread = one reference MPI rank; all_cores: the same "
+                    "on threads_all_cores processes over APPLE ranges (this box's CPU share), step = common "
+                    "barrier to the last rank; same inputs as the GPU workload of that size"}
+        out["cpu_baseline_all_cores"] = mine["all_cores"]
         out["host_cpu"] = host_cpu()
+        if "e2e" in out and "32768" in out["e2e"]["sizes"]:
+            e = out["e2e"]["sizes"]["32768"]
+            c1, cp = legs["sizes"]["32768"]["one_core"], legs["sizes"]["32768"]["all_cores"]
+            gpu_us = sum(v["us_per_step_median"] for v in e["variants"].values())
+            out["baltic_size"] = {
+                "cells": 32_768, "variants": list(variants),
+                "gpu_dropin_host_arrays_us_per_step": round(gpu_us, 1),
+                "gpu_dropin_Mcells_per_s": e["value"],
+                "cpu_one_core_us_per_step": c1["us_per_step"],
+                "cpu_all_cores_us_per_step": cp["us_per_step"], "cpu_all_cores_cores": cp["cores"],
+                "gpu_vs_all_cores": round(cp["us_per_step"] / gpu_us, 2),
+                "rule": "one coupling step of every variant from the caller's host arrays (e2e, fcx_step with the "
+                        "default transport) against the reference on this box's host cores, same grid size"}
     if rank == 0:
         print(json.dumps(out), flush=True)
     if comm is not None:

@@ -30,6 +30,9 @@ def kernel_key(name):
     m = re.search(r"cells_atmos_kernel<(\d), (double|float), (\d), (true|false)", name)
     if m:
         return VARIANTS[m.group(3)], 1, "f64" if m.group(2) == "double" else "f32"
+    m = re.search(r"cells_atmos_group_kernel<(\d), (double|float)", name)
+    if m:  # the variants' fused passes in one launch (fcx_run_group)
+        return "GROUP", 1, "f64" if m.group(2) == "double" else "f32"
     return None
 
 

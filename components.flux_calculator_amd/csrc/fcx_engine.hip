@@ -1874,9 +1874,9 @@ static int copy_bufs(fcx_engine *e, const std::vector<int> &ids, bool h2d, std::
 #define FCX_ZC_ONE_CELL 1
 #endif
 
-static int launch_plan(fcx_engine *e, Plan *pl, const double *corr_m, int64_t lo = 0, int64_t hi = -1,
-                       bool fixup = true) {
-  if (pl->host.n_max <= 0) return FCX_OK;
+// the launch shape of plan pl over cells [lo, hi) (hi < 0: to the end); *fused: the
+// exchange -> atmosphere accumulation rides in the launch (pl->af is brought up to date)
+static LaunchConfig plan_launch(fcx_engine *e, Plan *pl, int64_t lo, int64_t hi, bool *fused) {
   LaunchConfig lc = e->launch;
   lc.lo = lo;
   lc.hi = hi;
@@ -1897,9 +1897,8 @@ static int launch_plan(fcx_engine *e, Plan *pl, const double *corr_m, int64_t lo
   // remap records only from the T=1 specialised fp64 kernels with two cells per lane (the
   // rule plan_fused_records applied when it built the plan)
   lc.rec = pl->host.rec != nullptr && lc.variant && lc.cells_per_thread == 2 && !lc.f32;
-  e->rec_written = lc.rec;
-  const bool fused = pl->atm_fused && lc.variant && lc.cells_per_thread == 2;
-  if (fused) {  // the shared-slot pointers may have been set after the plan was built
+  *fused = pl->atm_fused && lc.variant && lc.cells_per_thread == 2;
+  if (*fused) {  // the shared-slot pointers may have been set after the plan was built
     pl->af.shared = e->atm_shared;
     pl->af.stride = e->atm_stride;
     pl->af.left = e->atm_left;
@@ -1915,12 +1914,27 @@ static int launch_plan(fcx_engine *e, Plan *pl, const double *corr_m, int64_t lo
       lc.halo = h;
     pl->af.halo = lc.halo;
   }
+  return lc;
+}
+
+// the crossing records' fix-up after a fused launch over the whole grid without halo tiles
+static int launch_fixup(fcx_engine *e, Plan *pl, const LaunchConfig &lc) {
+  if (e->atm_crossings <= 0 || lc.halo) return FCX_OK;
+  const int r = launch_atmos_fixup(pl->af, pl->host.n_max, lc.f32, e->stream);
+  if (r) return fail(FCX_E_HIP, "atmos_fixup launch: %s", hipGetErrorString((hipError_t)r));
+  return FCX_OK;
+}
+
+static int launch_plan(fcx_engine *e, Plan *pl, const double *corr_m, int64_t lo = 0, int64_t hi = -1,
+                       bool fixup = true) {
+  if (pl->host.n_max <= 0) return FCX_OK;
+  bool fused = false;
+  const LaunchConfig lc = plan_launch(e, pl, lo, hi, &fused);
+  e->rec_written = lc.rec;
   const int r = launch_cells(&pl->host, pl->dev, corr_m, lc, e->stream, fused ? &pl->af : nullptr);
   if (r) return fail(FCX_E_HIP, "cells_kernel launch: %s", hipGetErrorString((hipError_t)r));
-  if (fused && fixup && e->atm_crossings > 0 && !lc.halo) {
-    const int r2 = launch_atmos_fixup(pl->af, pl->host.n_max, lc.f32, e->stream);
-    if (r2) return fail(FCX_E_HIP, "atmos_fixup launch: %s", hipGetErrorString((hipError_t)r2));
-  }
+  if (fused && fixup)
+    if (int r2 = launch_fixup(e, pl, lc)) return r2;
   if (fused) e->atm_done_fused = true;
   return FCX_OK;
 }
@@ -2106,6 +2120,20 @@ static int download_remaps(fcx_engine *e, int phase, hipStream_t s, std::vector<
   return FCX_OK;
 }
 
+// after the flux launch(es) of fcx_run: the accumulation when it is not fused, the boundary
+// exchange of an attached communicator, the remaps, the closing timing event
+static int run_tail(fcx_engine *e, int phase) {
+  if (e->atmos_in_run && !e->atm_done_fused)
+    if (int r = run_atmos(e, phase)) return r;
+  e->atm_done = e->atmos_in_run || e->atm_done_fused;
+  if (e->atm_done)
+    if (int r = comm_exchange(e)) return r;
+  if (int r = run_remaps(e, phase)) return r;
+  if (e->timing) HIP_TRY(hipEventRecord(e->ev1, e->stream));
+  e->timed = e->timing;
+  return FCX_OK;
+}
+
 extern "C" int fcx_run(fcx_engine *e, int phase, int32_t t) {
   if (int r = check(e)) return r;
   if (phase < 1 || phase > 3) return fail(FCX_E_ARG, "phase %d unknown", phase);
@@ -2135,14 +2163,77 @@ extern "C" int fcx_run(fcx_engine *e, int phase, int32_t t) {
     if (int r = get_plan(e, S_AVG, phase, &pl)) return r;
     if (int r = launch_plan(e, pl, nullptr)) return r;
   }
-  if (e->atmos_in_run && !e->atm_done_fused)
-    if (int r = run_atmos(e, phase)) return r;
-  e->atm_done = e->atmos_in_run || e->atm_done_fused;
-  if (e->atm_done)
-    if (int r = comm_exchange(e)) return r;
-  if (int r = run_remaps(e, phase)) return r;
-  if (e->timing) HIP_TRY(hipEventRecord(e->ev1, e->stream));
-  e->timed = e->timing;
+  return run_tail(e, phase);
+}
+
+// fcx_run of several engines (e.g. one per bottom-model variant) in the order given, with
+// the flux passes of those whose whole phase is one fused T = 1 launch of the same shape on
+// the same stream merged into ONE launch (cells_atmos_group_kernel).  Each engine then does
+// what follows its launch in fcx_run (fix-up, accumulation, exchange, remaps).  The others
+// run as fcx_run.  Same results, bit for bit, as fcx_run of each.
+extern "C" int fcx_run_group(fcx_engine *const *es, int n, int phase, int32_t t) {
+  if (n < 0 || (n > 0 && !es)) return fail(FCX_E_ARG, "bad engine list");
+  if (phase < 1 || phase > 3) return fail(FCX_E_ARG, "phase %d unknown", phase);
+  for (int i = 0; i < n; ++i)
+    if (int r = check(es[i])) return r;
+  struct Member {
+    fcx_engine *e;
+    Plan *pl;
+    LaunchConfig lc;
+    const double *corr_m;
+  };
+  std::vector<Member> mem;
+  std::vector<fcx_engine *> solo;
+  for (int i = 0; i < n; ++i) {
+    fcx_engine *e = es[i];
+    bool ok = !e->any_regrid && !e->timing && (int)mem.size() < kMaxGroup;
+    Member m{e, nullptr, {}, nullptr};
+    if (ok) {
+      int rc;
+      m.corr_m = month_slice(e, t, &rc);
+      if (rc) return rc;
+      if (int r = get_plan(e, phase_stages(phase), phase, &m.pl)) return r;
+      bool fused = false;
+      m.lc = plan_launch(e, m.pl, 0, -1, &fused);
+      ok = fused && m.lc.variant >= 1 && !m.lc.rec && m.lc.max_blocks <= 0 && m.pl->host.num_types == 1 &&
+           m.pl->host.n_max > 0;
+      if (ok && !mem.empty()) {
+        const Member &f = mem[0];
+        ok = e->stream == f.e->stream && e->device == f.e->device && m.lc.f32 == f.lc.f32 &&
+             m.lc.nontemporal == f.lc.nontemporal && (m.lc.halo > 0) == (f.lc.halo > 0);
+      }
+    }
+    if (ok)
+      mem.push_back(m);
+    else
+      solo.push_back(e);
+  }
+  if (mem.size() == 1) {  // nothing to merge
+    solo.push_back(mem[0].e);
+    mem.clear();
+  }
+  for (fcx_engine *e : solo)
+    if (int r = fcx_run(e, phase, t)) return r;
+  if (mem.empty()) return FCX_OK;
+  GroupMember gm[kMaxGroup];
+  for (size_t k = 0; k < mem.size(); ++k) {
+    const Member &m = mem[k];
+    fcx_engine *e = m.e;
+    e->atm_done_fused = false;
+    e->atm_done = e->exchanged = false;
+    e->rec_plan = nullptr;
+    e->rec_written = false;
+    const int64_t own = (m.lc.f32 ? 4 : 2) * (64 - m.lc.halo);
+    gm[k] = GroupMember{m.pl->dev, m.corr_m, 0, m.lc.variant, 0, m.pl->af};
+    gm[k].af.n_tiles = (m.pl->host.n_max + own - 1) / own;
+  }
+  const int r = launch_cells_group(gm, (int)mem.size(), mem[0].lc, mem[0].e->stream);
+  if (r) return fail(FCX_E_HIP, "cells_atmos_group_kernel launch: %s", hipGetErrorString((hipError_t)r));
+  for (const Member &m : mem) {
+    if (int r2 = launch_fixup(m.e, m.pl, m.lc)) return r2;
+    m.e->atm_done_fused = true;
+    if (int r2 = run_tail(m.e, phase)) return r2;
+  }
   return FCX_OK;
 }
 
@@ -2687,7 +2778,13 @@ extern "C" int fcx_set_atmos_shared(fcx_engine *e, double *shared, int32_t nb, i
 
 extern "C" int fcx_atmos_finish(fcx_engine *e) {
   if (int r = check(e)) return r;
-  if (!e->atm_shared || e->n_atmos <= 0) return FCX_OK;
+  if (!e->atm_shared) return FCX_OK;
+  if (e->n_atmos <= 0) {  // a rank without cells (io:101-104): nothing to write back, but its
+                          // slots hold the reduced sums of an in-place all-reduce: re-zeroed
+    if (e->atm_nb > 0 && e->atm_stride > 0)
+      HIP_TRY(hipMemsetAsync(e->atm_shared, 0, (size_t)e->atm_nb * e->atm_stride * sizeof(double), e->stream));
+    return FCX_OK;
+  }
   const AtmosArgs a = atmos_args(e, FCX_PHASE_ALL);
   const int r = launch_atmos_finish(a, e->atm_nb, e->stream);
   if (r) return fail(FCX_E_HIP, "atmos_finish launch: %s", hipGetErrorString((hipError_t)r));

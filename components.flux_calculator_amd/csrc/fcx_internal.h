@@ -223,6 +223,27 @@ struct AtmosFused {
   uint64_t *trace;     // per wave (dispatch order): {start, end, HW_ID, XCC_ID}, or nullptr
 #endif
 };
+// Several engines' fused T = 1 launches in ONE launch (fcx_run_group): member k's wave tiles
+// are tiles [tile0, tile0 + af.n_tiles) of the grid.  Passed by value (kernel arguments).
+constexpr int kMaxGroup = 4;
+struct GroupMember {
+  const Params *P;        // the member's device parameter block
+  const double *corr_m;   // its month slice, or nullptr
+  int64_t tile0;          // its first tile in the group's grid
+  int32_t var;            // 1 CCLM, 2 MOM5, 3 RCO (the T = 1 specialisation)
+  int32_t pad;
+  AtmosFused af;          // its accumulation (af.n_tiles: its tile count)
+};
+struct GroupArgs {
+  int32_t n;
+  int32_t pad;
+  int64_t total_tiles;
+  GroupMember m[kMaxGroup];
+};
+// lc: the members' common launch shape (nontemporal, f32, halo > 0 or not); af.n_tiles of
+// every member is set here.  hipError_t as int.
+int launch_cells_group(GroupMember *members, int n, const LaunchConfig &lc, void *stream);
+
 // the segments carried over a tile boundary: carry of tile t-1 + the head cells of tile t,
 // for every tile of a launch of n_cells (fp32: 256-cell tiles of float fields)
 int launch_atmos_fixup(const AtmosFused &af, int64_t n_cells, bool f32, void *stream);

@@ -381,6 +381,17 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
   // random map): T = 2 step 1.672 -> 1.625 ms, CCLM 5.14 -> 5.26 TB/s, MOM5 5.54 -> 5.67,
   // RCO 5.26 -> 5.50.
   constexpr bool kPrefetch = kReload;
+  // Multi-type CCLM / MOM5 kernels: the atmosphere-only terms of the formulas are formed once
+  // per cell, when the type's atmosphere fields are (re)loaded, instead of once per type:
+  // T_a * EF (HSEN's pow, ta_exner) and, for CCLM, whose coefficients AMOI / AMOM are
+  // atmosphere fields too, a * max(vel, u_min) * p_s (MEVA, HSEN) and a * vel * p_s
+  // (momentum).  Same operations on the same values, so the same bits (fcx_physics.h); the
+  // type loop loses its pow and PATM / AMOI / AMOM / the wind speed need not stay live.
+#ifndef FCX_DERIVE  // A/B: 0 = every type forms its own terms (round 3)
+#define FCX_DERIVE 1
+#endif
+  constexpr bool kDerive = FCX_DERIVE && TM == 0 && (VAR == 1 || VAR == 2);
+  Vec<C, R> taef = {}, amv = {}, mvp = {};
   Vec<C, R> n_ts = {}, n_fi = {}, n_cmoi = {}, n_chea = {}, n_cmom = {}, n_fare = {};
   auto prefetch = [&](int s2) {
     const TypeParams &q = P->type[s2];
@@ -427,14 +438,50 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
         HOLD(ts, t, tsur)
         HOLD(fi, t, fice)
       }
+      // which derived atmosphere terms this type must (re)form: its fields differ from the held ones
+      const bool wind_new = (g.uatm && g.uatm != h_u) || (g.vatm && g.vatm != h_v);
+      bool d_ef = false, d_amv = false, d_mvp = false;
+      if constexpr (kDerive) {
+        const bool ps_new = g.psur && g.psur != h_ps;
+        d_ef = ps_new || (g.patm && g.patm != h_pa) || (g.tatm && g.tatm != h_ta);
+        if constexpr (VAR == 1) {
+          d_amv = ps_new || wind_new || (g.amoi && g.amoi != h_amoi);
+          d_mvp = ps_new || wind_new || (tp.uv[0].amom && tp.uv[0].amom != h_amom);
+        }
+      }
       HOLDA(ps, t, psur)
-      HOLDA(pa, t, patm)
+      if constexpr (!kDerive) HOLDA(pa, t, patm)
       HOLDA(qa, t, qatm)
       HOLDA(ta, t, tatm)
-      const bool wind_new = (g.uatm && g.uatm != h_u) || (g.vatm && g.vatm != h_v);
       HOLDA(u, t, uatm)
       HOLDA(v, t, vatm)
-      HOLDA(amoi, t, amoi)
+      if constexpr (!(kDerive && VAR == 1)) HOLDA(amoi, t, amoi)
+      if constexpr (kDerive) {
+        if (d_ef) {
+          Vec<C, R> pa_l = {};
+          if (g.patm) pa_l = LD(g.patm, j0, nt);
+          h_pa = g.patm;
+          FOR_C taef.v[i] = ta_exner(ta.v[i], ps.v[i], pa_l.v[i]);
+        }
+        if constexpr (VAR == 1) {
+          if (d_amv || d_mvp) {
+            Vec<C, R> w;  // the wind speed, only to form the two factors
+            FOR_C w.v[i] = wind(u.v[i], v.v[i]);
+            if (d_amv) {
+              Vec<C, R> am = {};
+              if (g.amoi) am = LD(g.amoi, j0, nt);
+              h_amoi = g.amoi;
+              FOR_C amv.v[i] = rate_num(am.v[i], w.v[i], ps.v[i]);
+            }
+            if (d_mvp) {
+              Vec<C, R> am = {};
+              if (tp.uv[0].amom) am = LD(tp.uv[0].amom, j0, nt);
+              h_amom = tp.uv[0].amom;
+              FOR_C mvp.v[i] = mom_num(am.v[i], w.v[i], ps.v[i]);
+            }
+          }
+        }
+      }
       if constexpr (!kPrefetch) {
         HOLD(cmoi, t, cmoi)
         HOLD(chea, t, chea)
@@ -442,10 +489,12 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
       if (g.qsur_in) qs = LD(g.qsur_in, j0, nt);  // may be written by this pass: never held
       if (g.meva_in) me = LD(g.meva_in, j0, nt);
       if constexpr (MERGED) {
-        HOLDA(amom, uv[0], amom)
+        if constexpr (!(kDerive && VAR == 1)) HOLDA(amom, uv[0], amom)
         if constexpr (!kPrefetch) HOLD(cmom, uv[0], cmom)
       }
-      if (wind_new) FOR_C vel.v[i] = wind(u.v[i], v.v[i]);
+      if constexpr (!(kDerive && VAR == 1)) {
+        if (wind_new) FOR_C vel.v[i] = wind(u.v[i], v.v[i]);
+      }
       if constexpr (RAVG) {
         if constexpr (!kPrefetch) {
           if (P->ravg_on) sink.fare = LD(P->ravg.fare[s], j0, nt);
@@ -478,8 +527,12 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
         if (m == FCX_ZERO) {
           me = splat<C, R>(R(0));
         } else if (m == FCX_CCLM || m == FCX_MOM5) {
-          const Vec<C, R> &a = (m == FCX_CCLM) ? amoi : cmoi;
-          FOR_C me.v[i] = meva_cclm(a.v[i], ps.v[i], qa.v[i], qs.v[i], ta.v[i], vel.v[i]);
+          if constexpr (kDerive && VAR == 1) {
+            FOR_C me.v[i] = meva_cclm_num(amv.v[i], qa.v[i], qs.v[i], ta.v[i]);
+          } else {
+            const Vec<C, R> &a = (m == FCX_CCLM) ? amoi : cmoi;
+            FOR_C me.v[i] = meva_cclm(a.v[i], ps.v[i], qa.v[i], qs.v[i], ta.v[i], vel.v[i]);
+          }
         } else if (m == FCX_RCO) {
           FOR_C me.v[i] = meva_rco(qa.v[i], ts.v[i], vel.v[i]);
         } else {
@@ -513,8 +566,14 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
         const int8_t m = m_hs;
         Vec<C, R> h;
         if (m == FCX_CCLM || m == FCX_MOM5) {
-          const Vec<C, R> &a = (m == FCX_CCLM) ? amoi : chea;
-          FOR_C h.v[i] = hsen_cclm(a.v[i], pa.v[i], ps.v[i], qa.v[i], ta.v[i], ts.v[i], vel.v[i]);
+          if constexpr (kDerive && VAR == 1) {
+            FOR_C h.v[i] = hsen_cclm_num(amv.v[i], qa.v[i], ts.v[i], taef.v[i]);
+          } else if constexpr (kDerive) {
+            FOR_C h.v[i] = hsen_cclm_num(rate_num(chea.v[i], vel.v[i], ps.v[i]), qa.v[i], ts.v[i], taef.v[i]);
+          } else {
+            const Vec<C, R> &a = (m == FCX_CCLM) ? amoi : chea;
+            FOR_C h.v[i] = hsen_cclm(a.v[i], pa.v[i], ps.v[i], qa.v[i], ta.v[i], ts.v[i], vel.v[i]);
+          }
           ST(g.hsen, j0, ns, h);
         } else if (m == FCX_RCO) {
           FOR_C h.v[i] = hsen_rco(ta.v[i], ts.v[i], vel.v[i]);
@@ -541,9 +600,21 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
         const bool do_u = (stages & S_UMOM) && tp.uv[0].mom;
         const bool do_v = (stages & S_VMOM) && tp.uv[1].mom;
         if (do_u || do_v) {
-          const Vec<C, R> &a = (m_mo == FCX_MOM5) ? cmom : amom;
-          if (do_u) momentum<C, NT, R>(m_mo, false, tp.uv[0], ts, ps, u, v, vel, qs, a, j0, ns, D_, sink, A_UMOM);
-          if (do_v) momentum<C, NT, R>(m_mo, true, tp.uv[1], ts, ps, u, v, vel, qs, a, j0, ns, D_, sink, A_VMOM);
+          if constexpr (kDerive && VAR == 1) {  // CCLM: the rate from a * vel * p_s formed once
+            Vec<C, R> rate;
+            FOR_C rate.v[i] = mom_cclm_rate_num(mvp.v[i], qs.v[i], ts.v[i]);
+            for (int k = 0; k < 2; ++k) {
+              if (!(k ? do_v : do_u)) continue;
+              Vec<C, R> out;
+              FOR_C out.v[i] = -(rate.v[i] * (k ? v.v[i] : u.v[i]));
+              ST(tp.uv[k].mom, j0, ns, out);
+              sink(k ? A_VMOM : A_UMOM, out);
+            }
+          } else {
+            const Vec<C, R> &a = (m_mo == FCX_MOM5) ? cmom : amom;
+            if (do_u) momentum<C, NT, R>(m_mo, false, tp.uv[0], ts, ps, u, v, vel, qs, a, j0, ns, D_, sink, A_UMOM);
+            if (do_v) momentum<C, NT, R>(m_mo, true, tp.uv[1], ts, ps, u, v, vel, qs, a, j0, ns, D_, sink, A_VMOM);
+          }
         }
       }
       // ---- distribute_shortwave_radiation_flux (calc:355-362): RSDR_s = RSDD_0
@@ -759,43 +830,21 @@ constexpr int atmos_waves() { return C == 4 ? FCX_F32_ATMOS_WAVES : FCX_ATMOS_WA
 // cells -- the head of the next tile -- only for their products (nothing of them is stored),
 // so every segment that starts in its own cells is summed inside the wave: no crossing
 // records, no fix-up launch.  Tiles are (64 - halo) * C cells apart.
-template <int C, class R, int VAR, bool NT, int TM, bool RAVG, bool REC = false, bool HALO = false>
-// (REC: the record stores took CCLM to 129 VGPRs and 3 waves per SIMD; capped at 4 blocks = 4 waves)
-__global__ __launch_bounds__(64 * atmos_waves<C>(), RAVG  ? FCX_RAVG_ATMOS_BLOCKS
-                                                  : REC ? 4
-                                                  : (C == 4 && VAR != 3) ? FCX_F32_ATMOS_BLOCKS
-                                                                         : FCX_T1_ATMOS_BLOCKS) void cells_atmos_kernel(const Params *__restrict__ P,
-                                                          const double *__restrict__ corr_m,
-                                                          const AtmosFused af, int64_t lo, int64_t hi) {
-  static_assert(!RAVG || (C == 2 && sizeof(R) == 8), "register averages: fp64 engine only");
+// One wave tile of the fused kernel: the fluxes of the tile's cells (process), their
+// products w * x parked in the wave's LDS rows, the segment sums in rounds, the crossing
+// record.  wp: the wave's LDS region.
+template <int C, class R, int VAR, bool NT, int TM, bool RAVG, bool REC, bool HALO>
+__device__ __forceinline__ void atmos_tile(const Params *__restrict__ P, const double *__restrict__ corr_m,
+                                           const AtmosFused &af, int64_t tile, double *wp) {
   constexpr int kT = tile_cells<C>();  // cells per wave tile (lane l: cells C*l .. C*l+C-1)
   constexpr int kR = row_len<C>();
-  // product rows [kFusedFields][kR]; with RAVG they first serve as the accumulators of
-  // the type-0 averages (slot k = row k, TSUR in an extra row), then hold w * average
-  constexpr int kRows = RAVG ? kAvgSlots : kFusedFields;
   constexpr bool kXF = sizeof(R) == 4;  // LDS holds fp32 fluxes + fp64 weights
-  static_assert(!kXF || C == 4, "fp32 flux rows: 4 cells per lane");
-  __shared__ double s_p[atmos_waves<C>()][wave_lds_doubles<R, C>(kRows)];
-  static_assert(!HALO || (TM == 1 && !RAVG) || (FCX_HALO_RAVG && RAVG), "halo tiles: the T=1 launch");
   const int64_t n = P->n_max;
   const int own_lanes = HALO ? 64 - af.halo : 64;
   const int64_t kO = (int64_t)C * own_lanes;  // cells a tile owns (HALO: lo == 0)
-  const int64_t n_tiles = af.n_tiles;  // (hi + kO - 1) / kO, from the host
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  double *wp = s_p[wv];
-  const int64_t waves = (int64_t)gridDim.x * (blockDim.x >> 6);
-  const int64_t wave0 =
-      (int64_t)xcd_block<C == 4 ? FCX_XCD_CHUNK_F32 : FCX_XCD_CHUNK>(blockIdx.x, gridDim.x) * (blockDim.x >> 6) + wv;
+  const int lane = threadIdx.x & 63;
   const uint64_t at_or_above = ~0ull << lane;
   const uint64_t above = lane == 63 ? 0ull : (~0ull << (lane + 1));
-#if FCX_WAVE_TRACE
-  const uint64_t trace_start = (uint64_t)wall_clock64();
-  uint64_t trace_loop = 0;
-#endif
-  for (int64_t tile = lo / kO + wave0; tile < n_tiles; tile += waves) {
-#if FCX_WAVE_TRACE
-    if (!trace_loop) trace_loop = (uint64_t)wall_clock64();
-#endif
     const int64_t t0 = tile * kO;
     const int64_t j0 = t0 + C * lane;
     LdsEmitT<C> emit{wp, {}, lds_slot(C * lane)};
@@ -924,6 +973,41 @@ __global__ __launch_bounds__(64 * atmos_waves<C>(), RAVG  ? FCX_RAVG_ATMOS_BLOCK
       }
     }
     wave_sync();  // every lane is done reading before the next tile overwrites the region
+}
+
+template <int C, class R, int VAR, bool NT, int TM, bool RAVG, bool REC = false, bool HALO = false>
+// (REC: the record stores took CCLM to 129 VGPRs and 3 waves per SIMD; capped at 4 blocks = 4 waves)
+__global__ __launch_bounds__(64 * atmos_waves<C>(), RAVG  ? FCX_RAVG_ATMOS_BLOCKS
+                                                  : REC ? 4
+                                                  : (C == 4 && VAR != 3) ? FCX_F32_ATMOS_BLOCKS
+                                                                         : FCX_T1_ATMOS_BLOCKS) void cells_atmos_kernel(const Params *__restrict__ P,
+                                                          const double *__restrict__ corr_m,
+                                                          const AtmosFused af, int64_t lo, int64_t hi) {
+  static_assert(!RAVG || (C == 2 && sizeof(R) == 8), "register averages: fp64 engine only");
+  static_assert(sizeof(R) == 8 || C == 4, "fp32 flux rows: 4 cells per lane");
+  // product rows [kFusedFields][kR]; with RAVG they first serve as the accumulators of
+  // the type-0 averages (slot k = row k, TSUR in an extra row), then hold w * average
+  constexpr int kRows = RAVG ? kAvgSlots : kFusedFields;
+  __shared__ double s_p[atmos_waves<C>()][wave_lds_doubles<R, C>(kRows)];
+  static_assert(!HALO || (TM == 1 && !RAVG) || (FCX_HALO_RAVG && RAVG), "halo tiles: the T=1 launch");
+  const int own_lanes = HALO ? 64 - af.halo : 64;
+  const int64_t kO = (int64_t)C * own_lanes;  // cells a tile owns (HALO: lo == 0)
+  const int64_t n_tiles = af.n_tiles;  // (hi + kO - 1) / kO, from the host
+  const int wv = threadIdx.x >> 6;
+  double *wp = s_p[wv];
+  const int64_t waves = (int64_t)gridDim.x * (blockDim.x >> 6);
+  const int64_t wave0 =
+      (int64_t)xcd_block<C == 4 ? FCX_XCD_CHUNK_F32 : FCX_XCD_CHUNK>(blockIdx.x, gridDim.x) * (blockDim.x >> 6) + wv;
+#if FCX_WAVE_TRACE
+  const int lane = threadIdx.x & 63;
+  const uint64_t trace_start = (uint64_t)wall_clock64();
+  uint64_t trace_loop = 0;
+#endif
+  for (int64_t tile = lo / kO + wave0; tile < n_tiles; tile += waves) {
+#if FCX_WAVE_TRACE
+    if (!trace_loop) trace_loop = (uint64_t)wall_clock64();
+#endif
+    atmos_tile<C, R, VAR, NT, TM, RAVG, REC, HALO>(P, corr_m, af, tile, wp);
   }
 #if FCX_WAVE_TRACE
   if (af.trace) {
@@ -938,6 +1022,43 @@ __global__ __launch_bounds__(64 * atmos_waves<C>(), RAVG  ? FCX_RAVG_ATMOS_BLOCK
     }
   }
 #endif
+}
+
+
+// Several engines' fused T = 1 launches as ONE launch (fcx_run_group): the members' wave
+// tiles side by side in one grid, [member 0's tiles][member 1's]..., each wave running the
+// tile of its member with that member's parameter block, variant and accumulation.  One
+// launch instead of one per engine: the ramp-up and the drain tail of a launch (~20-25 us
+// each) are paid once per step, and the tail of one member's tiles
+// overlaps the next member's.  Per tile the same code as cells_atmos_kernel, so the same bits.
+template <int C, class R, bool NT, bool HALO>
+#ifndef FCX_GROUP_BLOCKS  // blocks per CU the fp64 group kernel is compiled for
+#define FCX_GROUP_BLOCKS 4
+#endif
+__global__ __launch_bounds__(64 * atmos_waves<C>(), C == 4 ? FCX_F32_ATMOS_BLOCKS : FCX_GROUP_BLOCKS) void
+cells_atmos_group_kernel(const GroupArgs g) {
+  __shared__ double s_p[atmos_waves<C>()][wave_lds_doubles<R, C>(kFusedFields)];
+  const int wv = threadIdx.x >> 6;
+  double *wp = s_p[wv];
+  const int64_t waves = (int64_t)gridDim.x * (blockDim.x >> 6);
+  const int64_t wave0 =
+      (int64_t)xcd_block<C == 4 ? FCX_XCD_CHUNK_F32 : FCX_XCD_CHUNK>(blockIdx.x, gridDim.x) * (blockDim.x >> 6) + wv;
+  for (int64_t t = wave0; t < g.total_tiles; t += waves) {
+    // the member of tile t: wave-uniform, said so to the compiler (readfirstlane), so that
+    // its parameters are scalar loads -- derived from threadIdx.x >> 6, the index would be
+    // taken for a per-lane value and every member field would occupy VGPRs
+    int k = 0;
+    for (int q = 1; q < g.n; ++q)
+      if (t >= g.m[q].tile0) k = q;
+    k = __builtin_amdgcn_readfirstlane(k);
+    const GroupMember &m = g.m[k];
+    const int64_t tile = t - m.tile0;
+    switch (m.var) {
+      case 1: atmos_tile<C, R, 1, NT, 1, false, false, HALO>(m.P, m.corr_m, m.af, tile, wp); break;
+      case 2: atmos_tile<C, R, 2, NT, 1, false, false, HALO>(m.P, m.corr_m, m.af, tile, wp); break;
+      default: atmos_tile<C, R, 3, NT, 1, false, false, HALO>(m.P, m.corr_m, m.af, tile, wp); break;
+    }
+  }
 }
 
 // Segments that straddle a tile boundary: the launch leaves, in the crossing record of every tile t, the prefix sum of tile t-1's last
@@ -1365,6 +1486,42 @@ int launch_cells(const Params *hp, const Params *dp, const double *corr_m, const
     launch_r<2, double>(hp, lc, blocks, s, dp, corr_m, lo, hi);
   } else {
     launch_r<1, double>(hp, lc, blocks, s, dp, corr_m, lo, hi);
+  }
+  return (int)hipGetLastError();
+}
+
+template <int C, class R, bool NT>
+static void launch_group_h(bool halo, int blocks, hipStream_t s, const GroupArgs &g) {
+  if (halo)
+    hipLaunchKernelGGL((cells_atmos_group_kernel<C, R, NT, true>), dim3(blocks), dim3(64 * atmos_waves<C>()), 0, s, g);
+  else
+    hipLaunchKernelGGL((cells_atmos_group_kernel<C, R, NT, false>), dim3(blocks), dim3(64 * atmos_waves<C>()), 0, s, g);
+}
+
+int launch_cells_group(GroupMember *members, int n, const LaunchConfig &lc, void *stream) {
+  if (n < 1 || n > kMaxGroup) return (int)hipErrorInvalidValue;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  GroupArgs g{};
+  g.n = n;
+  int64_t total = 0;
+  for (int k = 0; k < n; ++k) {  // (af.n_tiles: set by the caller from the member's cells)
+    GroupMember &m = members[k];
+    if (m.var < 1 || m.var > 3 || (m.af.halo > 0) != (lc.halo > 0) || m.af.n_tiles < 0)
+      return (int)hipErrorInvalidValue;
+    m.tile0 = total;
+    total += m.af.n_tiles;
+    g.m[k] = m;
+  }
+  g.total_tiles = total;
+  if (total == 0) return 0;
+  const int64_t kw = lc.f32 ? atmos_waves<4>() : atmos_waves<2>();
+  const int blocks = (int)std::max<int64_t>(1, (total + kw - 1) / kw);
+  if (lc.f32) {
+    if (lc.nontemporal) launch_group_h<4, float, true>(lc.halo > 0, blocks, s, g);
+    else launch_group_h<4, float, false>(lc.halo > 0, blocks, s, g);
+  } else {
+    if (lc.nontemporal) launch_group_h<2, double, true>(lc.halo > 0, blocks, s, g);
+    else launch_group_h<2, double, false>(lc.halo > 0, blocks, s, g);
   }
   return (int)hipGetLastError();
 }

@@ -57,12 +57,26 @@ __device__ __forceinline__ R wind(R u, R v) {
   return sqrt(u * u + v * v);
 }
 
+// The atmosphere-only leading factor a * max(vel, u_min) * p_s of the CCLM/MOM5 exchange rate
+// (flux_mass_evap.F90:76, flux_heat_sensible.F90:88), left to right as the reference
+// evaluates it.  With several surface types and an atmosphere-side coefficient (CCLM: AMOI)
+// the multi-type kernels form it once per cell; the formulas below are written through it,
+// so both ways are the same operations and the same bits.
+template <class R>
+__device__ __forceinline__ R rate_num(R a, R vel, R ps) {
+  return a * fmax(vel, R(kUmin)) * ps;
+}
+
 // flux_lib/mass/flux_mass_evap.F90:72-83 (flux_mass_evap_cclm; _mom5 = same with CMOI)
+template <class R>
+__device__ __forceinline__ R meva_cclm_num(R num, R qa, R qs, R ts) {
+  const R fa = num / (R(kRd) * t_tilde(ts, qs));
+  return fa * (qs - qa);
+}
 template <class R>
 __device__ __forceinline__ R meva_cclm(R a, R ps, R qa, R qs, R ts, R vel) {
   FCX_TRIVIAL(a + ps + qa + qs + ts + vel)
-  const R fa = a * fmax(vel, R(kUmin)) * ps / (R(kRd) * t_tilde(ts, qs));
-  return fa * (qs - qa);
+  return meva_cclm_num(rate_num(a, vel, ps), qa, qs, ts);
 }
 
 // flux_lib/mass/flux_mass_evap.F90:117-156 (flux_mass_evap_rco)
@@ -93,13 +107,22 @@ __device__ __forceinline__ R pow_exner(R x, R y) {
 #endif
 }
 
-// flux_lib/heat/flux_heat_sensible.F90:74-94 (flux_heat_sensible_cclm; _mom5 = with CHEA)
+// flux_lib/heat/flux_heat_sensible.F90:74-94 (flux_heat_sensible_cclm; _mom5 = with CHEA).
+// T_a * EF = T_a * (p_s / p_a)**(R_d / c_p) involves atmosphere fields only: the multi-type
+// kernels form it once per cell (ta_exner) instead of one pow per surface type.
+template <class R>
+__device__ __forceinline__ R ta_exner(R ta, R ps, R pa) {
+  return ta * pow_exner(ps / pa, R(kRd / kCp));
+}
+template <class R>
+__device__ __forceinline__ R hsen_cclm_num(R num, R qs, R ts, R taef) {
+  const R fa = num / (R(kRd) * t_tilde(ts, qs));
+  return fa * R(kCp) * (ts - taef);
+}
 template <class R>
 __device__ __forceinline__ R hsen_cclm(R a, R pa, R ps, R qs, R ta, R ts, R vel) {
   FCX_TRIVIAL(a + pa + ps + qs + ta + ts + vel)
-  const R fa = a * fmax(vel, R(kUmin)) * ps / (R(kRd) * t_tilde(ts, qs));
-  const R ef = pow_exner(ps / pa, R(kRd / kCp));
-  return fa * R(kCp) * (ts - ta * ef);
+  return hsen_cclm_num(rate_num(a, vel, ps), qs, ts, ta_exner(ta, ps, pa));
 }
 
 // flux_lib/heat/flux_heat_sensible.F90:136-165 (flux_heat_sensible_rco)
@@ -112,10 +135,19 @@ __device__ __forceinline__ R hsen_rco(R ta, R ts, R vel) {
 }
 
 // flux_lib/momentum/flux_momentum.F90:56-69: mass exchange rate; east = -(fa*u), north = -(fa*v)
+// (no u_min here); a * vel * p_s is atmosphere-only for CCLM (AMOM): mom_num, formed once
+template <class R>
+__device__ __forceinline__ R mom_num(R a, R vel, R ps) {
+  return a * vel * ps;
+}
+template <class R>
+__device__ __forceinline__ R mom_cclm_rate_num(R num, R qs, R ts) {
+  return num / (R(kRd) * t_tilde(ts, qs));
+}
 template <class R>
 __device__ __forceinline__ R mom_cclm_rate(R a, R ps, R qs, R ts, R vel) {
   FCX_TRIVIAL(a + ps + qs + ts + vel)
-  return a * vel * ps / (R(kRd) * t_tilde(ts, qs));
+  return mom_cclm_rate_num(mom_num(a, vel, ps), qs, ts);
 }
 
 // flux_lib/momentum/flux_momentum.F90:107-136: -(rho_a*c_aw*vel*u) = -(rate*u)

@@ -67,6 +67,7 @@ SIGNATURES = [
     ("fcx_staging_bytes", _I, [_P, _c.POINTER(_I64)]),
     ("fcx_algorithmic_bytes", _I, [_P, _I, _c.POINTER(_I64)]),
     ("fcx_zero_copy_bytes", _I, [_P, _c.POINTER(_I64)]),
+    ("fcx_run_group", _I, [_P, _I, _I, _I32]),
     ("fcx_pinned_bytes", _I, [_P, _c.POINTER(_I64)]),
     ("fcx_handoff_recoveries", _I, [_P, _c.POINTER(_I64)]),
     ("fcx_host_malloc", _I, [_c.c_size_t, _c.POINTER(_P)]),

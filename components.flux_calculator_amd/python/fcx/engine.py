@@ -224,6 +224,16 @@ class Engine:
             pass
 
 
+def run_group(engines, phase=PHASE_ALL, current_step_time=0):
+    """fcx_run of every engine, the fused T = 1 flux passes of the same shape as ONE launch
+    (fcx_run_group): the same results as Engine.run of each."""
+    if not engines:
+        return
+    lib = engines[0].lib
+    arr = (ctypes.c_void_p * len(engines))(*[e.h.value for e in engines])
+    _lib.check(lib.fcx_run_group(arr, len(engines), phase, int(current_step_time)))
+
+
 def current_month(init_date, seconds):
     """datetime_helpers.get_current_date(...)['current_month'] via libfcx."""
     lib = _lib.load()
@@ -232,4 +242,4 @@ def current_month(init_date, seconds):
     return m.value
 
 
-__all__ = ["Engine", "current_month", "PHASE_EARLY", "PHASE_NORMAL", "PHASE_ALL"]
+__all__ = ["Engine", "run_group", "current_month", "PHASE_EARLY", "PHASE_NORMAL", "PHASE_ALL"]

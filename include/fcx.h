@@ -130,6 +130,12 @@ int fcx_commit(fcx_engine *e);
 int fcx_upload(fcx_engine *e, int phase);   /* H2D of host-bound inputs of the phase  */
 int fcx_run(fcx_engine *e, int phase, int32_t current_step_time); /* device compute  */
 int fcx_download(fcx_engine *e, int phase); /* D2H of host-bound outputs of the phase */
+/* fcx_run of several engines on one device (e.g. one per bottom-model variant), in the order
+ * given: the flux passes of those whose phase is one fused T = 1 launch of the same shape on
+ * the same stream go out as ONE launch (at most 4 engines; the others run as fcx_run), so a
+ * step pays the launch ramp and drain once.  Results are those of fcx_run of each, bit for
+ * bit. */
+int fcx_run_group(fcx_engine *const *engines, int n_engines, int phase, int32_t current_step_time);
 /* the three above; with host-bound fields pipelined over cell chunks (FCX_OPT_PIPELINE_CHUNKS) */
 int fcx_step(fcx_engine *e, int phase, int32_t current_step_time);
 /* waits for the engine's stream; the caller's host arrays hold the downloaded outputs once it

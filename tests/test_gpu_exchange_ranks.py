@@ -30,7 +30,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 MOCK = os.path.join(ROOT, "components.flux_calculator_amd", "lib", "test", "libmock_rccl.so")
 FIELDS = (("MEVA", 1), ("HLAT", 1), ("HSEN", 1), ("RBBR", 1), ("UMOM", 2), ("VMOM", 3))
 VARIANTS = ("CCLM", "MOM5", "RCO")
-N = 24_011
+N = 24_012  # every APPLE cut of 2 and 3 ranks falls inside an atmosphere cell
 
 # (name, slot layout, streams, special); run by every rank in this order
 SCENARIOS = [

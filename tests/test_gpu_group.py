@@ -1,0 +1,106 @@
+"""fcx_run_group: several engines' fused T = 1 flux passes (one per bottom-model variant) as
+ONE launch (cells_atmos_group_kernel).  Each tile runs the same code as the engine's own
+launch, so every flux and every atmosphere value must be the bits of fcx_run of each engine;
+engines that cannot join (several surface types, a grid cap) run as fcx_run inside the call."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+from fcx.basic import PHASE_ALL  # noqa: E402
+from fcx.workload import ATM_FIELDS, Workload  # noqa: E402
+
+
+def outputs(wl):
+    wl.download()
+    got = {}
+    for i, (case, outs) in enumerate(zip(wl.cases, wl.atm_outs)):
+        for k in case.outputs:
+            got[(i,) + k] = np.array(case.lf.field[k], copy=True)
+        for name, _ in ATM_FIELDS:
+            got[(i, "atm", name)] = np.array(outs[name], copy=True)
+    return got
+
+
+def run_both(n, variants, atmos_map, precision="f64", types=1, options=None, steps=2):
+    import torch
+
+    res = []
+    for grouped in (False, True):
+        wl = Workload(n, 0, 1, variants, types=types, precision=precision, atmos=True, atmos_map=atmos_map,
+                      engine_options=options)
+        for k in range(steps):
+            if grouped:
+                wl.run_group(3600 * k)
+            else:
+                wl.run(3600 * k)
+        torch.cuda.synchronize()
+        res.append(outputs(wl))
+        wl.close()
+    return res
+
+
+def same_bits(a, b):
+    assert a.keys() == b.keys()
+    for k in a:
+        np.testing.assert_array_equal(a[k], b[k], err_msg=str(k))
+
+
+@pytest.mark.parametrize("precision", ["f64", "f32"])
+@pytest.mark.parametrize("atmos_map", ["random", "periodic"])
+def test_group_launch_bit_identical(precision, atmos_map):
+    """CCLM + MOM5 + RCO in one launch: random map (segments cross the wave tiles: halo
+    tiles), periodic map (no crossing)."""
+    a, b = run_both(300_007, ("CCLM", "MOM5", "RCO"), atmos_map, precision)
+    same_bits(a, b)
+
+
+@pytest.mark.parametrize("variants", [("RCO", "CCLM"), ("MOM5", "MOM5", "CCLM", "RCO")])
+def test_group_orders_and_sizes(variants):
+    """Any order, repeated variants, four members (the most one launch takes)."""
+    a, b = run_both(70_001, variants, "random")
+    same_bits(a, b)
+
+
+def test_group_without_halo_uses_crossing_records():
+    """Halo tiles off (FCX_OPT_ATMOS_HALO 0): the members' crossing records and fix-ups."""
+    a, b = run_both(130_003, ("CCLM", "MOM5", "RCO"), "random", options={"atmos_halo": 0})
+    same_bits(a, b)
+
+
+def test_group_falls_back_for_engines_that_cannot_join():
+    """Two surface types (register averages, not a T = 1 launch) and a grid cap: every engine
+    runs as fcx_run inside fcx_run_group, with the same results."""
+    a, b = run_both(50_021, ("CCLM", "RCO"), "random", types=2)
+    same_bits(a, b)
+    a, b = run_both(50_021, ("CCLM", "RCO"), "random", options={"max_blocks": 32})
+    same_bits(a, b)
+
+
+def test_group_of_engines_on_different_streams_runs_them_apart():
+    """Engines on different streams are not merged (each keeps its stream order)."""
+    import torch
+    from fcx.engine import Engine, run_group
+    from fcx.synthetic import build_case
+
+    n = 40_003
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    cases = [build_case(v, n=n, T=1, bias=True) for v in ("CCLM", "MOM5")]
+    engines = [Engine(c.lf, 1, c.methods, corrections=c.corrections, stream=s.cuda_stream)
+               for c, s in zip(cases, streams)]
+    for e in engines:
+        e.upload(PHASE_ALL)
+    run_group(engines, PHASE_ALL, 7200)
+    for e in engines:
+        e.download(PHASE_ALL)
+        e.synchronize()
+    got = [{k: np.array(c.lf.field[k], copy=True) for k in c.outputs} for c in cases]
+    for e in engines:
+        e.run(PHASE_ALL, 7200)
+        e.download(PHASE_ALL)
+        e.synchronize()
+    for c, g in zip(cases, got):
+        for k in c.outputs:
+            np.testing.assert_array_equal(g[k], np.asarray(c.lf.field[k]), err_msg=str(k))
+    for e in engines:
+        e.close()
