@@ -395,7 +395,7 @@ def main():
     # fcx_run_group merges the fused T = 1 passes (the accumulation in the flux kernel, no grid
     # cap); elsewhere the engines would run one by one inside it, so the one-launch roofline
     # does not apply and the step runs them as fcx_run
-    args.group = int(bool(args.group) and args.types == 1 and la is not None and len(variants) >= 2
+    args.group = int(bool(args.group) and la is not None and len(variants) >= 2 and (args.types == 1 or not f32)
                      and (args.max_blocks is None or args.max_blocks <= 0))
     m = measure(wl, args, world, dist, coll, args.steps, args.warmup, t_base, cold=True)
     t_max = m["t_max"]

@@ -2195,12 +2195,14 @@ extern "C" int fcx_run_group(fcx_engine *const *es, int n, int phase, int32_t t)
       if (int r = get_plan(e, phase_stages(phase), phase, &m.pl)) return r;
       bool fused = false;
       m.lc = plan_launch(e, m.pl, 0, -1, &fused);
-      ok = fused && m.lc.variant >= 1 && !m.lc.rec && m.lc.max_blocks <= 0 && m.pl->host.num_types == 1 &&
-           m.pl->host.n_max > 0;
+      // one surface type, or several with the type-0 averages in registers (fp64, no halo)
+      const bool shape = m.pl->host.num_types == 1 || (m.lc.ravg && !m.lc.f32 && m.lc.halo == 0);
+      ok = fused && shape && m.lc.variant >= 1 && !m.lc.rec && m.lc.max_blocks <= 0 && m.pl->host.n_max > 0;
       if (ok && !mem.empty()) {
         const Member &f = mem[0];
         ok = e->stream == f.e->stream && e->device == f.e->device && m.lc.f32 == f.lc.f32 &&
-             m.lc.nontemporal == f.lc.nontemporal && (m.lc.halo > 0) == (f.lc.halo > 0);
+             m.lc.nontemporal == f.lc.nontemporal && (m.lc.halo > 0) == (f.lc.halo > 0) &&
+             m.lc.ravg == f.lc.ravg && (m.pl->host.num_types == 1) == (f.pl->host.num_types == 1);
       }
     }
     if (ok)

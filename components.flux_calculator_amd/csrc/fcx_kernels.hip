@@ -1025,19 +1025,25 @@ __global__ __launch_bounds__(64 * atmos_waves<C>(), RAVG  ? FCX_RAVG_ATMOS_BLOCK
 }
 
 
-// Several engines' fused T = 1 launches as ONE launch (fcx_run_group): the members' wave
+// Several engines' fused launches as ONE launch (fcx_run_group): the members' wave
 // tiles side by side in one grid, [member 0's tiles][member 1's]..., each wave running the
 // tile of its member with that member's parameter block, variant and accumulation.  One
 // launch instead of one per engine: the ramp-up and the drain tail of a launch (~20-25 us
 // each) are paid once per step, and the tail of one member's tiles
 // overlaps the next member's.  Per tile the same code as cells_atmos_kernel, so the same bits.
-template <int C, class R, bool NT, bool HALO>
-#ifndef FCX_GROUP_BLOCKS  // blocks per CU the fp64 group kernel is compiled for
+// Blocks per CU the fp64 T = 1 group kernel is compiled for: 4 = 128 VGPRs, 4 waves per SIMD
+// like the members' own kernels (left free, the three inlined bodies take 139-146 VGPRs and
+// 3 waves; at 128 one 8-B value of the preamble spills: one store and two reloads per wave).
+// The multi-type group (RAVG) keeps the members' FCX_RAVG_ATMOS_BLOCKS.
+#ifndef FCX_GROUP_BLOCKS
 #define FCX_GROUP_BLOCKS 4
 #endif
-__global__ __launch_bounds__(64 * atmos_waves<C>(), C == 4 ? FCX_F32_ATMOS_BLOCKS : FCX_GROUP_BLOCKS) void
+template <int C, class R, bool NT, bool HALO, int TM = 1, bool RAVG = false>
+__global__ __launch_bounds__(64 * atmos_waves<C>(), RAVG ? FCX_RAVG_ATMOS_BLOCKS
+                                                    : C == 4 ? FCX_F32_ATMOS_BLOCKS : FCX_GROUP_BLOCKS) void
 cells_atmos_group_kernel(const GroupArgs g) {
-  __shared__ double s_p[atmos_waves<C>()][wave_lds_doubles<R, C>(kFusedFields)];
+  constexpr int kRows = RAVG ? kAvgSlots : kFusedFields;
+  __shared__ double s_p[atmos_waves<C>()][wave_lds_doubles<R, C>(kRows)];
   const int wv = threadIdx.x >> 6;
   double *wp = s_p[wv];
   const int64_t waves = (int64_t)gridDim.x * (blockDim.x >> 6);
@@ -1054,9 +1060,9 @@ cells_atmos_group_kernel(const GroupArgs g) {
     const GroupMember &m = g.m[k];
     const int64_t tile = t - m.tile0;
     switch (m.var) {
-      case 1: atmos_tile<C, R, 1, NT, 1, false, false, HALO>(m.P, m.corr_m, m.af, tile, wp); break;
-      case 2: atmos_tile<C, R, 2, NT, 1, false, false, HALO>(m.P, m.corr_m, m.af, tile, wp); break;
-      default: atmos_tile<C, R, 3, NT, 1, false, false, HALO>(m.P, m.corr_m, m.af, tile, wp); break;
+      case 1: atmos_tile<C, R, 1, NT, TM, RAVG, false, HALO>(m.P, m.corr_m, m.af, tile, wp); break;
+      case 2: atmos_tile<C, R, 2, NT, TM, RAVG, false, HALO>(m.P, m.corr_m, m.af, tile, wp); break;
+      default: atmos_tile<C, R, 3, NT, TM, RAVG, false, HALO>(m.P, m.corr_m, m.af, tile, wp); break;
     }
   }
 }
@@ -1491,7 +1497,14 @@ int launch_cells(const Params *hp, const Params *dp, const double *corr_m, const
 }
 
 template <int C, class R, bool NT>
-static void launch_group_h(bool halo, int blocks, hipStream_t s, const GroupArgs &g) {
+static void launch_group_h(bool halo, bool ravg, int blocks, hipStream_t s, const GroupArgs &g) {
+  if constexpr (C == 2) {
+    if (ravg) {  // several surface types, the type-0 averages in registers (no halo tiles)
+      hipLaunchKernelGGL((cells_atmos_group_kernel<C, R, NT, false, 0, true>), dim3(blocks),
+                         dim3(64 * atmos_waves<C>()), 0, s, g);
+      return;
+    }
+  }
   if (halo)
     hipLaunchKernelGGL((cells_atmos_group_kernel<C, R, NT, true>), dim3(blocks), dim3(64 * atmos_waves<C>()), 0, s, g);
   else
@@ -1516,12 +1529,13 @@ int launch_cells_group(GroupMember *members, int n, const LaunchConfig &lc, void
   if (total == 0) return 0;
   const int64_t kw = lc.f32 ? atmos_waves<4>() : atmos_waves<2>();
   const int blocks = (int)std::max<int64_t>(1, (total + kw - 1) / kw);
+  if (lc.ravg && (lc.f32 || lc.halo > 0)) return (int)hipErrorInvalidValue;
   if (lc.f32) {
-    if (lc.nontemporal) launch_group_h<4, float, true>(lc.halo > 0, blocks, s, g);
-    else launch_group_h<4, float, false>(lc.halo > 0, blocks, s, g);
+    if (lc.nontemporal) launch_group_h<4, float, true>(lc.halo > 0, false, blocks, s, g);
+    else launch_group_h<4, float, false>(lc.halo > 0, false, blocks, s, g);
   } else {
-    if (lc.nontemporal) launch_group_h<2, double, true>(lc.halo > 0, blocks, s, g);
-    else launch_group_h<2, double, false>(lc.halo > 0, blocks, s, g);
+    if (lc.nontemporal) launch_group_h<2, double, true>(lc.halo > 0, lc.ravg, blocks, s, g);
+    else launch_group_h<2, double, false>(lc.halo > 0, lc.ravg, blocks, s, g);
   }
   return (int)hipGetLastError();
 }

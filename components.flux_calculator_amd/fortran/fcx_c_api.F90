@@ -129,6 +129,14 @@ MODULE fcx_c_api
       INTEGER(c_int32_t), VALUE :: t
       INTEGER(c_int) :: fcx_run
     END FUNCTION
+    ! several engines' fcx_run, their fused flux passes as one launch (engines: c_ptr array)
+    FUNCTION fcx_run_group(engines, n, phase, t) BIND(C, name='fcx_run_group')
+      IMPORT :: c_int, c_int32_t, c_ptr
+      TYPE(c_ptr), DIMENSION(*), INTENT(IN) :: engines
+      INTEGER(c_int), VALUE :: n, phase
+      INTEGER(c_int32_t), VALUE :: t
+      INTEGER(c_int) :: fcx_run_group
+    END FUNCTION
     FUNCTION fcx_upload(engine, phase) BIND(C, name='fcx_upload')
       IMPORT :: c_int, c_ptr
       TYPE(c_ptr), VALUE :: engine

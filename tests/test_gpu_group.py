@@ -68,12 +68,20 @@ def test_group_without_halo_uses_crossing_records():
     same_bits(a, b)
 
 
-def test_group_falls_back_for_engines_that_cannot_join():
-    """Two surface types (register averages, not a T = 1 launch) and a grid cap: every engine
-    runs as fcx_run inside fcx_run_group, with the same results."""
-    a, b = run_both(50_021, ("CCLM", "RCO"), "random", types=2)
+@pytest.mark.parametrize("types", [2, 3])
+def test_group_of_multi_type_launches(types):
+    """Several surface types: the members' multi-type kernels (type-0 averages in registers,
+    accumulated on the fly) in one launch."""
+    a, b = run_both(50_021, ("CCLM", "MOM5", "RCO"), "random", types=types)
     same_bits(a, b)
+
+
+def test_group_falls_back_for_engines_that_cannot_join():
+    """A grid cap (not a one-trip fused launch) and fp32 at two surface types (no fused
+    multi-type fp32 kernel): every engine runs as fcx_run inside fcx_run_group."""
     a, b = run_both(50_021, ("CCLM", "RCO"), "random", options={"max_blocks": 32})
+    same_bits(a, b)
+    a, b = run_both(50_021, ("CCLM", "RCO"), "random", precision="f32", types=2)
     same_bits(a, b)
 
 
