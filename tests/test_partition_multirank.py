@@ -325,3 +325,25 @@ def test_geometric_maps_are_conservative_and_ordered():
     np.testing.assert_allclose(s[s > 0], 1.0, rtol=1e-13)
     # within an atmosphere cell the ocean cells come row by row
     assert n == pytest.approx(am.n_atmos * (1 + 1 / 0.75) ** 2, rel=0.05)
+
+
+@pytest.mark.parametrize("mapcls", ["PeriodicAtmosMap", "BlockedRandomAtmosMap"])
+def test_structured_maps_take_the_boundary_slot_rule(mapcls):
+    """With every rank's ranges, the O(size) structured maps of the bench give the slots of
+    boundary_slots on their global map -- including ranks inside one atmosphere cell
+    (left == right) and APPLE ranges of many ranks."""
+    import fcx.parallel as par
+
+    mk = getattr(par, mapcls)()
+    n = 20_000
+    g = mk.global_map(n)
+    c0 = int(np.flatnonzero(np.bincount(g.atmos_index) >= 4)[5])
+    c0 = int(np.searchsorted(g.atmos_index, c0))
+    cases = [[apple_range(n, r, 7) for r in range(7)],
+             [(0, c0 + 1), (c0 + 1, 1), (c0 + 2, 1), (c0 + 3, n - c0 - 3)]]
+    for ranges in cases:
+        p = len(ranges)
+        for rank, (off, size) in enumerate(ranges):
+            a = mk.local(off, size, rank, p, n, ranges=ranges)
+            b = local_atmos(g, rank, p, ranges=ranges)
+            assert (a.left, a.right, a.n_atmos, a.atmos_offset) == (b.left, b.right, b.n_atmos, b.atmos_offset)
