@@ -89,6 +89,10 @@ def parse():
     p.add_argument("--precision", choices=("f64", "f32"), default="f64",
                    help="f32: the fp32 variant (config 5): fp32 cell pass with the accumulation fused in "
                         "(fp32 fluxes, fp64 weights, products and sums, fp32 outputs)")
+    p.add_argument("--group", type=int, default=1,
+                   help="1: every step runs the variants' engines through fcx_run_group, their fused flux "
+                        "passes as ONE launch (one event pair around it in the timed steps); 0: one launch "
+                        "per engine")
     p.add_argument("--kernel-events", choices=("dominant", "all"), default="dominant",
                    help="HIP event pairs inside the timed steps: around the dominant engine's launch only "
                         "(picked in an event-timed warm-up block), or around every engine's")
@@ -249,9 +253,13 @@ def measure(wl, args, world, dist, comm, steps, warmup, t_base=0, cold=False):
     import torch
 
     stream = wl.stream
+    group = bool(args.group)
 
-    def step(t, events=None):
-        wl.run(t, events)
+    def step(t, events=None, grouped=group):
+        if grouped:  # fcx_run_group: the variants' flux passes as one launch
+            wl.run_group(t, events)
+        else:
+            wl.run(t, events)
         if comm is not None:
             comm.atmos_allreduce(wl.engines)  # the one collective of the step (RCCL over xGMI)
 
@@ -268,6 +276,7 @@ def measure(wl, args, world, dist, comm, steps, warmup, t_base=0, cold=False):
     # the timed steps' events exist before the warm-up starts: nothing host-side sits between
     # the warm-up and the timed region (an idle GPU drops its clocks)
     ev = pairs(steps)
+    ev_group = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
     step(t_base)  # builds the engines' plans
     torch.cuda.synchronize()
     cold_ms = None
@@ -291,8 +300,8 @@ def measure(wl, args, world, dist, comm, steps, warmup, t_base=0, cold=False):
         torch.cuda.synchronize()
         if warm >= warmup and time.perf_counter() - t_w >= MIN_WARMUP_S:
             break
-    for k in range(probe_steps):  # still warm-up: the event-timed block
-        step(t_base + (warm + k) * 3600, ev_probe[k])
+    for k in range(probe_steps):  # still warm-up: the event-timed block, one launch per engine
+        step(t_base + (warm + k) * 3600, ev_probe[k], grouped=False)
     torch.cuda.synchronize()
     probe_ms = np.array([[a.elapsed_time(b) for (a, b) in row] for row in ev_probe])  # [steps][variant]
     dom = int(np.argmax(probe_ms.mean(axis=0)))
@@ -308,7 +317,7 @@ def measure(wl, args, world, dist, comm, steps, warmup, t_base=0, cold=False):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(steps):
-        step(t_base + k * 3600, ev[k])
+        step(t_base + k * 3600, ev_group[k] if group else ev[k])
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -316,8 +325,9 @@ def measure(wl, args, world, dist, comm, steps, warmup, t_base=0, cold=False):
     # per-variant mean kernel time: the timed steps where they carry events (the dominant
     # engine; every engine with --kernel-events all), the event-timed warm-up block otherwise
     kern_mean = probe_ms.mean(axis=0)
-    timed = {i: np.array([row[i][0].elapsed_time(row[i][1]) for row in ev])
-             for i in range(nv) if ev and ev[0][i] is not None}
+    timed = {} if group else {i: np.array([row[i][0].elapsed_time(row[i][1]) for row in ev])
+                              for i in range(nv) if ev and ev[0][i] is not None}
+    group_ms = float(np.mean([a.elapsed_time(b) for a, b in ev_group])) if group and steps else None
     for i, x in timed.items():
         kern_mean[i] = x.mean()
     t_max = elapsed
@@ -327,7 +337,7 @@ def measure(wl, args, world, dist, comm, steps, warmup, t_base=0, cold=False):
         t_max = float(tt.item())
     del stream
     return {"t_max": t_max, "kern_mean": kern_mean, "dom": dom, "timed_events": sorted(timed),
-            "cold_ms": cold_ms, "warm": warm, "warmup_s": warmup_s}
+            "cold_ms": cold_ms, "warm": warm, "warmup_s": warmup_s, "group_ms": group_ms}
 
 
 def main():

@@ -79,11 +79,8 @@ __device__ __forceinline__ Vec<C, R> ld(const R *__restrict__ p, int64_t j0, int
   return r;
 }
 
-// temporal: a plain store even when NT (a line this wave shares with its neighbour, which
-// should stay in L2 until the neighbour's part merges into it)
 template <int C, bool NT, class R>
-__device__ __forceinline__ void st(R *__restrict__ p, int64_t j0, int64_t n, const Vec<C, R> &x,
-                                   bool temporal = false) {
+__device__ __forceinline__ void st(R *__restrict__ p, int64_t j0, int64_t n, const Vec<C, R> &x) {
   if constexpr (C * sizeof(R) == 16) {
     if (j0 + C <= n) {
       using V = typename std::conditional<sizeof(R) == 8, d2, f4>::type;
@@ -93,7 +90,7 @@ __device__ __forceinline__ void st(R *__restrict__ p, int64_t j0, int64_t n, con
       for (int i = 0; i < C; ++i) t[i] = x.v[i];
       // (write-through sc1 / sc1 nt stores instead of nt: step +9 to +27 %,
       // profiles/r03/store_wt_ab/ -- the L2 write-back merges the output lines)
-      if (NT && !temporal)
+      if (NT)
         __builtin_nontemporal_store(t, q);
       else
         *q = t;
@@ -121,13 +118,7 @@ __device__ __forceinline__ Vec<C, R> splat(R a) {
 // the C cells of one lane (j0 is a multiple of C, C divides the tile).  D_ is in scope
 // wherever these are used; D_ = 0 for contiguous arrays.
 #define LD(p, j, n) ld<C, NT, R>(reinterpret_cast<const R *>(p) + D_, j, n)
-#define ST(p, j, n, ...) st<C, NT, R>(reinterpret_cast<R *>(p) + D_, j, n, __VA_ARGS__, ST_T_)
-// FCX_EDGE_TEMPORAL (A/B): in halo tiles, the lanes whose 16-B stores fall in the first or the
-// last 128-B line of the wave's own cells -- lines the neighbouring wave writes the rest of --
-// store without the non-temporal hint
-#ifndef FCX_EDGE_TEMPORAL
-#define FCX_EDGE_TEMPORAL 0
-#endif
+#define ST(p, j, n, ...) st<C, NT, R>(reinterpret_cast<R *>(p) + D_, j, n, __VA_ARGS__)
 
 // Momentum of one (type, u- or v-grid) cell group; `north` selects VMOM.
 struct NoEmit {
@@ -139,8 +130,7 @@ template <int C, bool NT, class R, class Emit>
 __device__ __forceinline__ void momentum(int8_t m, bool north, const UVGridPtrs &g,
                                          const Vec<C, R> &ts, const Vec<C, R> &ps, const Vec<C, R> &u,
                                          const Vec<C, R> &v, const Vec<C, R> &vel, const Vec<C, R> &qs,
-                                         const Vec<C, R> &a, int64_t j0, int64_t n, int64_t D_, Emit &emit, int slot,
-                                         bool ST_T_ = false);
+                                         const Vec<C, R> &a, int64_t j0, int64_t n, int64_t D_, Emit &emit, int slot);
 
 template <int C, bool NT, class R>
 __device__ __forceinline__ void momentum(int8_t m, bool north, const UVGridPtrs &g,
@@ -155,8 +145,7 @@ template <int C, bool NT, class R, class Emit>
 __device__ __forceinline__ void momentum(int8_t m, bool north, const UVGridPtrs &g,
                                          const Vec<C, R> &ts, const Vec<C, R> &ps, const Vec<C, R> &u,
                                          const Vec<C, R> &v, const Vec<C, R> &vel, const Vec<C, R> &qs,
-                                         const Vec<C, R> &a, int64_t j0, int64_t n, int64_t D_, Emit &emit, int slot,
-                                         bool ST_T_) {
+                                         const Vec<C, R> &a, int64_t j0, int64_t n, int64_t D_, Emit &emit, int slot) {
   if (!g.mom) return;
   Vec<C, R> out;
   if (m == FCX_ZERO) {
@@ -182,7 +171,6 @@ __device__ __forceinline__ void momentum(int8_t m, bool north, const UVGridPtrs 
 template <int C, bool NT, class R>
 __device__ __forceinline__ void uv_grid(const TypeParams &tp, int k, uint32_t stages, int64_t j0,
                                         int64_t n, int64_t D_) {
-  constexpr bool ST_T_ = false;
   const UVGridPtrs &g = tp.uv[k];
   const uint32_t s_qsur = k == 0 ? S_QSUR_U : S_QSUR_V;
   const uint32_t s_mom = k == 0 ? S_UMOM : S_VMOM;
@@ -350,12 +338,6 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
       return emit_in;
   }();
   const int64_t D_ = (j0 >> kLayoutShift) * P->tpad;  // field layout shift of this lane's cells
-  bool ST_T_ = false;  // FCX_EDGE_TEMPORAL: this lane's stores share a line with the next / previous wave
-  if constexpr (HALO && FCX_EDGE_TEMPORAL) {
-    const int64_t t0 = j0 - (int64_t)C * (threadIdx.x & 63), e1 = ns - 1;
-    auto line = [&](int64_t j) { return ((j + (j >> kLayoutShift) * P->tpad) * (int64_t)sizeof(R)) >> 7; };
-    ST_T_ = line(j0) == line(t0) || line(j0 + C - 1) == line(e1);
-  }
   Vec<C, R> corr = {};  // the month slice is a plain contiguous array
   if (do_t && corr_m && (stages & S_MEVA)) corr = ld<C, NT, R>(reinterpret_cast<const R *>(corr_m), j0, nt);
   Vec<C, R> rsdd = {};
@@ -398,20 +380,16 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
   // SIMD, no spills.  In one process over the same arrays (profiles/r03/ab_t2_prefetch.json,
   // random map): T = 2 step 1.672 -> 1.625 ms, CCLM 5.14 -> 5.26 TB/s, MOM5 5.54 -> 5.67,
   // RCO 5.26 -> 5.50.
-#ifndef FCX_PREFETCH
-#define FCX_PREFETCH 1
-#endif
-  constexpr bool kPrefetch = kReload && FCX_PREFETCH;
+  constexpr bool kPrefetch = kReload;
   // Multi-type CCLM / MOM5 kernels: the atmosphere-only terms of the formulas are formed once
   // per cell, when the type's atmosphere fields are (re)loaded, instead of once per type:
   // T_a * EF (HSEN's pow, ta_exner) and, for CCLM, whose coefficients AMOI / AMOM are
   // atmosphere fields too, a * max(vel, u_min) * p_s (MEVA, HSEN) and a * vel * p_s
   // (momentum).  Same operations on the same values, so the same bits (fcx_physics.h); the
   // type loop loses its pow and PATM / AMOI / AMOM / the wind speed need not stay live.
-#ifndef FCX_DERIVE  // A/B: 0 = every type forms its own terms (round 3)
-#define FCX_DERIVE 1
-#endif
-  constexpr bool kDerive = FCX_DERIVE && TM == 0 && (VAR == 1 || VAR == 2);
+  // (round 4, in one process over the same arrays, profiles/r04/ab_derive_t2.json: T = 2 step
+  // 1.665 -> 1.628 ms, MOM5 0.616 -> 0.582 ms, CCLM 0.595 -> 0.588 ms)
+  constexpr bool kDerive = TM == 0 && (VAR == 1 || VAR == 2);
   Vec<C, R> taef = {}, amv = {}, mvp = {};
   Vec<C, R> n_ts = {}, n_fi = {}, n_cmoi = {}, n_chea = {}, n_cmom = {}, n_fare = {};
   auto prefetch = [&](int s2) {
@@ -633,10 +611,8 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
             }
           } else {
             const Vec<C, R> &a = (m_mo == FCX_MOM5) ? cmom : amom;
-            if (do_u)
-              momentum<C, NT, R>(m_mo, false, tp.uv[0], ts, ps, u, v, vel, qs, a, j0, ns, D_, sink, A_UMOM, ST_T_);
-            if (do_v)
-              momentum<C, NT, R>(m_mo, true, tp.uv[1], ts, ps, u, v, vel, qs, a, j0, ns, D_, sink, A_VMOM, ST_T_);
+            if (do_u) momentum<C, NT, R>(m_mo, false, tp.uv[0], ts, ps, u, v, vel, qs, a, j0, ns, D_, sink, A_UMOM);
+            if (do_v) momentum<C, NT, R>(m_mo, true, tp.uv[1], ts, ps, u, v, vel, qs, a, j0, ns, D_, sink, A_VMOM);
           }
         }
       }

@@ -13,7 +13,7 @@ all-reduce per step completes them.
 import numpy as np
 
 from .basic import PHASE_ALL, PHASE_NORMAL
-from .engine import Engine
+from .engine import Engine, run_group
 from .parallel import BlockedRandomAtmosMap, PeriodicAtmosMap, apple_range
 from .synthetic import BASE_SEED, as_dtype, build_case, inputs_for_bench
 
@@ -112,6 +112,18 @@ class Workload:
                 ev[1].record(self.stream)
             if self.la is not None:
                 e.run_atmos(PHASE_ALL)
+
+    def run_group(self, t, event=None):
+        """One coupling step of every variant with their flux passes merged into ONE launch
+        (fcx_run_group); event = (start, end) recorded around it, or None."""
+        if event is not None:
+            event[0].record(self.stream)
+        run_group(self.engines, PHASE_ALL, t)
+        if event is not None:
+            event[1].record(self.stream)
+        if self.la is not None:
+            for e in self.engines:
+                e.run_atmos(PHASE_ALL)  # (a no-op where the accumulation rode in the launch)
 
     def finish(self):
         """After the all-reduce of `shared`: the completed boundary sums into the outputs."""
