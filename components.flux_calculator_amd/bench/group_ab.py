@@ -26,11 +26,16 @@ def main():
     ap.add_argument("--atmos-map", choices=("random", "periodic"), default="random")
     ap.add_argument("--rounds", type=int, default=8)
     ap.add_argument("--steps", type=int, default=20, help="steps per block")
+    ap.add_argument("--variants", default="CCLM,MOM5,RCO")
+    ap.add_argument("--lib", default=None, help="another libfcx build (A/B of the group kernel)")
     a = ap.parse_args()
     import torch
+    if a.lib:
+        os.environ["FCX_LIBRARY"] = a.lib
     from fcx.workload import Workload
 
-    wl = Workload(a.cells, 0, 1, types=a.types, precision=a.precision, atmos=True, atmos_map=a.atmos_map)
+    wl = Workload(a.cells, 0, 1, variants=tuple(a.variants.split(",")), types=a.types, precision=a.precision,
+                  atmos=True, atmos_map=a.atmos_map)
     s = wl.stream
     runs = {"group": lambda t: wl.run_group(t), "per_engine": lambda t: wl.run(t)}
     t_w = time.perf_counter()

@@ -1040,7 +1040,14 @@ __global__ __launch_bounds__(64 * atmos_waves<C>(), RAVG  ? FCX_RAVG_ATMOS_BLOCK
 template <int C, class R, bool NT, bool HALO, int TM = 1, bool RAVG = false>
 __global__ __launch_bounds__(64 * atmos_waves<C>(), RAVG ? FCX_RAVG_ATMOS_BLOCKS
                                                     : C == 4 ? FCX_F32_ATMOS_BLOCKS : FCX_GROUP_BLOCKS) void
-cells_atmos_group_kernel(const GroupArgs g) {
+cells_atmos_group_kernel(const GroupArgs g, const Params *__restrict__ P0, const Params *__restrict__ P1,
+                         const Params *__restrict__ P2, const Params *__restrict__ P3) {
+  // The members' parameter blocks are separate const __restrict__ kernel arguments (not the
+  // pointers inside GroupArgs): the compiler then knows the blocks are not written by the
+  // launch and reads them with scalar loads, as in cells_atmos_kernel.  Read through a
+  // pointer out of the argument struct, every field was a vector load (and a dependent
+  // round trip before the field loads): the group kernel took 1.156 ms against 0.783 ms
+  // for the three launches it replaced (profiles/r04/gdiag/).
   constexpr int kRows = RAVG ? kAvgSlots : kFusedFields;
   __shared__ double s_p[atmos_waves<C>()][wave_lds_doubles<R, C>(kRows)];
   const int wv = threadIdx.x >> 6;
@@ -1057,11 +1064,12 @@ cells_atmos_group_kernel(const GroupArgs g) {
       if (t >= g.m[q].tile0) k = q;
     k = __builtin_amdgcn_readfirstlane(k);
     const GroupMember &m = g.m[k];
+    const Params *__restrict__ P = k == 0 ? P0 : k == 1 ? P1 : k == 2 ? P2 : P3;
     const int64_t tile = t - m.tile0;
     switch (m.var) {
-      case 1: atmos_tile<C, R, 1, NT, TM, RAVG, false, HALO>(m.P, m.corr_m, m.af, tile, wp); break;
-      case 2: atmos_tile<C, R, 2, NT, TM, RAVG, false, HALO>(m.P, m.corr_m, m.af, tile, wp); break;
-      default: atmos_tile<C, R, 3, NT, TM, RAVG, false, HALO>(m.P, m.corr_m, m.af, tile, wp); break;
+      case 1: atmos_tile<C, R, 1, NT, TM, RAVG, false, HALO>(P, m.corr_m, m.af, tile, wp); break;
+      case 2: atmos_tile<C, R, 2, NT, TM, RAVG, false, HALO>(P, m.corr_m, m.af, tile, wp); break;
+      default: atmos_tile<C, R, 3, NT, TM, RAVG, false, HALO>(P, m.corr_m, m.af, tile, wp); break;
     }
   }
 }
@@ -1497,17 +1505,21 @@ int launch_cells(const Params *hp, const Params *dp, const double *corr_m, const
 
 template <int C, class R, bool NT>
 static void launch_group_h(bool halo, bool ravg, int blocks, hipStream_t s, const GroupArgs &g) {
+  const Params *p[kMaxGroup];
+  for (int k = 0; k < kMaxGroup; ++k) p[k] = g.m[k < g.n ? k : 0].P;
   if constexpr (C == 2) {
     if (ravg) {  // several surface types, the type-0 averages in registers (no halo tiles)
       hipLaunchKernelGGL((cells_atmos_group_kernel<C, R, NT, false, 0, true>), dim3(blocks),
-                         dim3(64 * atmos_waves<C>()), 0, s, g);
+                         dim3(64 * atmos_waves<C>()), 0, s, g, p[0], p[1], p[2], p[3]);
       return;
     }
   }
   if (halo)
-    hipLaunchKernelGGL((cells_atmos_group_kernel<C, R, NT, true>), dim3(blocks), dim3(64 * atmos_waves<C>()), 0, s, g);
+    hipLaunchKernelGGL((cells_atmos_group_kernel<C, R, NT, true>), dim3(blocks), dim3(64 * atmos_waves<C>()), 0, s, g,
+                       p[0], p[1], p[2], p[3]);
   else
-    hipLaunchKernelGGL((cells_atmos_group_kernel<C, R, NT, false>), dim3(blocks), dim3(64 * atmos_waves<C>()), 0, s, g);
+    hipLaunchKernelGGL((cells_atmos_group_kernel<C, R, NT, false>), dim3(blocks), dim3(64 * atmos_waves<C>()), 0, s,
+                       g, p[0], p[1], p[2], p[3]);
 }
 
 int launch_cells_group(GroupMember *members, int n, const LaunchConfig &lc, void *stream) {

@@ -1,7 +1,7 @@
-"""libfcx's own collective (fcx_comm_*, include/fcx.h) on the GPU box: an RCCL communicator
-through the C ABI, world size 1 (one GPU per box; RCCL refuses two ranks on one device --
-the N > 1 numerics of the same boundary slots run over gloo in test_gpu_multirank.py and
-on the CPU in test_partition_multirank.py, and the 8-GPU run is bench.py's).
+"""libfcx's own collective (fcx_comm_*, include/fcx.h) on the GPU box: a real RCCL
+communicator through the C ABI, world size 1 (one GPU per box; RCCL refuses two ranks on one
+device -- libfcx's exchange with 2 and 3 ranks runs through a librccl stand-in in
+test_gpu_exchange_ranks.py, and the 8-GPU run is bench.py's).
 
 With one rank the all-reduce is the identity, so an engine given a boundary slot for its
 last atmosphere cell must come out bit-identical to the sequential SCRIP sum after the
@@ -114,12 +114,13 @@ def test_one_allreduce_for_three_variants():
 @pytest.mark.parametrize("layout", ["separate_buffers", "gapped_buffer", "reversed_adjacent"])
 @pytest.mark.parametrize("streams", ["one", "per_engine"])
 def test_atmos_allreduce_regions_and_streams(layout, streams):
-    """fcx_atmos_allreduce over three engines whose boundary-slot regions are NOT adjacent in
-    one buffer (separate buffers, or one buffer with gaps: one all-reduce per engine inside one
-    RCCL group) or adjacent in reverse engine order (one call from the lowest address), with
-    the engines on one stream or each on its own stream (the all-reduce on the first engine's
-    stream waits for the others' accumulations, and each engine's finish waits for it).  One
-    rank: every atmosphere cell bit-identical to the sequential sum, every slot re-zeroed."""
+    """fcx_atmos_allreduce over three engines whose boundary-slot regions do not follow each
+    other in list order in one buffer (separate buffers, one buffer with gaps, or adjacent in
+    reverse engine order): the slots are packed through the communicator's scratch for the
+    one all-reduce and copied back; with the engines on one stream or each on its own stream
+    (the all-reduce on the first engine's stream waits for the others' accumulations, and each
+    engine's finish waits for it).  One rank: every atmosphere cell bit-identical to the
+    sequential sum, every slot re-zeroed.  (2 and 3 ranks: tests/test_gpu_exchange_ranks.py.)"""
     import torch
     from fcx.comm import Comm, unique_id
     from fcx.engine import Engine
