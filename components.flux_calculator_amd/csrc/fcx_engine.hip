@@ -262,6 +262,10 @@ struct fcx_engine {
   // the device pools that hold their mirrors, allocated at the first staged transfer
   bool staging = true;
   bool deferred_scatter = false;        // FCX_OPT_DEFERRED_SCATTER: downloads scattered at fcx_synchronize
+#ifdef FCX_AB_BUILD
+  bool ab_fixup_each = false;
+  bool ab_no_head = false;
+#endif
   int host_threads = 0;                 // FCX_OPT_HOST_THREADS (0: default_host_threads)
   std::vector<StagePool> spools;
   std::vector<Xfer> pending_out;        // D2H into the arena whose scatter waits for the stream
@@ -709,6 +713,9 @@ static void plan_fused_atmos(fcx_engine *e, Plan &pl, uint32_t stages, int phase
   af.w = e->d_atm_w;
   af.xrec = e->d_atm_xrec;
   af.xrec_on = e->atm_crossings > 0;
+#ifdef FCX_AB_BUILD
+  if (e->ab_no_head) af.xrec_on = 0;
+#endif
   af.n_atmos = e->n_atmos;
   af.shared = e->atm_shared;
   af.stride = e->atm_stride;
@@ -2231,8 +2238,30 @@ extern "C" int fcx_run_group(fcx_engine *const *es, int n, int phase, int32_t t)
   }
   const int r = launch_cells_group(gm, (int)mem.size(), mem[0].lc, mem[0].e->stream);
   if (r) return fail(FCX_E_HIP, "cells_atmos_group_kernel launch: %s", hipGetErrorString((hipError_t)r));
+  // the members' crossing-record fix-ups (launch_fixup's rule) as one launch
+  AtmosFused fx[kMaxGroup];
+  int64_t fx_n[kMaxGroup];
+  int nfx = 0;
+#ifdef FCX_AB_BUILD
+  if (mem[0].e->ab_fixup_each) {
+    for (const Member &m : mem) {
+      if (int r2 = launch_fixup(m.e, m.pl, m.lc)) return r2;
+      m.e->atm_done_fused = true;
+      if (int r2 = run_tail(m.e, phase)) return r2;
+    }
+    return FCX_OK;
+  }
+#endif
+  for (const Member &m : mem)
+    if (m.e->atm_crossings > 0 && m.lc.halo == 0) {
+      fx[nfx] = m.pl->af;
+      fx_n[nfx++] = m.pl->host.n_max;
+    }
+  if (nfx) {
+    const int r2 = launch_atmos_fixup_group(fx, fx_n, nfx, mem[0].lc.f32, mem[0].e->stream);
+    if (r2) return fail(FCX_E_HIP, "atmos_fixup_group launch: %s", hipGetErrorString((hipError_t)r2));
+  }
   for (const Member &m : mem) {
-    if (int r2 = launch_fixup(m.e, m.pl, m.lc)) return r2;
     m.e->atm_done_fused = true;
     if (int r2 = run_tail(m.e, phase)) return r2;
   }
@@ -2691,6 +2720,15 @@ extern "C" int fcx_set_option(fcx_engine *e, int option, int64_t value) {
       // removed in version 3 (nothing of the caller's memory is page-locked; the in-launch
       // carry hand-off is gone): accepted and ignored, so hosts that set them still run
       return FCX_OK;
+#ifdef FCX_AB_BUILD
+    case 98:  // measurement builds: no head records (wrong crossing values; cost of the stores)
+      e->ab_no_head = value != 0;
+      for (auto &kv : e->plans) kv.second.af.xrec_on = !e->ab_no_head && e->atm_crossings > 0;
+      return FCX_OK;
+    case 99:  // measurement builds: the group's fix-ups as one launch per member (old path)
+      e->ab_fixup_each = value != 0;
+      return FCX_OK;
+#endif
     default:
       return fail(FCX_E_ARG, "option %d unknown", option);
   }

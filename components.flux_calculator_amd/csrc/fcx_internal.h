@@ -247,6 +247,14 @@ int launch_cells_group(GroupMember *members, int n, const LaunchConfig &lc, void
 // the segments carried over a tile boundary: carry of tile t-1 + the head cells of tile t,
 // for every tile of a launch of n_cells (fp32: 256-cell tiles of float fields)
 int launch_atmos_fixup(const AtmosFused &af, int64_t n_cells, bool f32, void *stream);
+// the fix-ups of several engines' fused launches (fcx_run_group members) as one launch
+struct FixupGroup {
+  int32_t n;
+  int32_t pad;
+  int64_t first[kMaxGroup + 1];  // member m's (tile boundary, field) threads: [first[m], first[m+1])
+  AtmosFused af[kMaxGroup];
+};
+int launch_atmos_fixup_group(const AtmosFused *afs, const int64_t *n_cells, int n, bool f32, void *stream);
 int launch_atmos_finish(const AtmosArgs &a, int32_t n_boundaries, void *stream);
 
 // f32: w, src and dst are float arrays (the reference's single-precision build, where the

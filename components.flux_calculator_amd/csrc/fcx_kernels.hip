@@ -1081,14 +1081,12 @@ cells_atmos_group_kernel(const GroupArgs g, const Params *__restrict__ P0, const
 // the in-launch sum.  Cells of a longer head are recomputed from the stored fluxes with the
 // kernel's own operation (w * x, fp32 fluxes widened).
 // Segments are at most half a tile (the fused path's rule), so a carry never spans a tile.
+// field k of the segment across tile boundary t (tile t's crossing record)
 template <class R, int kT>
-__global__ __launch_bounds__(256) void atmos_fixup_kernel(const AtmosFused af, int64_t n_tiles) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t t = 1 + i / kFusedFields;
-  const int k = (int)(i % kFusedFields);
-  if (t >= n_tiles || !af.out[k]) return;
+__device__ __forceinline__ void fixup_one(const AtmosFused &af, int64_t t, int k) {
   // one crossing record (two lines) holds everything of the common case: every load issued
-  // before the head count is known, one memory round trip
+  // before the head count is known, one memory round trip.  (One thread per boundary with
+  // the whole record in 16-B loads measured the same: profiles/r04/inproc3/.)
   const int64_t x0 = t * kT;
   const double *rec = af.xrec + t * kXRec;
   const int2 ha = *reinterpret_cast<const int2 *>(rec + 30);
@@ -1104,15 +1102,37 @@ __global__ __launch_bounds__(256) void atmos_fixup_kernel(const AtmosFused af, i
     if (e < h) acc = acc + p[e];
   const R *xk = reinterpret_cast<const R *>(af.x[k]);
   for (int e = kRecHead; e < h; ++e) acc = acc + af.w[x0 + e] * (double)xk[tiled(x0 + e, af.tpad)];
-#ifndef FCX_FIXUP_NT  // A/B: non-temporal fix-up stores
-#define FCX_FIXUP_NT 0
-#endif
-  if (FCX_FIXUP_NT)
-    __builtin_nontemporal_store((R)acc, reinterpret_cast<R *>(af.out[k]) + tiled(a, af.out_tpad));
-  else
-    reinterpret_cast<R *>(af.out[k])[tiled(a, af.out_tpad)] = (R)acc;
+  reinterpret_cast<R *>(af.out[k])[tiled(a, af.out_tpad)] = (R)acc;
   if (a == 0 && af.left >= 0) af.shared[(int64_t)af.left * af.stride + af.scol[k]] = acc;
   if (a == af.n_atmos - 1 && af.right >= 0) af.shared[(int64_t)af.right * af.stride + af.scol[k]] = acc;
+}
+
+template <class R, int kT>
+__global__ __launch_bounds__(256) void atmos_fixup_kernel(const AtmosFused af, int64_t n_tiles) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t t = 1 + i / kFusedFields;
+  const int k = (int)(i % kFusedFields);
+  if (t >= n_tiles || !af.out[k]) return;
+  fixup_one<R, kT>(af, t, k);
+}
+
+// The fix-ups of a group launch's members (fcx_run_group) as ONE launch: member m's
+// (boundary, field) threads are [first[m], first[m + 1]).  Each dependent launch costs the
+// step its predecessor's drain, the dispatch and the ramp on top of its work: in one process
+// over the same arrays, T = 2 group step 1.560 against 1.566 ms with one fix-up launch per
+// member, T = 1 without halo tiles 0.759 against 0.766 ms (profiles/r04/inproc1/).
+template <class R, int kT>
+__global__ __launch_bounds__(256) void atmos_fixup_group_kernel(const FixupGroup g) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= g.first[g.n]) return;
+  int m = 0;
+  for (int q = 1; q < g.n; ++q)
+    if (i >= g.first[q]) m = q;
+  const int64_t j = i - g.first[m];
+  const int64_t t = 1 + j / kFusedFields;
+  const int k = (int)(j % kFusedFields);
+  if (!g.af[m].out[k]) return;
+  fixup_one<R, kT>(g.af[m], t, k);
 }
 
 // do_regridding (basic:463-522) as CSR-by-destination: row d holds the links with
@@ -1615,6 +1635,26 @@ int launch_atmos_fixup(const AtmosFused &af, int64_t n, bool f32, void *stream) 
     hipLaunchKernelGGL((atmos_fixup_kernel<float, tile_cells<4>()>), dim3(blocks), dim3(256), 0, s, af, tiles);
   else
     hipLaunchKernelGGL((atmos_fixup_kernel<double, tile_cells<2>()>), dim3(blocks), dim3(256), 0, s, af, tiles);
+  return (int)hipGetLastError();
+}
+
+int launch_atmos_fixup_group(const AtmosFused *afs, const int64_t *n_cells, int n, bool f32, void *stream) {
+  if (n < 1 || n > kMaxGroup) return (int)hipErrorInvalidValue;
+  const int64_t kt = f32 ? tile_cells<4>() : tile_cells<2>();
+  FixupGroup g{};
+  g.n = n;
+  for (int m = 0; m < n; ++m) {
+    g.af[m] = afs[m];
+    const int64_t tiles = (n_cells[m] + kt - 1) / kt;
+    g.first[m + 1] = g.first[m] + std::max<int64_t>(tiles - 1, 0) * kFusedFields;
+  }
+  if (g.first[n] == 0) return 0;
+  const int blocks = (int)((g.first[n] + 255) / 256);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (f32)
+    hipLaunchKernelGGL((atmos_fixup_group_kernel<float, tile_cells<4>()>), dim3(blocks), dim3(256), 0, s, g);
+  else
+    hipLaunchKernelGGL((atmos_fixup_group_kernel<double, tile_cells<2>()>), dim3(blocks), dim3(256), 0, s, g);
   return (int)hipGetLastError();
 }
 

@@ -121,7 +121,7 @@ class Engine:
                     _lib.check(self.lib.fcx_add_remap_field(h, rid.value, phase, s, g, IDX[name],
                                                             ctypes.c_void_p(data_ptr(out)), flags))
             for name, value in (options or {}).items():
-                _lib.check(self.lib.fcx_set_option(h, self.OPTIONS[name], int(value)))
+                _lib.check(self.lib.fcx_set_option(h, self._option_id(name), int(value)))
             _lib.check(self.lib.fcx_commit(h))
         except Exception:
             self.lib.fcx_destroy(h)
@@ -197,8 +197,15 @@ class Engine:
         _lib.check(self.lib.fcx_remap_info(self.h, remap_id, ctypes.byref(sc), ctypes.byref(pk)))
         return sc.value, pk.value
 
+    @classmethod
+    def _option_id(cls, name):
+        """an OPTIONS name, or a raw enum fcx_option value (measurement builds' extra knobs)"""
+        if isinstance(name, int) or (isinstance(name, str) and name.isdigit()):
+            return int(name)
+        return cls.OPTIONS[name]
+
     def set_option(self, name, value):
-        _lib.check(self.lib.fcx_set_option(self.h, self.OPTIONS[name], int(value)))
+        _lib.check(self.lib.fcx_set_option(self.h, self._option_id(name), int(value)))
 
     def device_ptr(self, s, g, name):
         p = ctypes.POINTER(ctypes.c_double)()
