@@ -230,6 +230,66 @@ def e2e_host(args, variants, sizes=(10_000_000, 32_768)):
     return out
 
 
+def e2e_concurrent(args, variants, n=32_768, steps=500):
+    """The drop-in as the reference deploys it: every bottom model's flux_calculator is its
+    own MPI task (flux_calculator.F90:275-298), so the variants' steps run side by side.  One
+    engine per variant on its own HIP stream, driven by its own host thread (ctypes releases
+    the GIL in fcx_step); a step = all of them from a common start to the last one done, each
+    from its caller heap arrays with the default transport.  Wall time per step."""
+    import threading
+
+    import torch
+    from fcx.basic import PHASE_ALL
+    from fcx.engine import Engine
+    from fcx.synthetic import build_case, inputs_for_bench
+
+    data = inputs_for_bench(n)
+    streams = [torch.cuda.Stream() for _ in variants]
+    cases = [build_case(v, n=n, T=args.types, bias=args.bias, data=data if args.types == 1 else None)
+             for v in variants]
+    engines = [Engine(c.lf, c.num_surface_types, c.methods, corrections=c.corrections, averages=c.averages,
+                      stream=st.cuda_stream) for c, st in zip(cases, streams)]
+    total = 50 + steps
+    start, done = threading.Barrier(len(engines) + 1), threading.Barrier(len(engines) + 1)
+    errors = []
+
+    def worker(e):
+        try:
+            for k in range(total):
+                start.wait()
+                e.step(PHASE_ALL, k * 3600)
+                done.wait()
+        except Exception as ex:  # noqa: BLE001 -- reported by the main thread
+            errors.append(ex)
+            start.abort()
+            done.abort()
+
+    threads = [threading.Thread(target=worker, args=(e,)) for e in engines]
+    for t in threads:
+        t.start()
+    ts = []
+    try:
+        for k in range(total):
+            start.wait()
+            t0 = time.perf_counter()
+            done.wait()
+            if k >= 50:  # first touch, plans, arenas, clocks
+                ts.append(time.perf_counter() - t0)
+    except threading.BrokenBarrierError:
+        pass
+    for t in threads:
+        t.join()
+    for e in engines:
+        e.close()
+    if errors:
+        raise errors[0]
+    med = float(np.median(ts))
+    return {"us_per_step_median": round(med * 1e6, 1), "us_per_step_p90": round(float(np.percentile(ts, 90)) * 1e6, 1),
+            "steps": steps, "engines": len(engines),
+            "rule": "every variant's engine on its own stream and host thread, side by side as the reference's "
+                    "per-bottom-model MPI tasks; a step = common start to the last engine done"}
+
+
 def relaunch(n):
     """`python bench.py --gpus N` outside a launcher: run this same command under
     torch.distributed.run (one rank per GPU, rendezvous on 127.0.0.1) as a child process,
@@ -615,6 +675,9 @@ def main():
                 "gpu_vs_all_cores": round(cp["us_per_step"] / gpu_us, 2),
                 "rule": "one coupling step of every variant from the caller's host arrays (e2e, fcx_step with the "
                         "default transport) against the reference on this box's host cores, same grid size"}
+            conc = e2e_concurrent(args, variants)
+            out["baltic_size"]["gpu_dropin_concurrent"] = conc
+            out["baltic_size"]["gpu_concurrent_vs_all_cores"] = round(cp["us_per_step"] / conc["us_per_step_median"], 2)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if comm is not None:

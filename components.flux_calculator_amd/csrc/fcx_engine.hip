@@ -199,6 +199,10 @@ struct fcx_engine {
   bool atm_contiguous = true;
   int32_t *d_atm_row = nullptr, *d_atm_col = nullptr, *d_atm_idx = nullptr;
   std::vector<int32_t> atm_idx;
+  // atmosphere cells without exchange cells (land, on a real intersection grid): the fused
+  // accumulation has no segment for them, so their zero sums are stored after its launch
+  std::vector<int32_t> atm_empty;
+  int32_t *d_atm_empty = nullptr;
   int32_t atm_maxseg = 0;
   double *d_atm_xrec = nullptr;    // [tiles][kXRec] crossing records (fix-up kernel)
   int64_t atm_crossings = 0;       // 128-cell tile boundaries inside a segment of the map
@@ -376,6 +380,7 @@ extern "C" int fcx_destroy(fcx_engine *e) {
   (void)hipFree(e->corr_dev);
   (void)hipFree(e->d_atm_row);
   (void)hipFree(e->d_atm_idx);
+  (void)hipFree(e->d_atm_empty);
   (void)hipFree(e->d_atm_xrec);
   (void)hipFree(e->d_atm_col);
   (void)hipFree(e->d_atm_w);
@@ -1747,6 +1752,11 @@ extern "C" int fcx_commit(fcx_engine *e) {
       // tile) means no fix-up launch at all
       e->atm_crossings = 0;
       for (size_t b = kTile; b < e->atm_idx.size(); b += kTile) e->atm_crossings += e->atm_idx[b - 1] == e->atm_idx[b];
+      if (!e->atm_empty.empty()) {
+        HIP_TRY(hipMalloc(&e->d_atm_empty, e->atm_empty.size() * sizeof(int32_t)));
+        HIP_TRY(hipMemcpy(e->d_atm_empty, e->atm_empty.data(), e->atm_empty.size() * sizeof(int32_t),
+                          hipMemcpyHostToDevice));
+      }
     }
     if (!e->atm_contiguous) {
       HIP_TRY(hipMalloc(&e->d_atm_col, std::max<size_t>(e->atm_col.size(), 1) * sizeof(int32_t)));
@@ -1925,7 +1935,15 @@ static LaunchConfig plan_launch(fcx_engine *e, Plan *pl, int64_t lo, int64_t hi,
 }
 
 // the crossing records' fix-up after a fused launch over the whole grid without halo tiles
+static int launch_empty_cells(fcx_engine *e, Plan *pl, const LaunchConfig &lc) {
+  if (e->atm_empty.empty()) return FCX_OK;
+  const int r = launch_atmos_zero(pl->af, e->d_atm_empty, (int64_t)e->atm_empty.size(), lc.f32, e->stream);
+  if (r) return fail(FCX_E_HIP, "atmos_zero launch: %s", hipGetErrorString((hipError_t)r));
+  return FCX_OK;
+}
+
 static int launch_fixup(fcx_engine *e, Plan *pl, const LaunchConfig &lc) {
+  if (int r = launch_empty_cells(e, pl, lc)) return r;
   if (e->atm_crossings <= 0 || lc.halo) return FCX_OK;
   const int r = launch_atmos_fixup(pl->af, pl->host.n_max, lc.f32, e->stream);
   if (r) return fail(FCX_E_HIP, "atmos_fixup launch: %s", hipGetErrorString((hipError_t)r));
@@ -2261,6 +2279,8 @@ extern "C" int fcx_run_group(fcx_engine *const *es, int n, int phase, int32_t t)
     const int r2 = launch_atmos_fixup_group(fx, fx_n, nfx, mem[0].lc.f32, mem[0].e->stream);
     if (r2) return fail(FCX_E_HIP, "atmos_fixup_group launch: %s", hipGetErrorString((hipError_t)r2));
   }
+  for (const Member &m : mem)
+    if (int r2 = launch_empty_cells(m.e, m.pl, m.lc)) return r2;
   for (const Member &m : mem) {
     m.e->atm_done_fused = true;
     if (int r2 = run_tail(m.e, phase)) return r2;
@@ -2753,7 +2773,11 @@ extern "C" int fcx_set_atmos_map(fcx_engine *e, int64_t n_atmos, const int32_t *
   e->n_atmos = n_atmos;
   e->atm_idx.assign(idx, idx + n);
   e->atm_maxseg = 0;
-  for (int64_t a = 0; a < n_atmos; ++a) e->atm_maxseg = std::max(e->atm_maxseg, count[(size_t)a + 1]);
+  e->atm_empty.clear();
+  for (int64_t a = 0; a < n_atmos; ++a) {
+    e->atm_maxseg = std::max(e->atm_maxseg, count[(size_t)a + 1]);
+    if (count[(size_t)a + 1] == 0) e->atm_empty.push_back((int32_t)a);
+  }
   e->atm_row.assign((size_t)n_atmos + 1, 0);
   for (int64_t a = 0; a < n_atmos; ++a) e->atm_row[(size_t)a + 1] = e->atm_row[(size_t)a] + count[(size_t)a + 1];
   e->atm_contiguous = sorted;

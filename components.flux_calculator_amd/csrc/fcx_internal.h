@@ -247,6 +247,8 @@ int launch_cells_group(GroupMember *members, int n, const LaunchConfig &lc, void
 // the segments carried over a tile boundary: carry of tile t-1 + the head cells of tile t,
 // for every tile of a launch of n_cells (fp32: 256-cell tiles of float fields)
 int launch_atmos_fixup(const AtmosFused &af, int64_t n_cells, bool f32, void *stream);
+// zero the fused outputs of the n atmosphere cells in cells[] (cells without exchange cells)
+int launch_atmos_zero(const AtmosFused &af, const int32_t *cells, int64_t n, bool f32, void *stream);
 // the fix-ups of several engines' fused launches (fcx_run_group members) as one launch
 struct FixupGroup {
   int32_t n;

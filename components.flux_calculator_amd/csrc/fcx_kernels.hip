@@ -1638,6 +1638,29 @@ int launch_atmos_fixup(const AtmosFused &af, int64_t n, bool f32, void *stream) 
   return (int)hipGetLastError();
 }
 
+// Atmosphere cells without exchange cells: the sequential SCRIP sum over no links is 0, and
+// the fused launch, which stores one value per segment, has none for them.
+template <class R>
+__global__ __launch_bounds__(256) void atmos_zero_kernel(const AtmosFused af, const int32_t *cells, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int32_t a = cells[i];
+#pragma unroll
+  for (int k = 0; k < kFusedFields; ++k)
+    if (af.out[k]) reinterpret_cast<R *>(af.out[k])[tiled(a, af.out_tpad)] = R(0);
+}
+
+int launch_atmos_zero(const AtmosFused &af, const int32_t *cells, int64_t n, bool f32, void *stream) {
+  if (n <= 0) return 0;
+  const int blocks = (int)((n + 255) / 256);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (f32)
+    hipLaunchKernelGGL(atmos_zero_kernel<float>, dim3(blocks), dim3(256), 0, s, af, cells, n);
+  else
+    hipLaunchKernelGGL(atmos_zero_kernel<double>, dim3(blocks), dim3(256), 0, s, af, cells, n);
+  return (int)hipGetLastError();
+}
+
 int launch_atmos_fixup_group(const AtmosFused *afs, const int64_t *n_cells, int n, bool f32, void *stream) {
   if (n < 1 || n > kMaxGroup) return (int)hipErrorInvalidValue;
   const int64_t kt = f32 ? tile_cells<4>() : tile_cells<2>();

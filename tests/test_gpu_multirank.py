@@ -82,8 +82,10 @@ def random_run_map(n, lengths, seed):
 # run lengths: 1..5, 1..7, 1..9 (halo tiles: 1, 3 and 4 halo lanes), 1..10 (one cell too long
 # for the halo: crossing records + fix-up), 20..64 (the fix-up; heads longer than the records'
 # kRecHead kept products are recomputed); 130..140 and 1..400 (longer than half a tile: the
-# engine runs atmos_kernel instead)
-@pytest.mark.parametrize("lengths", [(1, 5), (1, 7), (1, 9), (1, 10), (20, 64), (130, 140), (1, 400)])
+# engine runs atmos_kernel instead); 0..5 and 0..10: atmosphere cells without exchange cells
+# (land on an intersection grid) among them, whose sums are 0
+@pytest.mark.parametrize("lengths", [(1, 5), (1, 7), (1, 9), (1, 10), (20, 64), (130, 140), (1, 400), (0, 5),
+                                     (0, 10)])
 @pytest.mark.parametrize("mode", ["default", "nohalo", "capped", "pipelined", "pipelined_runtime"])
 def test_fused_accumulation_long_segments(lengths, mode):
     """The accumulation with segments crossing 128-cell wave tiles: completed inside the launch
@@ -119,7 +121,7 @@ def test_fused_accumulation_long_segments(lengths, mode):
     eng.close()
 
 
-@pytest.mark.parametrize("lengths", [(1, 5), (1, 9), (1, 10), (20, 64)])
+@pytest.mark.parametrize("lengths", [(1, 5), (1, 9), (1, 10), (20, 64), (0, 5)])
 @pytest.mark.parametrize("mode", ["default", "nohalo", "pipelined"])
 def test_fused_accumulation_of_averages_long_segments(lengths, mode):
     """Two surface types: the type-0 averages accumulated by the multi-type fused kernel on
