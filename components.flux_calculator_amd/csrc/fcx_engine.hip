@@ -1924,10 +1924,10 @@ static LaunchConfig plan_launch(fcx_engine *e, Plan *pl, int64_t lo, int64_t hi,
     // pipelined chunk) of one surface type, on a map whose segments are short enough that
     // `halo` lanes of the next tile's head (at most 1/16 of a wave) cover every crossing
     lc.halo = 0;
-    const int cpl = e->f32 ? 4 : 2;
+    const int cpl = e->f32 ? kF32Cpl : 2;
     const int h = (e->atm_maxseg - 1 + cpl - 1) / cpl;
     if (e->atm_halo && e->atm_crossings > 0 && lo == 0 && (hi < 0 || hi >= pl->host.n_max) &&
-        (pl->host.num_types == 1 || (FCX_HALO_RAVG && pl->host.ravg_on)) && h >= 1 && h <= (e->f32 ? 2 : 4))
+        (pl->host.num_types == 1 || (FCX_HALO_RAVG && pl->host.ravg_on)) && h >= 1 && h <= (cpl == 4 ? 2 : 4))
       lc.halo = h;
     pl->af.halo = lc.halo;
   }
@@ -2250,7 +2250,7 @@ extern "C" int fcx_run_group(fcx_engine *const *es, int n, int phase, int32_t t)
     e->atm_done = e->exchanged = false;
     e->rec_plan = nullptr;
     e->rec_written = false;
-    const int64_t own = (m.lc.f32 ? 4 : 2) * (64 - m.lc.halo);
+    const int64_t own = (m.lc.f32 ? kF32Cpl : 2) * (64 - m.lc.halo);
     gm[k] = GroupMember{m.pl->dev, m.corr_m, 0, m.lc.variant, 0, m.pl->af};
     gm[k].af.n_tiles = (m.pl->host.n_max + own - 1) / own;
   }

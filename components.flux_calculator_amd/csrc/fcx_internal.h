@@ -226,6 +226,12 @@ struct AtmosFused {
 // Several engines' fused T = 1 launches in ONE launch (fcx_run_group): member k's wave tiles
 // are tiles [tile0, tile0 + af.n_tiles) of the grid.  Passed by value (kernel arguments).
 constexpr int kMaxGroup = 4;
+// cells per lane of the fp32 engine's fused kernels (16-B lanes of 4 floats; A/B builds: 2,
+// 8-B lanes of 2 floats in 128-cell tiles like the fp64 kernels, half the registers per lane)
+#ifndef FCX_F32_CPL
+#define FCX_F32_CPL 4
+#endif
+constexpr int kF32Cpl = FCX_F32_CPL;
 struct GroupMember {
   const Params *P;        // the member's device parameter block
   const double *corr_m;   // its month slice, or nullptr

@@ -38,6 +38,7 @@ typedef double d2 __attribute__((ext_vector_type(2)));
 typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
 #endif
 typedef float f4 __attribute__((ext_vector_type(4)));
+typedef float f2v __attribute__((ext_vector_type(2)));
 typedef int i2v __attribute__((ext_vector_type(2)));
 typedef int i4v __attribute__((ext_vector_type(4)));
 
@@ -64,9 +65,9 @@ __device__ __forceinline__ FCX_GLOBAL T *gptr(T *p) {
 template <int C, bool NT, class R>
 __device__ __forceinline__ Vec<C, R> ld(const R *__restrict__ p, int64_t j0, int64_t n) {
   Vec<C, R> r;
-  if constexpr (C * sizeof(R) == 16) {
+  if constexpr (C * sizeof(R) == 16 || (C == 2 && sizeof(R) == 4)) {
     if (j0 + C <= n) {
-      using V = typename std::conditional<sizeof(R) == 8, d2, f4>::type;
+      using V = typename std::conditional<sizeof(R) == 8, d2, typename std::conditional<C == 4, f4, f2v>::type>::type;
       const FCX_GLOBAL V *q = gptr(reinterpret_cast<const V *>(p + j0));
       const V t = NT ? __builtin_nontemporal_load(q) : *q;
 #pragma unroll
@@ -81,9 +82,9 @@ __device__ __forceinline__ Vec<C, R> ld(const R *__restrict__ p, int64_t j0, int
 
 template <int C, bool NT, class R>
 __device__ __forceinline__ void st(R *__restrict__ p, int64_t j0, int64_t n, const Vec<C, R> &x) {
-  if constexpr (C * sizeof(R) == 16) {
+  if constexpr (C * sizeof(R) == 16 || (C == 2 && sizeof(R) == 4)) {
     if (j0 + C <= n) {
-      using V = typename std::conditional<sizeof(R) == 8, d2, f4>::type;
+      using V = typename std::conditional<sizeof(R) == 8, d2, typename std::conditional<C == 4, f4, f2v>::type>::type;
       FCX_GLOBAL V *q = gptr(reinterpret_cast<V *>(p + j0));
       V t;
 #pragma unroll
@@ -717,6 +718,10 @@ struct LdsEmitT {
       *reinterpret_cast<f4 *>(reinterpret_cast<float *>(p) + k * tile_cells<C>() + C * lane) =
           f4{x.v[0], x.v[1], x.v[2], x.v[3]};
       return;
+    } else if constexpr (sizeof(R) == 4 && C == 2) {  // (kF32Cpl 2: one 8-B store)
+      const int lane = threadIdx.x & 63;
+      *reinterpret_cast<f2v *>(reinterpret_cast<float *>(p) + k * tile_cells<C>() + C * lane) = f2v{x.v[0], x.v[1]};
+      return;
     }
 #pragma unroll
     for (int h = 0; h < C / 2; ++h) {  // 16-B LDS stores, w * x in fp64
@@ -983,7 +988,7 @@ __global__ __launch_bounds__(64 * atmos_waves<C>(), RAVG  ? FCX_RAVG_ATMOS_BLOCK
                                                           const double *__restrict__ corr_m,
                                                           const AtmosFused af, int64_t lo, int64_t hi) {
   static_assert(!RAVG || (C == 2 && sizeof(R) == 8), "register averages: fp64 engine only");
-  static_assert(sizeof(R) == 8 || C == 4, "fp32 flux rows: 4 cells per lane");
+  static_assert(sizeof(R) == 8 || C == 4 || C == 2, "fp32 flux rows: 4 or 2 cells per lane");
   // product rows [kFusedFields][kR]; with RAVG they first serve as the accumulators of
   // the type-0 averages (slot k = row k, TSUR in an extra row), then hold w * average
   constexpr int kRows = RAVG ? kAvgSlots : kFusedFields;
@@ -1408,9 +1413,9 @@ static int launch_atm_r(const Params *hp, const LaunchConfig &lc, int blocks, hi
   if (halo && ((hp->num_types != 1 && !(FCX_HALO_RAVG && lc.ravg)) || lo != 0)) return (int)hipErrorInvalidValue;
   if (hp->num_types == 1 && lc.f32) {  // fp32 engine: 4 cells per lane, T = 1 only
     if (halo)
-      launch_atm<4, float, VAR, 1, false, false, true>(lc.nontemporal, blocks, s, dp, corr_m, af, lo, hi);
+      launch_atm<kF32Cpl, float, VAR, 1, false, false, true>(lc.nontemporal, blocks, s, dp, corr_m, af, lo, hi);
     else
-      launch_atm<4, float, VAR, 1, false>(lc.nontemporal, blocks, s, dp, corr_m, af, lo, hi);
+      launch_atm<kF32Cpl, float, VAR, 1, false>(lc.nontemporal, blocks, s, dp, corr_m, af, lo, hi);
   } else if (lc.f32) {
     return (int)hipErrorInvalidValue;
   } else if (hp->num_types == 1 && lc.rec) {
@@ -1470,7 +1475,7 @@ int launch_cells(const Params *hp, const Params *dp, const double *corr_m, const
   AtmosFused afl;  // this launch's copy: its tile count (and, in trace builds, its trace slot)
   if (atm) {
     afl = *atm;
-    const int64_t own = (lc.f32 ? 4 : 2) * (64 - lc.halo);
+    const int64_t own = (lc.f32 ? kF32Cpl : 2) * (64 - lc.halo);
     afl.n_tiles = (hi + own - 1) / own;
 #if FCX_WAVE_TRACE
     afl.trace = g_trace.base ? g_trace.base + (g_trace.launches++ % g_trace.slots) * g_trace.stride : nullptr;
@@ -1480,8 +1485,8 @@ int launch_cells(const Params *hp, const Params *dp, const double *corr_m, const
   if (atm) {  // fused accumulation: T=1 specialised merged kernel, 2 cells per lane
     // four waves per block (fp32: two), one 128-cell (fp32: 256-cell) tile per wave and trip.  Default: one trip (full
     // grid) -- +2 % per T=1 step over the 8192-block cap, equal at T=2 (profiles/r01/grid_ab)
-    const int64_t kt = (lc.f32 ? 4 : 2) * (64 - lc.halo);  // cells a wave tile owns
-    const int64_t kw = lc.f32 ? atmos_waves<4>() : atmos_waves<2>();
+    const int64_t kt = (lc.f32 ? kF32Cpl : 2) * (64 - lc.halo);  // cells a wave tile owns
+    const int64_t kw = lc.f32 ? atmos_waves<kF32Cpl>() : atmos_waves<2>();
     const int64_t tiles = (hi - lo + kt - 1) / kt;
     const int64_t full = (tiles + kw - 1) / kw;
     const int blocks = (int)std::max<int64_t>(1, lc.max_blocks > 0 ? std::min<int64_t>(full, lc.max_blocks) : full);
@@ -1527,7 +1532,7 @@ template <int C, class R, bool NT>
 static void launch_group_h(bool halo, bool ravg, int blocks, hipStream_t s, const GroupArgs &g) {
   const Params *p[kMaxGroup];
   for (int k = 0; k < kMaxGroup; ++k) p[k] = g.m[k < g.n ? k : 0].P;
-  if constexpr (C == 2) {
+  if constexpr (C == 2 && sizeof(R) == 8) {
     if (ravg) {  // several surface types, the type-0 averages in registers (no halo tiles)
       hipLaunchKernelGGL((cells_atmos_group_kernel<C, R, NT, false, 0, true>), dim3(blocks),
                          dim3(64 * atmos_waves<C>()), 0, s, g, p[0], p[1], p[2], p[3]);
@@ -1558,12 +1563,12 @@ int launch_cells_group(GroupMember *members, int n, const LaunchConfig &lc, void
   }
   g.total_tiles = total;
   if (total == 0) return 0;
-  const int64_t kw = lc.f32 ? atmos_waves<4>() : atmos_waves<2>();
+  const int64_t kw = lc.f32 ? atmos_waves<kF32Cpl>() : atmos_waves<2>();
   const int blocks = (int)std::max<int64_t>(1, (total + kw - 1) / kw);
   if (lc.ravg && (lc.f32 || lc.halo > 0)) return (int)hipErrorInvalidValue;
   if (lc.f32) {
-    if (lc.nontemporal) launch_group_h<4, float, true>(lc.halo > 0, false, blocks, s, g);
-    else launch_group_h<4, float, false>(lc.halo > 0, false, blocks, s, g);
+    if (lc.nontemporal) launch_group_h<kF32Cpl, float, true>(lc.halo > 0, false, blocks, s, g);
+    else launch_group_h<kF32Cpl, float, false>(lc.halo > 0, false, blocks, s, g);
   } else {
     if (lc.nontemporal) launch_group_h<2, double, true>(lc.halo > 0, lc.ravg, blocks, s, g);
     else launch_group_h<2, double, false>(lc.halo > 0, lc.ravg, blocks, s, g);
@@ -1626,13 +1631,13 @@ int launch_atmos_finish(const AtmosArgs &a, int32_t n_boundaries, void *stream) 
 }
 
 int launch_atmos_fixup(const AtmosFused &af, int64_t n, bool f32, void *stream) {
-  const int64_t kt = f32 ? tile_cells<4>() : tile_cells<2>();
+  const int64_t kt = f32 ? tile_cells<kF32Cpl>() : tile_cells<2>();
   const int64_t tiles = (n + kt - 1) / kt;
   if (tiles < 2) return 0;
   const int blocks = (int)(((tiles - 1) * kFusedFields + 255) / 256);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (f32)
-    hipLaunchKernelGGL((atmos_fixup_kernel<float, tile_cells<4>()>), dim3(blocks), dim3(256), 0, s, af, tiles);
+    hipLaunchKernelGGL((atmos_fixup_kernel<float, tile_cells<kF32Cpl>()>), dim3(blocks), dim3(256), 0, s, af, tiles);
   else
     hipLaunchKernelGGL((atmos_fixup_kernel<double, tile_cells<2>()>), dim3(blocks), dim3(256), 0, s, af, tiles);
   return (int)hipGetLastError();
@@ -1663,7 +1668,7 @@ int launch_atmos_zero(const AtmosFused &af, const int32_t *cells, int64_t n, boo
 
 int launch_atmos_fixup_group(const AtmosFused *afs, const int64_t *n_cells, int n, bool f32, void *stream) {
   if (n < 1 || n > kMaxGroup) return (int)hipErrorInvalidValue;
-  const int64_t kt = f32 ? tile_cells<4>() : tile_cells<2>();
+  const int64_t kt = f32 ? tile_cells<kF32Cpl>() : tile_cells<2>();
   FixupGroup g{};
   g.n = n;
   for (int m = 0; m < n; ++m) {
@@ -1675,7 +1680,7 @@ int launch_atmos_fixup_group(const AtmosFused *afs, const int64_t *n_cells, int 
   const int blocks = (int)((g.first[n] + 255) / 256);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (f32)
-    hipLaunchKernelGGL((atmos_fixup_group_kernel<float, tile_cells<4>()>), dim3(blocks), dim3(256), 0, s, g);
+    hipLaunchKernelGGL((atmos_fixup_group_kernel<float, tile_cells<kF32Cpl>()>), dim3(blocks), dim3(256), 0, s, g);
   else
     hipLaunchKernelGGL((atmos_fixup_group_kernel<double, tile_cells<2>()>), dim3(blocks), dim3(256), 0, s, g);
   return (int)hipGetLastError();
