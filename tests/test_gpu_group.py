@@ -112,3 +112,44 @@ def test_group_of_engines_on_different_streams_runs_them_apart():
             np.testing.assert_array_equal(g[k], np.asarray(c.lf.field[k]), err_msg=str(k))
     for e in engines:
         e.close()
+
+
+def test_group_with_empty_atmosphere_cells():
+    """A map with atmosphere cells that no exchange cell maps to (runs of 0..5 cells): the
+    grouped launch stores their zero sums for every member, as fcx_run does, and matches the
+    sequential SCRIP application of each member's own fluxes."""
+    import torch
+    import oracle_lib
+    from fcx.engine import Engine, run_group
+    from fcx.parallel import local_atmos
+    from fcx.synthetic import build_case
+    from test_gpu_multirank import random_run_map
+
+    n = 60_013
+    amap = random_run_map(n, (0, 5), seed=41)
+    la = local_atmos(amap, 0, 1)
+    fields = (("MEVA", 1), ("HLAT", 1), ("HSEN", 1), ("RBBR", 1), ("UMOM", 2), ("VMOM", 3))
+    cases, engines, outs = [], [], []
+    for v in ("CCLM", "MOM5", "RCO"):
+        c = build_case(v, n=n, T=1, bias=True, seed=5)
+        o = {name: torch.full((la.n_atmos,), float("nan"), dtype=torch.float64, device="cuda:0")
+             for name, _ in fields}
+        atmos = {"local": la, "fields": [(2, 1, g, name, o[name]) for name, g in fields]}
+        engines.append(Engine(c.lf, 1, c.methods, corrections=c.corrections, atmos=atmos))
+        cases.append(c)
+        outs.append(o)
+    for e in engines:
+        e.upload(PHASE_ALL)
+    run_group(engines, PHASE_ALL, 3600)
+    for e in engines:
+        e.download(PHASE_ALL)
+        e.synchronize()
+    for c, o in zip(cases, outs):
+        for name, g in fields:
+            if (1, g, name) not in c.outputs:
+                continue
+            want = oracle_lib.atmos_accumulate(amap.atmos_index, amap.weight, np.asarray(c.lf.field[(1, g, name)]),
+                                               amap.n_atmos)
+            np.testing.assert_array_equal(o[name].cpu().numpy(), want, err_msg=name)
+    for e in engines:
+        e.close()
