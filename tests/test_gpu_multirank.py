@@ -227,6 +227,51 @@ def test_sharded_engines_one_process(variant, world, fused):
 
 
 @pytest.mark.parametrize("fused", [True, False])
+def test_sharded_engines_with_empty_atmosphere_cells(fused):
+    """A map with atmosphere cells that no exchange cell maps to (runs of 0..5 cells), over 3
+    shards: inside a shard they get the zero sum, the shared boundary cells still close
+    through the slots; fused and unfused paths."""
+    import torch
+
+    n, world, variant = 30_011, 3, "MOM5"
+    full = build_case(variant, n=n, T=1, bias=True, seed=911)
+    out = oracle_lib.run_case(full, "c", current_step_time=7200)
+    amap = random_run_map(n, (0, 5), seed=23)
+    ref = {name: oracle_lib.atmos_accumulate(amap.atmos_index, amap.weight, out[(1, g, name)], amap.n_atmos)
+           for name, g in FIELDS}
+    stride = len(FIELDS)
+    engines = []
+    for r in range(world):
+        la = local_atmos(amap, r, world)
+        shared = torch.zeros(max(world - 1, 1) * stride, dtype=torch.float64, device="cuda:0")
+        case = shard_case(full, la.offset, la.offset + la.size, variant)
+        eng, outs = make_engine(case, la, shared, stride, fused=fused)
+        engines.append((la, shared, eng, outs))
+    for la, shared, eng, outs in engines:
+        eng.upload(PHASE_ALL)
+        eng.run(PHASE_ALL, 7200)
+        eng.synchronize()
+    total = sum(sh for _, sh, _, _ in engines)
+    for la, shared, eng, outs in engines:
+        shared.copy_(total)
+        eng.atmos_finish()
+        eng.synchronize()
+    got = {name: np.full(amap.n_atmos, np.nan) for name, _ in FIELDS}
+    covered = np.zeros(amap.n_atmos, bool)
+    for la, shared, eng, outs in engines:
+        covered[la.atmos_offset: la.atmos_offset + la.n_atmos] = True
+        for name, _ in FIELDS:
+            got[name][la.atmos_offset: la.atmos_offset + la.n_atmos] = outs[name].cpu().numpy()[: la.n_atmos]
+        eng.close()
+    # cells between two ranks' ranges have no exchange cell on any rank: no rank holds them
+    # (the host assembles the field from the ranks' ranges; their sum over no links is 0)
+    assert not np.bincount(amap.atmos_index, minlength=amap.n_atmos)[~covered].any()
+    for name, _ in FIELDS:
+        got[name][~covered] = 0.0
+    assert_parity(got, ref, label=f"{variant} x{world} with empty atmosphere cells")
+
+
+@pytest.mark.parametrize("fused", [True, False])
 def test_sharded_engines_field_order_and_phases(fused):
     """Fields registered out of the fused kernel's slot order, RBBR accumulated at the end of
     the early phase and the rest at the end of the normal one: every path writes a field's
