@@ -197,8 +197,8 @@ def test_fp32_engine_rejects_fp64_outputs():
 
 # run lengths: 1..5, 1..9 (the fp32 fused kernel's halo tiles: 1 and 2 halo lanes of 4 cells),
 # 1..10 and 40..64 (256-cell wave tiles crossed: records + fix-up), 1..400 (longer than half a
-# 128-cell tile: atmos_kernel)
-@pytest.mark.parametrize("lengths", [(1, 5), (1, 9), (1, 10), (40, 64), (1, 400)])
+# 128-cell tile: atmos_kernel), 0..5 (atmosphere cells without exchange cells among them)
+@pytest.mark.parametrize("lengths", [(1, 5), (1, 9), (1, 10), (40, 64), (1, 400), (0, 5)])
 @pytest.mark.parametrize("mode", ["default", "nohalo", "capped", "pipelined", "pipelined_runtime"])
 @pytest.mark.parametrize("variant", ["CCLM", "MOM5", "RCO"])
 def test_fp32_fused_accumulation(variant, mode, lengths):
