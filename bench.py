@@ -350,6 +350,17 @@ def measure(wl, args, world, dist, comm, steps, warmup, t_base=0, cold=False):
         step(t_base)
         torch.cuda.synchronize()
         cold_ms = (time.perf_counter() - t_c) * 1e3
+    def all_ranks(flag):
+        """A loop exit every rank takes together: each warm-up step issues the step's
+        collective, so a rank-local exit test (wall time) would let the ranks run different
+        numbers of all-reduces -- the N > 1 abort of GPUTEST_r04 (a hang under real RCCL).
+        MIN over the ranks of the local flag, on the torch group."""
+        if world == 1:
+            return flag
+        t = torch.tensor([1.0 if flag else 0.0], dtype=torch.float64, device=wl.dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        return bool(t.item() > 0.5)
+
     # warm-up: the clocks reach steady state after ~40 ms of load; a short warm-up timed the
     # ramp (34.7 Gcells/s with 5 steps against 37.5 at steady state, round 1)
     warm, t_w = 0, time.perf_counter()
@@ -358,7 +369,7 @@ def measure(wl, args, world, dist, comm, steps, warmup, t_base=0, cold=False):
             step(t_base + warm * 3600)
             warm += 1
         torch.cuda.synchronize()
-        if warm >= warmup and time.perf_counter() - t_w >= MIN_WARMUP_S:
+        if all_ranks(warm >= warmup and time.perf_counter() - t_w >= MIN_WARMUP_S):
             break
     for k in range(probe_steps):  # still warm-up: the event-timed block, one launch per engine
         step(t_base + (warm + k) * 3600, ev_probe[k], grouped=False)

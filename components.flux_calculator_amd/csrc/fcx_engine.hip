@@ -220,6 +220,7 @@ struct fcx_engine {
   int64_t atm_out_tpad = 0;  // tile-blocked atmosphere outputs (kernels: tiled(a, atm_out_tpad))
   bool atmos_in_run = true;
   bool atm_done_fused = false;  // the last fcx_run already accumulated the atmosphere fields
+  int group_members = 0;        // engines in the merged launch of its last run (0: fcx_run)
   // exchange -> model remaps (SCRIP links, CSR by destination in link order)
   struct RemapField {
     int phase, s, g, var;
@@ -300,6 +301,22 @@ static void stage_free(fcx_engine *e);
 
 extern "C" const char *fcx_last_error(void) { return g_err.c_str(); }
 extern "C" int fcx_version(void) { return FCX_VERSION; }
+
+// the host's abort routine (flux_calculator.F90:883-887: oasis_abort(comp_id, comp_name, msg)),
+// called by the drop-in module before it stops the rank, so the coupled job ends together
+static std::atomic<fcx_abort_handler> g_abort{nullptr};
+
+extern "C" int fcx_set_abort_handler(fcx_abort_handler handler) {
+  g_abort.store(handler);
+  return FCX_OK;
+}
+
+extern "C" int fcx_abort(const char *message) {
+  fcx_abort_handler h = g_abort.load();
+  if (!h) return fail(FCX_E_STATE, "no abort handler registered");
+  h(message ? message : "");
+  return FCX_OK;  // the handler returned (oasis_abort does not)
+}
 
 extern "C" int fcx_method_from_string(const char *s, size_t len) {
   if (!s) return -1;
@@ -2169,6 +2186,7 @@ extern "C" int fcx_run(fcx_engine *e, int phase, int32_t t) {
   e->atm_done_fused = false;
   e->atm_done = e->exchanged = false;
   e->rec_plan = nullptr;
+  e->group_members = 0;
   if (!e->any_regrid) {
     Plan *pl;
     if (int r = get_plan(e, phase_stages(phase), phase, &pl)) return r;
@@ -2191,6 +2209,14 @@ extern "C" int fcx_run(fcx_engine *e, int phase, int32_t t) {
   return run_tail(e, phase);
 }
 
+struct GroupLaunchMember {
+  fcx_engine *e;
+  Plan *pl;
+  LaunchConfig lc;
+  const double *corr_m;
+};
+static int launch_group(const GroupLaunchMember *mem, int nm);
+
 // fcx_run of several engines (e.g. one per bottom-model variant) in the order given, with
 // the flux passes of those whose whole phase is one fused T = 1 launch of the same shape on
 // the same stream merged into ONE launch (cells_atmos_group_kernel).  Each engine then does
@@ -2201,18 +2227,12 @@ extern "C" int fcx_run_group(fcx_engine *const *es, int n, int phase, int32_t t)
   if (phase < 1 || phase > 3) return fail(FCX_E_ARG, "phase %d unknown", phase);
   for (int i = 0; i < n; ++i)
     if (int r = check(es[i])) return r;
-  struct Member {
-    fcx_engine *e;
-    Plan *pl;
-    LaunchConfig lc;
-    const double *corr_m;
-  };
-  std::vector<Member> mem;
-  std::vector<fcx_engine *> solo;
+  std::vector<GroupLaunchMember> mem;
+  std::vector<int> member_of(n, -1);  // list position -> member index (-1: runs as fcx_run)
   for (int i = 0; i < n; ++i) {
     fcx_engine *e = es[i];
     bool ok = !e->any_regrid && !e->timing && (int)mem.size() < kMaxGroup;
-    Member m{e, nullptr, {}, nullptr};
+    GroupLaunchMember m{e, nullptr, {}, nullptr};
     if (ok) {
       int rc;
       m.corr_m = month_slice(e, t, &rc);
@@ -2224,27 +2244,45 @@ extern "C" int fcx_run_group(fcx_engine *const *es, int n, int phase, int32_t t)
       const bool shape = m.pl->host.num_types == 1 || (m.lc.ravg && !m.lc.f32 && m.lc.halo == 0);
       ok = fused && shape && m.lc.variant >= 1 && !m.lc.rec && m.lc.max_blocks <= 0 && m.pl->host.n_max > 0;
       if (ok && !mem.empty()) {
-        const Member &f = mem[0];
+        const GroupLaunchMember &f = mem[0];
         ok = e->stream == f.e->stream && e->device == f.e->device && m.lc.f32 == f.lc.f32 &&
              m.lc.nontemporal == f.lc.nontemporal && (m.lc.halo > 0) == (f.lc.halo > 0) &&
              m.lc.ravg == f.lc.ravg && (m.pl->host.num_types == 1) == (f.pl->host.num_types == 1);
       }
     }
-    if (ok)
+    if (ok) {
+      member_of[(size_t)i] = (int)mem.size();
       mem.push_back(m);
-    else
-      solo.push_back(e);
+    }
   }
   if (mem.size() == 1) {  // nothing to merge
-    solo.push_back(mem[0].e);
+    std::fill(member_of.begin(), member_of.end(), -1);
     mem.clear();
   }
-  for (fcx_engine *e : solo)
-    if (int r = fcx_run(e, phase, t)) return r;
-  if (mem.empty()) return FCX_OK;
+  // every engine's tail (fix-up, accumulation, boundary exchange of an attached communicator,
+  // remaps) runs in LIST order below, whichever engines could join: group eligibility is
+  // rank-local (map, grid cap, halo), the order of the per-engine all-reduces must not be
+  if (!mem.empty())
+    if (int r = launch_group(mem.data(), (int)mem.size())) return r;
+  for (int i = 0; i < n; ++i) {
+    fcx_engine *e = es[i];
+    if (member_of[(size_t)i] < 0) {
+      if (int r = fcx_run(e, phase, t)) return r;
+      continue;
+    }
+    e->group_members = (int)mem.size();
+    e->atm_done_fused = true;
+    if (int r = run_tail(e, phase)) return r;
+  }
+  return FCX_OK;
+}
+
+// the merged launch of fcx_run_group's members, their crossing-record fix-ups as one launch
+// and their empty-cell stores (what precedes run_tail in fcx_run)
+static int launch_group(const GroupLaunchMember *mem, int nm) {
   GroupMember gm[kMaxGroup];
-  for (size_t k = 0; k < mem.size(); ++k) {
-    const Member &m = mem[k];
+  for (int k = 0; k < nm; ++k) {
+    const GroupLaunchMember &m = mem[k];
     fcx_engine *e = m.e;
     e->atm_done_fused = false;
     e->atm_done = e->exchanged = false;
@@ -2254,7 +2292,7 @@ extern "C" int fcx_run_group(fcx_engine *const *es, int n, int phase, int32_t t)
     gm[k] = GroupMember{m.pl->dev, m.corr_m, 0, m.lc.variant, 0, m.pl->af};
     gm[k].af.n_tiles = (m.pl->host.n_max + own - 1) / own;
   }
-  const int r = launch_cells_group(gm, (int)mem.size(), mem[0].lc, mem[0].e->stream);
+  const int r = launch_cells_group(gm, nm, mem[0].lc, mem[0].e->stream);
   if (r) return fail(FCX_E_HIP, "cells_atmos_group_kernel launch: %s", hipGetErrorString((hipError_t)r));
   // the members' crossing-record fix-ups (launch_fixup's rule) as one launch
   AtmosFused fx[kMaxGroup];
@@ -2262,29 +2300,24 @@ extern "C" int fcx_run_group(fcx_engine *const *es, int n, int phase, int32_t t)
   int nfx = 0;
 #ifdef FCX_AB_BUILD
   if (mem[0].e->ab_fixup_each) {
-    for (const Member &m : mem) {
-      if (int r2 = launch_fixup(m.e, m.pl, m.lc)) return r2;
-      m.e->atm_done_fused = true;
-      if (int r2 = run_tail(m.e, phase)) return r2;
-    }
+    for (int k = 0; k < nm; ++k)
+      if (int r2 = launch_fixup(mem[k].e, mem[k].pl, mem[k].lc)) return r2;
     return FCX_OK;
   }
 #endif
-  for (const Member &m : mem)
+  for (int k = 0; k < nm; ++k) {
+    const GroupLaunchMember &m = mem[k];
     if (m.e->atm_crossings > 0 && m.lc.halo == 0) {
       fx[nfx] = m.pl->af;
       fx_n[nfx++] = m.pl->host.n_max;
     }
+  }
   if (nfx) {
     const int r2 = launch_atmos_fixup_group(fx, fx_n, nfx, mem[0].lc.f32, mem[0].e->stream);
     if (r2) return fail(FCX_E_HIP, "atmos_fixup_group launch: %s", hipGetErrorString((hipError_t)r2));
   }
-  for (const Member &m : mem)
-    if (int r2 = launch_empty_cells(m.e, m.pl, m.lc)) return r2;
-  for (const Member &m : mem) {
-    m.e->atm_done_fused = true;
-    if (int r2 = run_tail(m.e, phase)) return r2;
-  }
+  for (int k = 0; k < nm; ++k)
+    if (int r2 = launch_empty_cells(mem[k].e, mem[k].pl, mem[k].lc)) return r2;
   return FCX_OK;
 }
 
@@ -2862,7 +2895,13 @@ extern "C" int fcx_run_atmos(fcx_engine *e, int phase) {
     if (int r = run_atmos(e, phase)) return r;
     e->atm_done = true;
   }
-  return comm_exchange(e);  // no-op without a communicator or once done for this run
+  return comm_exchange(e);  // no-op without a communicator, or when fcx_run already exchanged
+}
+
+extern "C" int fcx_last_group_size(fcx_engine *e, int32_t *members) {
+  if (!e || !members) return fail(FCX_E_ARG, "NULL argument");
+  *members = e->group_members;
+  return FCX_OK;
 }
 
 // ------------------------------------------------------------------ exchange -> model remaps
@@ -3017,6 +3056,7 @@ struct fcx_comm {
   size_t scratch_cap = 0;
   double *agree = nullptr;  // 2 * kSigWords doubles (device)
   std::vector<double> agreed;
+  bool verify_every = false;  // fcx_comm_verify: the agreement before every exchange
 };
 
 extern "C" int fcx_comm_unique_id(void *id) {
@@ -3086,8 +3126,9 @@ constexpr int kSigWords = 3;
 }
 
 static int exchange_agree(fcx_comm *c, const std::vector<double> &sig, hipStream_t s) {
-  for (size_t i = 0; i + kSigWords <= c->agreed.size(); i += kSigWords)
-    if (std::equal(sig.begin(), sig.end(), c->agreed.begin() + (std::ptrdiff_t)i)) return FCX_OK;
+  if (!c->verify_every)
+    for (size_t i = 0; i + kSigWords <= c->agreed.size(); i += kSigWords)
+      if (std::equal(sig.begin(), sig.end(), c->agreed.begin() + (std::ptrdiff_t)i)) return FCX_OK;
   if (!c->agree) HIP_TRY(hipMalloc(&c->agree, 2 * kSigWords * sizeof(double)));
   double h[2 * kSigWords];
   for (int i = 0; i < kSigWords; ++i) {
@@ -3106,7 +3147,13 @@ static int exchange_agree(fcx_comm *c, const std::vector<double> &sig, hipStream
                 "%.0f slot values, layout hash %.0f; over the ranks %.0f..%.0f engines, %.0f..%.0f values, hash "
                 "%.0f..%.0f",
                 c->rank, c->nranks, sig[0], sig[1], sig[2], -h[3], h[0], -h[4], h[1], -h[5], h[2]);
-  c->agreed.insert(c->agreed.end(), sig.begin(), sig.end());
+  if (!c->verify_every) c->agreed.insert(c->agreed.end(), sig.begin(), sig.end());
+  return FCX_OK;
+}
+
+extern "C" int fcx_comm_verify(fcx_comm *c, int every_exchange) {
+  if (!c) return fail(FCX_E_ARG, "NULL communicator");
+  c->verify_every = every_exchange != 0;
   return FCX_OK;
 }
 
@@ -3205,9 +3252,11 @@ extern "C" int fcx_set_comm(fcx_engine *e, fcx_comm *c) {
   return FCX_OK;
 }
 
-// the engine's own boundary exchange after its accumulation (fcx_set_comm)
+// the engine's own boundary exchange after its accumulation (fcx_set_comm).  Once its slots
+// are completed in this run there is nothing to agree on and nothing to send: fcx_run_atmos
+// after an fcx_run that exchanged issues no collective (every rank ran the same fcx_run)
 static int comm_exchange(fcx_engine *e) {
-  if (!e->comm) return FCX_OK;
+  if (!e->comm || e->exchanged) return FCX_OK;
   fcx_engine *one[1] = {e};
   return atmos_exchange(e->comm, one, 1);
 }

@@ -335,6 +335,33 @@ MODULE fcx_c_api
       TYPE(c_ptr), VALUE :: ptr
       INTEGER(c_int) :: fcx_host_free
     END FUNCTION
+    ! engines in the merged launch of the engine's last fcx_run_group (0: ran as fcx_run)
+    FUNCTION fcx_last_group_size(engine, members) BIND(C, name='fcx_last_group_size')
+      IMPORT :: c_int, c_int32_t, c_ptr
+      TYPE(c_ptr), VALUE :: engine
+      INTEGER(c_int32_t), INTENT(OUT) :: members
+      INTEGER(c_int) :: fcx_last_group_size
+    END FUNCTION
+    ! 1: the boundary-exchange signature agreement before every exchange (0: first of each)
+    FUNCTION fcx_comm_verify(comm, every_exchange) BIND(C, name='fcx_comm_verify')
+      IMPORT :: c_int, c_ptr
+      TYPE(c_ptr), VALUE :: comm
+      INTEGER(c_int), VALUE :: every_exchange
+      INTEGER(c_int) :: fcx_comm_verify
+    END FUNCTION
+    ! ---- the host's abort routine (oasis_abort, flux_calculator.F90:883-887): a BIND(C)
+    ! subroutine taking CHARACTER(kind=c_char), DIMENSION(*) (NUL-terminated), registered
+    ! with c_funloc; fcx_abort calls it (fcx_c_string turns the message into a string)
+    FUNCTION fcx_set_abort_handler(handler) BIND(C, name='fcx_set_abort_handler')
+      IMPORT :: c_int, c_funptr
+      TYPE(c_funptr), VALUE :: handler
+      INTEGER(c_int) :: fcx_set_abort_handler
+    END FUNCTION
+    FUNCTION fcx_abort(message) BIND(C, name='fcx_abort')
+      IMPORT :: c_int, c_char
+      CHARACTER(kind=c_char), DIMENSION(*), INTENT(IN) :: message
+      INTEGER(c_int) :: fcx_abort
+    END FUNCTION
   END INTERFACE
 
 CONTAINS
@@ -349,6 +376,18 @@ CONTAINS
     p = fcx_last_error()
     IF (.NOT. c_associated(p)) RETURN
     CALL c_f_pointer(p, chars, [512])
+    DO i = 1, 512
+      IF (chars(i) == c_null_char) EXIT
+      msg(i:i) = chars(i)
+    END DO
+  END FUNCTION
+
+  ! a NUL-terminated C string (an abort handler's argument) as a Fortran string
+  FUNCTION fcx_c_string(chars) RESULT(msg)
+    CHARACTER(kind=c_char), DIMENSION(*), INTENT(IN) :: chars
+    CHARACTER(len=512) :: msg
+    INTEGER :: i
+    msg = ''
     DO i = 1, 512
       IF (chars(i) == c_null_char) EXIT
       msg(i:i) = chars(i)

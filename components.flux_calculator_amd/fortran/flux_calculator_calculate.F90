@@ -14,8 +14,11 @@
 !   fcx_run_phase           fused coupling-step phase (replaces :902 and :972-991)
 !   fcx_detach              at finalisation
 ! The per-call subroutines keep the reference's exact semantics (each uploads what it
-! reads, computes on the GPU, downloads what it writes).  Errors are written to w_unit
-! and stop the rank (the reference's prepare-time errors call mpi_finalize(1)).
+! reads, computes on the GPU, downloads what it writes).  Errors are written to w_unit,
+! handed to the host's abort routine when one is registered (fcx_register_abort: a routine
+! that calls oasis_abort, as the reference does on a failed exchange, flux_calculator.F90:
+! 883-887, so the other components do not wait forever in their next exchange) and stop
+! the rank.
 MODULE flux_calculator_calculate
 
     USE flux_calculator_basic
@@ -35,6 +38,7 @@ MODULE flux_calculator_calculate
     PUBLIC distribute_shortwave_radiation_flux
     PUBLIC average_across_surface_types
     PUBLIC fcx_attach, fcx_register_average, fcx_commit_engine, fcx_run_phase, fcx_detach
+    PUBLIC fcx_register_abort
 
     TYPE(c_ptr), SAVE :: engine = c_null_ptr
     ! What fcx_attach bound.  The reference subroutines take the bottom model, the type count,
@@ -46,21 +50,35 @@ MODULE flux_calculator_calculate
 
 CONTAINS
 
+    ! the host's abort routine: a BIND(C) subroutine with one argument
+    ! CHARACTER(kind=c_char), DIMENSION(*) (the NUL-terminated message; fcx_c_string), passed
+    ! as c_funloc(routine).  It is called before the rank stops; a routine that calls
+    ! oasis_abort(comp_id, comp_name, fcx_c_string(msg)) ends the coupled job.
+    SUBROUTINE fcx_register_abort(handler)
+        TYPE(c_funptr), INTENT(IN) :: handler
+        INTEGER(c_int) :: r
+        r = fcx_set_abort_handler(handler)
+    END SUBROUTINE fcx_register_abort
+
+    ! the end of the rank on an error: message to w_unit, the host's abort routine, stop
+    SUBROUTINE stop_run(msg)
+        CHARACTER(len=*), INTENT(IN) :: msg
+        INTEGER(c_int) :: r
+        WRITE (w_unit, '(A)') msg
+        CALL FLUSH(w_unit)
+        r = fcx_abort(msg // c_null_char)  ! FCX_E_STATE when no routine is registered
+        ERROR STOP 1
+    END SUBROUTINE stop_run
+
     SUBROUTINE check(status, where)
         INTEGER(c_int),   INTENT(IN) :: status
         CHARACTER(len=*), INTENT(IN) :: where
-        IF (status /= FCX_OK) THEN
-            WRITE (w_unit,*) 'flux engine error in ', where, ': ', TRIM(fcx_error_message())
-            CALL FLUSH(w_unit)
-            ERROR STOP 1
-        ENDIF
+        IF (status /= FCX_OK) CALL stop_run('flux engine error in ' // where // ': ' // TRIM(fcx_error_message()))
     END SUBROUTINE check
 
     SUBROUTINE contract_error(where, msg)
         CHARACTER(len=*), INTENT(IN) :: where, msg
-        WRITE (w_unit, '(4A)') 'flux engine contract violation in ', where, ': ', msg
-        CALL FLUSH(w_unit)
-        ERROR STOP 1
+        CALL stop_run('flux engine contract violation in ' // where // ': ' // msg)
     END SUBROUTINE contract_error
 
     ! the per-call subroutine `where` against the attached engine: an engine exists, and
@@ -114,10 +132,7 @@ CONTAINS
         INTEGER(c_int) :: m
         DO i = 1, num_surface_types
             m = fcx_method_id(methods(my_bottom_model, i))
-            IF (m < 0) THEN
-                WRITE (w_unit,*) 'Method ', methods(my_bottom_model, i), ' is not known.'
-                ERROR STOP 1
-            ENDIF
+            IF (m < 0) CALL stop_run('Method ' // TRIM(methods(my_bottom_model, i)) // ' is not known.')
             CALL check(fcx_set_method(engine, flux, INT(i, c_int), m), 'fcx_set_method')
             att_methods(flux, i) = methods(my_bottom_model, i)
         ENDDO

@@ -55,6 +55,11 @@ class Comm:
         arr = (ctypes.c_void_p * len(engines))(*[e.h.value for e in engines])
         _lib.check(self.lib.fcx_atmos_allreduce(self.h, arr, len(engines)))
 
+    def verify(self, every_exchange=True):
+        """fcx_comm_verify: the signature agreement before every exchange (hosts that change
+        their engine lists at run time) or only before the first of each signature."""
+        _lib.check(self.lib.fcx_comm_verify(self.h, int(bool(every_exchange))))
+
     def close(self):
         if getattr(self, "h", None) is not None:
             self.lib.fcx_comm_destroy(self.h)

@@ -219,6 +219,12 @@ class Engine:
         _lib.check(self.lib.fcx_device_layout(self.h, ctypes.byref(tile), ctypes.byref(stride)))
         return tile.value, stride.value
 
+    def last_group_size(self):
+        """Engines in the merged launch of this engine's last fcx_run_group (0: ran as fcx_run)."""
+        m = ctypes.c_int32()
+        _lib.check(self.lib.fcx_last_group_size(self.h, ctypes.byref(m)))
+        return m.value
+
     def close(self):
         if self.h is not None:
             self.lib.fcx_destroy(self.h)

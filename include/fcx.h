@@ -79,6 +79,18 @@ typedef struct fcx_engine fcx_engine;
 const char *fcx_last_error(void);
 int fcx_version(void);
 
+/* The host's abort routine for errors that must end the coupled run, not just this rank:
+ * the reference turns them into oasis_abort(comp_id, comp_name, msg)
+ * (flux_calculator.F90:883-887, 930-934, 960-964).  The Fortran drop-in module calls
+ * fcx_abort(message) on a failed call or a contract violation before its own ERROR STOP, so
+ * a host that registers a routine calling oasis_abort (or MPI_Abort) takes the other
+ * components down with it instead of leaving them waiting in their next exchange.
+ * Process-wide; NULL unregisters.  fcx_abort returns FCX_E_STATE when none is registered,
+ * FCX_OK when the handler returned. */
+typedef void (*fcx_abort_handler)(const char *message);
+int fcx_set_abort_handler(fcx_abort_handler handler);
+int fcx_abort(const char *message);
+
 /* trim(method)=='CCLM' etc. on a blank-padded Fortran CHARACTER(len=20); -1 if unknown */
 int fcx_method_from_string(const char *s, size_t len);
 
@@ -136,6 +148,11 @@ int fcx_download(fcx_engine *e, int phase); /* D2H of host-bound outputs of the 
  * step pays the launch ramp and drain once.  Results are those of fcx_run of each, bit for
  * bit. */
 int fcx_run_group(fcx_engine *const *engines, int n_engines, int phase, int32_t current_step_time);
+/* engines in the merged launch of the engine's last fcx_run_group (0: it ran as fcx_run).
+ * Every engine's work after its launch (fix-up, accumulation, the boundary exchange of an
+ * attached communicator, remaps) runs in LIST order whichever engines were merged, so the
+ * per-engine collectives of fcx_set_comm keep the same order on every rank. */
+int fcx_last_group_size(fcx_engine *e, int32_t *members);
 /* the three above; with host-bound fields pipelined over cell chunks (FCX_OPT_PIPELINE_CHUNKS) */
 int fcx_step(fcx_engine *e, int phase, int32_t current_step_time);
 /* waits for the engine's stream; the caller's host arrays hold the downloaded outputs once it
@@ -232,7 +249,8 @@ int fcx_comm_destroy(fcx_comm *c);
 int fcx_comm_allreduce_sum(fcx_comm *c, double *buf, size_t count, void *hip_stream);
 /* attach: from now on fcx_run / fcx_step / fcx_run_atmos of the engine complete its
  * boundary slots themselves (all-reduce on the engine's stream, then fcx_atmos_finish);
- * every rank's engine must then run the same steps.  NULL detaches. */
+ * every rank's engine must then run the same steps.  fcx_run_atmos after an fcx_run that
+ * already exchanged issues no collective.  NULL detaches. */
 int fcx_set_comm(fcx_engine *e, fcx_comm *c);
 /* several engines of this rank (e.g. one per bottom-model variant) in ONE all-reduce of
  * sum(n_boundaries * stride) doubles over their slots in list order, on the first engine's
@@ -240,12 +258,21 @@ int fcx_set_comm(fcx_engine *e, fcx_comm *c);
  * one buffer are reduced in place, others through the communicator's scratch; the collective
  * is the same either way.  Call after their accumulation (fcx_run, or fcx_run_atmos).
  * Collective contract: every rank passes its engines in the same order with the same
- * n_boundaries and strides.  The first exchange of each such signature checks it with a
- * blocking max-all-reduce, and ranks that disagree all return FCX_E_ARG.  An engine already
- * completed in this run (fcx_set_comm) takes part with zeros and is skipped; one with no
- * accumulation since its last exchange takes part with zeros and the call returns
+ * n_boundaries and strides.  What is checked: by default, the FIRST exchange of each
+ * signature a rank has not exchanged before on this communicator is preceded by a blocking
+ * max-all-reduce of the signature, and ranks that disagree all return FCX_E_ARG -- this
+ * catches a decomposition the ranks disagree on from the start, without a host wait per
+ * step.  It cannot catch a rank that switches to a new engine list after exchanging while
+ * another keeps an already agreed one (that rank skips the check, the collectives differ);
+ * fcx_comm_verify(c, 1) runs the check before EVERY exchange (one 6-double all-reduce and a
+ * host wait per exchange) for hosts that change their engine lists at run time.  An engine
+ * already completed in this run (fcx_set_comm) takes part with zeros and is skipped; one
+ * with no accumulation since its last exchange takes part with zeros and the call returns
  * FCX_E_STATE after the collective, so no rank is left waiting. */
 int fcx_atmos_allreduce(fcx_comm *c, fcx_engine *const *engines, int n_engines);
+/* 1: the signature agreement before every exchange of the communicator; 0 (default): before
+ * the first exchange of each signature */
+int fcx_comm_verify(fcx_comm *c, int every_exchange);
 
 /* ---- exchange-grid -> model remaps ----
  * The SCRIP weight application OASIS3-MCT performs on the 'S' fields sent to a model

@@ -8,7 +8,10 @@
 ! No regridding matrices are set, so the reference's do_regridding calls between the
 ! calc_* calls would be no-ops and are left out.
 !
-!   dropin_host <dir> percall|fused|noattach|badtable|badgrid|badtypes
+!   dropin_host <dir> percall|fused|noattach|badtable|badgrid|badtypes[+abort]
+!
+! +abort: the host registers its abort routine (fcx_register_abort) first, as a coupled
+! host registers one that calls oasis_abort; this one prints the message and stops with 3.
 !
 ! <dir>/manifest.txt (written by tests/test_fortran.py), one record per line:
 !   N nbufs T nt nu nv          buffer count, surface types, grid sizes
@@ -23,7 +26,14 @@ PROGRAM dropin_host
     USE flux_calculator_basic
     USE flux_calculator_calculate
     USE fcx_c_api, ONLY: FCX_PHASE_EARLY, FCX_PHASE_NORMAL
+    USE, INTRINSIC :: iso_c_binding, ONLY: c_funloc, c_char
     IMPLICIT NONE
+    INTERFACE
+        SUBROUTINE host_abort(msg) BIND(C)
+            IMPORT :: c_char
+            CHARACTER(kind=c_char), DIMENSION(*), INTENT(IN) :: msg
+        END SUBROUTINE host_abort
+    END INTERFACE
 
     TYPE buf_t
         REAL(wp), POINTER :: p(:) => NULL()
@@ -44,6 +54,10 @@ PROGRAM dropin_host
 
     CALL get_command_argument(1, dir)
     CALL get_command_argument(2, mode)
+    IF (INDEX(mode, '+abort') > 0) THEN
+        CALL fcx_register_abort(c_funloc(host_abort))
+        mode = mode(1:INDEX(mode, '+abort') - 1)
+    ENDIF
     w_unit = 6
     CALL init_varname_idx
     DO s = 0, MAX_SURFACE_TYPES
@@ -205,3 +219,13 @@ SUBROUTINE mpi_finalize(ierror)
     WRITE (*, '(A,I0)') 'mpi_finalize called by flux_calculator_basic, code ', ierror
     ERROR STOP 2
 END SUBROUTINE mpi_finalize
+
+! The coupled host's abort routine (test stand-in for one that calls oasis_abort(comp_id,
+! comp_name, msg), flux_calculator.F90:883-887): reports the message and ends the run with 3.
+SUBROUTINE host_abort(msg) BIND(C)
+    USE, INTRINSIC :: iso_c_binding, ONLY: c_char
+    USE fcx_c_api, ONLY: fcx_c_string
+    CHARACTER(kind=c_char), DIMENSION(*), INTENT(IN) :: msg
+    WRITE (*, '(2A)') 'HOST ABORT ROUTINE: ', TRIM(fcx_c_string(msg))
+    ERROR STOP 3
+END SUBROUTINE host_abort

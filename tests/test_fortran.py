@@ -124,3 +124,26 @@ def test_dropin_per_call_checks_its_arguments(tmp_path, mode, message):
     assert r.returncode != 0, out
     assert "flux engine contract violation" in out and message in out, out
     assert "DROPIN_HOST OK" not in out
+
+
+@pytest.mark.skipif(not os.path.exists(DROPIN), reason="Fortran drop-in host not built")
+@pytest.mark.parametrize("mode,message", [
+    ("noattach", "no flux engine attached"),
+    ("badtable", "method table differs from the attached one: surface type 1"),
+])
+def test_dropin_hands_errors_to_the_host_abort_routine(tmp_path, mode, message):
+    """The reference ends a coupled run with oasis_abort(comp_id, comp_name, msg)
+    (flux_calculator.F90:883-887), so the other components do not wait in their next
+    exchange.  A host that registers its abort routine (fcx_register_abort -> the C ABI's
+    fcx_set_abort_handler) gets the drop-in's contract-violation message there before the
+    rank would stop: the test host's routine prints it and ends the run with code 3."""
+    from fcx.synthetic import build_case
+
+    case = build_case("CCLM", n=257, T=2, bias=False)
+    write_manifest(case, str(tmp_path), 3600)
+    r = subprocess.run([DROPIN, str(tmp_path), mode + "+abort"], capture_output=True, text=True, timeout=120)
+    out = r.stdout + r.stderr
+    assert r.returncode == 3, out
+    line = [x for x in out.splitlines() if x.startswith("HOST ABORT ROUTINE: ")]
+    assert line and "flux engine contract violation" in line[0] and message in line[0], out
+    assert "DROPIN_HOST OK" not in out

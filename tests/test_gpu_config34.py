@@ -49,13 +49,22 @@ def sample(n, rng):
 
 
 @pytest.mark.timeout(300)
+@pytest.mark.parametrize("path", ["run_group", "run"])
 @pytest.mark.parametrize("atmos_map", ["random", "periodic"])
-def test_config3_bench_path_10M(atmos_map):
+def test_config3_bench_path_10M(atmos_map, path):
     """The bench's exact path at config 3's size: the random-run atmosphere map (segments
-    cross the wave tiles: the fix-up kernel completes them) and the periodic one (none do)."""
+    cross the wave tiles: halo tiles complete them) and the periodic one (none do).
+    run_group is the bench's timed step -- the three variants in ONE
+    cells_atmos_group_kernel launch (fcx_run_group) -- checked here against the oracle
+    directly, not only against the per-engine launches; run is one launch per engine."""
     wl = Workload(10_000_000, variants=VARIANTS, atmos_map=atmos_map)
     try:
-        wl.run(T_STEP)
+        if path == "run_group":
+            wl.run_group(T_STEP)
+            assert [e.last_group_size() for e in wl.engines] == [len(VARIANTS)] * len(VARIANTS)
+        else:
+            wl.run(T_STEP)
+            assert [e.last_group_size() for e in wl.engines] == [0] * len(VARIANTS)
         wl.download()
         rng = np.random.default_rng(11)
         idx = sample(wl.n, rng)

@@ -42,6 +42,13 @@ SCENARIOS = [
     ("attached_comm", "own", "one", "attached"),
     ("signature_mismatch", "adjacent", "one", "mismatch"),
     ("stale_engine", "adjacent", "one", "stale"),
+    # fcx_set_comm + fcx_run_group where the ranks merge different engines (rank 0's last
+    # engine has a grid cap, so it runs as fcx_run): the per-engine exchanges must still go
+    # in list order on every rank (solo engines used to exchange first)
+    ("attached_group_differs", "own", "one", "attached_group"),
+    # the signature agreement before every exchange (fcx_comm_verify): after an agreed
+    # exchange, rank 1 passes a shorter engine list -- every rank gets the named error
+    ("relisted_after_agreement", "adjacent", "one", "relist"),
 ]
 SCENARIOS_3 = [
     ("empty_middle_rank", "adjacent", "one", "empty_middle"),
@@ -77,7 +84,7 @@ def _scenario(rank, world, uid, name, layout, streams, special, log):
     import torch
     from fcx.basic import PHASE_ALL, PHASE_NORMAL
     from fcx.comm import Comm
-    from fcx.engine import Engine
+    from fcx.engine import Engine, run_group
     from fcx.parallel import local_atmos, synthetic_atmos_map
     from test_gpu_multirank import shard_case
     from fcx.synthetic import build_case
@@ -104,6 +111,8 @@ def _scenario(rank, world, uid, name, layout, streams, special, log):
         bufs, slots = [], [None] * 3
     own = [torch.cuda.Stream() for _ in range(3)] if streams == "per_engine" else [torch.cuda.current_stream()] * 3
     comm = Comm(0, world, rank, uid)
+    if special == "relist":
+        comm.verify(True)
     engines, cases, outs_all = [], [], []
     for i, v in enumerate(VARIANTS):
         full = build_case(v, n=N, T=1, bias=True, seed=41 + i)
@@ -114,8 +123,12 @@ def _scenario(rank, world, uid, name, layout, streams, special, log):
             atmos.update(own_boundaries=True, comm=comm)
         else:
             atmos["shared"] = (slots[i], stride)
+        if special == "attached_group":
+            opts = {"max_blocks": 32} if (rank == 0 and i == 2) else None
+        else:
+            opts = {"atmos_in_run": 0} if i == 1 else None
         e = Engine(case.lf, 1, case.methods, corrections=case.corrections, atmos=atmos,
-                   stream=own[i].cuda_stream, options={"atmos_in_run": 0} if i == 1 else None)
+                   stream=own[i].cuda_stream, options=opts)
         e.upload(PHASE_ALL)
         engines.append(e)
         cases.append(case)
@@ -128,8 +141,13 @@ def _scenario(rank, world, uid, name, layout, streams, special, log):
             for o in outs.values():
                 o.fill_(float("nan"))
         torch.cuda.synchronize()
-        err = None
+        err, group = None, None
+        if special == "attached_group":
+            run_group(engines, PHASE_ALL, 3600 * step)  # every engine's exchange inside
+            group = [e.last_group_size() for e in engines]
         for i, e in enumerate(engines):
+            if special == "attached_group":
+                break
             if special == "stale" and rank == world - 1 and step == 0 and i == 2:
                 continue  # this rank never runs engine 2 before the first exchange
             e.run(PHASE_ALL, 3600 * step)
@@ -137,7 +155,8 @@ def _scenario(rank, world, uid, name, layout, streams, special, log):
                 e.run_atmos(PHASE_ALL)  # atmos_in_run 0: the accumulation on its own
         try:
             if layout != "own":
-                use = engines[:2] if (special == "mismatch" and rank == 1) else engines
+                short = (special == "mismatch" and rank == 1) or (special == "relist" and rank == 1 and step == 1)
+                use = engines[:2] if short else engines
                 comm.atmos_allreduce(use)
         except Exception as ex:  # noqa: BLE001 -- reported to the parent
             err = str(ex)
@@ -145,7 +164,7 @@ def _scenario(rank, world, uid, name, layout, streams, special, log):
             e.download(PHASE_ALL)
             e.synchronize()
         torch.cuda.synchronize()
-        rec = {"error": err, "slots_zero": all(float(b.abs().sum()) == 0.0 for b in bufs),
+        rec = {"error": err, "group": group, "slots_zero": all(float(b.abs().sum()) == 0.0 for b in bufs),
                "out": [{f: outs[f].cpu().numpy()[: la.n_atmos].copy() for f, _ in FIELDS} for outs in outs_all],
                "flux": [{f: np.array(c.lf.field[(1, g, f)], copy=True) for f, g in FIELDS} for c in cases]}
         result["steps"].append(rec)
@@ -218,7 +237,16 @@ def test_exchange_ranks_through_libfcx(world, tmp_path):
             if not (all(e is None for e in errs[:-1]) and errs[-1] and "no accumulation" in errs[-1]):
                 problems.append(f"{name}: expected {want_err}, got {errs}")
             continue
-        for step in range(2):
+        if special == "relist":
+            errs = [p["steps"][1]["error"] for p in per]
+            if not all(e and "ranks disagree" in e for e in errs):
+                problems.append(f"{name}: step 1 expected every rank to report the disagreement, got {errs}")
+        if special == "attached_group":
+            for r, p in enumerate(per):
+                want_g = [2, 2, 0] if r == 0 else [3, 3, 3]
+                if any(st["group"] != want_g for st in p["steps"]):
+                    problems.append(f"{name} rank {r}: group sizes {[st['group'] for st in p['steps']]}, want {want_g}")
+        for step in range(1 if special == "relist" else 2):
             for p in per:
                 if p["steps"][step]["error"]:
                     problems.append(f"{name} rank step {step}: {p['steps'][step]['error']}")
