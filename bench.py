@@ -290,6 +290,58 @@ def e2e_concurrent(args, variants, n=32_768, steps=500):
                     "per-bottom-model MPI tasks; a step = common start to the last engine done"}
 
 
+def e2e_async(args, variants, n=32_768, steps=500):
+    """The variants' steps started one after the other from ONE host thread with
+    fcx_step_async (each engine on its own stream), then every engine synchronised: the
+    asynchronous phase, no host threads of the caller's.  Wall time per step."""
+    import torch
+    from fcx.basic import PHASE_ALL
+    from fcx.engine import Engine
+    from fcx.synthetic import build_case, inputs_for_bench
+
+    data = inputs_for_bench(n)
+    streams = [torch.cuda.Stream() for _ in variants]
+    cases = [build_case(v, n=n, T=args.types, bias=args.bias, data=data if args.types == 1 else None)
+             for v in variants]
+    engines = [Engine(c.lf, c.num_surface_types, c.methods, corrections=c.corrections, averages=c.averages,
+                      stream=st.cuda_stream) for c, st in zip(cases, streams)]
+    ts = []
+    for k in range(50 + steps):
+        t0 = time.perf_counter()
+        for e in engines:
+            e.step_async(PHASE_ALL, k * 3600)
+        for e in engines:
+            e.synchronize()
+        if k >= 50:
+            ts.append(time.perf_counter() - t0)
+    for e in engines:
+        e.close()
+    med = float(np.median(ts))
+    return {"us_per_step_median": round(med * 1e6, 1), "us_per_step_p90": round(float(np.percentile(ts, 90)) * 1e6, 1),
+            "steps": steps, "engines": len(engines),
+            "rule": "fcx_step_async of every variant's engine (own stream) from one host thread, then fcx_synchronize "
+                    "of each; a step = first start to the last engine synchronised"}
+
+
+def link_bytes(variants, n, args):
+    """Bytes one coupling step of the variants moves over the host link from host arrays:
+    every distinct input array up, every output array down (the staged transfers)."""
+    from fcx.basic import PHASE_ALL
+    from fcx.engine import Engine
+    from fcx.synthetic import build_case
+
+    b_in = b_out = 0
+    for v in variants:
+        c = build_case(v, n=n, T=args.types, bias=args.bias)
+        e = Engine(c.lf, c.num_surface_types, c.methods, corrections=c.corrections, averages=c.averages)
+        total = e.algorithmic_bytes(PHASE_ALL)  # the plan's distinct arrays read once, written once
+        e.close()
+        outs = sum(c.lf.field[k].nbytes for k in dict.fromkeys(c.outputs))
+        b_in += total - outs - (8 * n if args.bias else 0)  # (the month slice stays on the device)
+        b_out += outs
+    return b_in, b_out
+
+
 def relaunch(n):
     """`python bench.py --gpus N` outside a launcher: run this same command under
     torch.distributed.run (one rank per GPU, rendezvous on 127.0.0.1) as a child process,
@@ -689,6 +741,20 @@ def main():
             conc = e2e_concurrent(args, variants)
             out["baltic_size"]["gpu_dropin_concurrent"] = conc
             out["baltic_size"]["gpu_concurrent_vs_all_cores"] = round(cp["us_per_step"] / conc["us_per_step_median"], 2)
+            asy = e2e_async(args, variants)
+            out["baltic_size"]["gpu_dropin_async"] = asy
+            out["baltic_size"]["gpu_async_vs_all_cores"] = round(cp["us_per_step"] / asy["us_per_step_median"], 2)
+            # the host link's bound: the step's fields must cross it once
+            # each way; measured both directions at once on this box
+            from link_probe import link_rates
+            lk = link_rates(*link_bytes(variants, 32_768, args))
+            both = lk["256MiB"]["both_GBps"]
+            b_step = lk["step"]["h2d_bytes"] + lk["step"]["d2h_bytes"]
+            out["baltic_size"]["host_link"] = dict(lk, bound_us=round(b_step / both / 1e3, 1),
+                                                   bound_vs_all_cores=round(cp["us_per_step"] / (b_step / both / 1e3), 2),
+                                                   rule="bound_us: the step's input bytes up plus output bytes down at "
+                                                        "the rate of both directions at once (256 MiB copies); "
+                                                        "no step from host arrays can be faster")
     if rank == 0:
         print(json.dumps(out), flush=True)
     if comm is not None:

@@ -45,6 +45,44 @@ def med_us(f, reps, warm=20):
     return round(float(np.median(ts)) * 1e6, 1)
 
 
+def link_rates(b_in, b_out, reps=200):
+    """Page-locked host <-> device DMA of b_in bytes up and b_out bytes down, one copy per
+    direction: each alone, and both at once on two streams; plus 256 MiB copies (the link's
+    asymptotic rate).  Median microseconds and GB/s."""
+    import torch
+
+    dev = torch.device("cuda", 0)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    out = {}
+    for name, bi, bo, r in (("step", b_in, b_out, reps), ("256MiB", 256 << 20, 256 << 20, 10)):
+        hi, ho = torch.empty(bi, dtype=torch.uint8).pin_memory(), torch.empty(bo, dtype=torch.uint8).pin_memory()
+        di, do = torch.empty(bi, dtype=torch.uint8, device=dev), torch.empty(bo, dtype=torch.uint8, device=dev)
+
+        def up():
+            with torch.cuda.stream(s1):
+                di.copy_(hi, non_blocking=True)
+
+        def down():
+            with torch.cuda.stream(s2):
+                ho.copy_(do, non_blocking=True)
+
+        def run(fs):
+            def f():
+                for g in fs:
+                    g()
+                s1.synchronize()
+                s2.synchronize()
+            return f
+        t_in = med_us(run([up]), r, warm=3)
+        t_out = med_us(run([down]), r, warm=3)
+        t_both = med_us(run([up, down]), r, warm=3)
+        out[name] = {"h2d_bytes": bi, "d2h_bytes": bo, "h2d_us": t_in, "d2h_us": t_out, "both_us": t_both,
+                     "h2d_GBps": round(bi / t_in / 1e3, 1), "d2h_GBps": round(bo / t_out / 1e3, 1),
+                     "both_GBps": round((bi + bo) / t_both / 1e3, 1)}
+        del hi, ho, di, do
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--cells", type=int, default=32_768)

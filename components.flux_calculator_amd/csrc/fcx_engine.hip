@@ -2483,6 +2483,28 @@ extern "C" int fcx_step(fcx_engine *e, int phase, int32_t t) {
   return fcx_synchronize(e);
 }
 
+// fcx_step without the final wait: the inputs are in the engine's hands when it returns (caller
+// heap arrays copied into the staging arena), the launch and the downloads are queued, and the
+// caller's output arrays are filled by the next fcx_synchronize.  A host can start the next
+// engine (or its own work: the other phase's oasis_get, diagnostics) meanwhile.  Host-bound
+// grids that take the chunk pipeline complete inside the call.
+extern "C" int fcx_step_async(fcx_engine *e, int phase, int32_t t) {
+  if (int r = check(e)) return r;
+  if (phase < 1 || phase > 3) return fail(FCX_E_ARG, "phase %d unknown", phase);
+  if (e->chunks > 1 && !e->any_regrid) {
+    Plan *pl;
+    if (int r = get_plan(e, phase_stages(phase), phase, &pl)) return r;
+    if (host_bound(e, pl) && pl->host.n_max >= 2 * e->min_chunk) return step_pipelined(e, phase, t, pl);
+  }
+  if (int r = fcx_upload(e, phase)) return r;
+  if (int r = fcx_run(e, phase, t)) return r;
+  const bool keep = e->deferred_scatter;
+  e->deferred_scatter = true;  // the host copies of the downloads wait for fcx_synchronize
+  const int r = fcx_download(e, phase);
+  e->deferred_scatter = keep;
+  return r;
+}
+
 extern "C" int fcx_synchronize(fcx_engine *e) {
   if (!e) return fail(FCX_E_ARG, "NULL engine");
   HIP_TRY(hipStreamSynchronize(e->stream));

@@ -122,6 +122,14 @@ MODULE fcx_c_api
       INTEGER(c_int32_t), VALUE :: t
       INTEGER(c_int) :: fcx_step
     END FUNCTION
+    ! fcx_step without its final wait: outputs in the host arrays after fcx_synchronize
+    FUNCTION fcx_step_async(engine, phase, t) BIND(C, name='fcx_step_async')
+      IMPORT :: c_int, c_int32_t, c_ptr
+      TYPE(c_ptr), VALUE :: engine
+      INTEGER(c_int), VALUE :: phase
+      INTEGER(c_int32_t), VALUE :: t
+      INTEGER(c_int) :: fcx_step_async
+    END FUNCTION
     FUNCTION fcx_run(engine, phase, t) BIND(C, name='fcx_run')
       IMPORT :: c_int, c_int32_t, c_ptr
       TYPE(c_ptr), VALUE :: engine

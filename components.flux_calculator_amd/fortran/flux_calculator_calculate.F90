@@ -12,6 +12,9 @@
 !   fcx_register_average    for each type-0 output (optional: fused averaging)
 !   fcx_commit_engine       validate + device mirrors
 !   fcx_run_phase           fused coupling-step phase (replaces :902 and :972-991)
+!   fcx_start_phase /       the same phase in two halves: started (inputs taken, launch and
+!   fcx_finish_phase        downloads queued), then completed (outputs in local_field), so
+!                           the host can do other work -- e.g. an oasis_get -- in between
 !   fcx_detach              at finalisation
 ! The per-call subroutines keep the reference's exact semantics (each uploads what it
 ! reads, computes on the GPU, downloads what it writes).  Errors are written to w_unit,
@@ -38,7 +41,7 @@ MODULE flux_calculator_calculate
     PUBLIC distribute_shortwave_radiation_flux
     PUBLIC average_across_surface_types
     PUBLIC fcx_attach, fcx_register_average, fcx_commit_engine, fcx_run_phase, fcx_detach
-    PUBLIC fcx_register_abort
+    PUBLIC fcx_register_abort, fcx_start_phase, fcx_finish_phase
 
     TYPE(c_ptr), SAVE :: engine = c_null_ptr
     ! What fcx_attach bound.  The reference subroutines take the bottom model, the type count,
@@ -263,6 +266,18 @@ CONTAINS
         INTEGER(c_int), INTENT(IN) :: phase
         CALL check(fcx_step(engine, phase, INT(current_step_time, c_int32_t)), 'fcx_step')
     END SUBROUTINE fcx_run_phase
+
+    ! fcx_run_phase in two halves (fcx_step_async + fcx_synchronize): after fcx_start_phase
+    ! the phase's input fields may be overwritten (their values are in the engine); its
+    ! output fields hold the results after fcx_finish_phase
+    SUBROUTINE fcx_start_phase(phase)
+        INTEGER(c_int), INTENT(IN) :: phase
+        CALL check(fcx_step_async(engine, phase, INT(current_step_time, c_int32_t)), 'fcx_step_async')
+    END SUBROUTINE fcx_start_phase
+
+    SUBROUTINE fcx_finish_phase()
+        CALL check(fcx_synchronize(engine), 'fcx_synchronize')
+    END SUBROUTINE fcx_finish_phase
 
     SUBROUTINE fcx_detach()
         INTEGER(c_int) :: r

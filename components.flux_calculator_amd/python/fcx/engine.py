@@ -141,6 +141,10 @@ class Engine:
     def step(self, phase=PHASE_ALL, current_step_time=0):
         _lib.check(self.lib.fcx_step(self.h, phase, int(current_step_time)))
 
+    def step_async(self, phase=PHASE_ALL, current_step_time=0):
+        """fcx_step_async: the step queued; the host arrays hold the outputs after synchronize()."""
+        _lib.check(self.lib.fcx_step_async(self.h, phase, int(current_step_time)))
+
     def set_stream(self, stream):
         """fcx_set_stream: launch on this HIP stream (a raw hipStream_t, e.g. a torch
         stream's .cuda_stream) from now on, e.g. a capturing stream for a HIP graph."""

@@ -160,6 +160,14 @@ int fcx_step(fcx_engine *e, int phase, int32_t current_step_time);
  * FCX_OPT_DEFERRED_SCATTER they are filled from the staging arena here.  fcx_step and the
  * per-call subroutines end with it. */
 int fcx_synchronize(fcx_engine *e);
+/* fcx_step without its final wait (the asynchronous phase): when it returns the engine holds
+ * the inputs (caller heap arrays are copied into the staging arena inside the call, so the
+ * host may overwrite them), the launch and the output DMAs are queued, and the caller's
+ * output arrays are filled by the next fcx_synchronize.  Inputs in fcx_host_malloc memory
+ * are read in place until then.  A host starts several engines this way from one thread (each
+ * on its own stream), or overlaps its own work -- another component's exchange -- with the
+ * step.  Host-bound grids of at least two pipeline chunks complete inside the call. */
+int fcx_step_async(fcx_engine *e, int phase, int32_t current_step_time);
 
 /* ---- per call: the reference subroutines one by one (exact drop-in semantics; each
  * call uploads what it reads, computes, downloads what it writes, and synchronises) ---- */

@@ -8,7 +8,7 @@
 ! No regridding matrices are set, so the reference's do_regridding calls between the
 ! calc_* calls would be no-ops and are left out.
 !
-!   dropin_host <dir> percall|fused|noattach|badtable|badgrid|badtypes[+abort]
+!   dropin_host <dir> percall|fused|async|noattach|badtable|badgrid|badtypes[+abort]
 !
 ! +abort: the host registers its abort routine (fcx_register_abort) first, as a coupled
 ! host registers one that calls oasis_abort; this one prints the message and stops with 3.
@@ -141,14 +141,23 @@ PROGRAM dropin_host
         CALL average_across_surface_types(1, 22, nsurf + 1, grid_size, local_field)
     ENDIF
 
-    IF (TRIM(mode) == 'fused') THEN
+    IF (TRIM(mode) == 'fused' .OR. TRIM(mode) == 'async') THEN
         ! INTEGRATION.md: two phases replace :902-918 and :972-1008
         DO i = 1, nav
             CALL fcx_register_average(av(1, i) == 1, av(2, i), av(3, i))
         ENDDO
         CALL fcx_commit_engine()
-        CALL fcx_run_phase(FCX_PHASE_EARLY)
-        CALL fcx_run_phase(FCX_PHASE_NORMAL)
+        IF (TRIM(mode) == 'async') THEN
+            ! each phase started, then finished; the early phase's outputs are complete
+            ! before the normal phase starts (its oasis_put precedes the normal oasis_get)
+            CALL fcx_start_phase(FCX_PHASE_EARLY)
+            CALL fcx_finish_phase()
+            CALL fcx_start_phase(FCX_PHASE_NORMAL)
+            CALL fcx_finish_phase()
+        ELSE
+            CALL fcx_run_phase(FCX_PHASE_EARLY)
+            CALL fcx_run_phase(FCX_PHASE_NORMAL)
+        ENDIF
     ELSE
         CALL fcx_commit_engine()
         ! flux_calculator.F90:902 and the early type-0 outputs (:909-918, P7 trigger)

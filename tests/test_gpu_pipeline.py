@@ -354,3 +354,50 @@ def test_staging_arena_failure_falls_back_to_direct_copies(monkeypatch):
                  averages=case.averages, options=opts)
     assert eng.staging_bytes() == 0
     eng.close()
+
+
+@pytest.mark.parametrize("n", [32_768, 600_001])
+def test_step_async_engines_started_from_one_thread(n):
+    """fcx_step_async (the asynchronous phase, Fortran fcx_start_phase / fcx_finish_phase):
+    three engines on their own streams started one after the other from ONE host thread,
+    the host overwriting every input array before it synchronizes (as the next oasis_get
+    would) -- the outputs are those of fcx_step on the inputs at the start, bit for bit.  At
+    32,768 cells the downloads complete at fcx_synchronize; at 600,001 the chunk pipeline
+    completes inside the call."""
+    import torch
+
+    variants = ("CCLM", "MOM5", "RCO")
+    cases = [build_case(v, n=n, T=1, bias=True, seed=3 + i) for i, v in enumerate(variants)]
+    want = []
+    for c in cases:  # reference: the synchronous step of fresh engines
+        for k in c.outputs:
+            c.lf.field[k][:] = np.nan
+        e = Engine(c.lf, 1, c.methods, corrections=c.corrections)
+        e.step(PHASE_ALL, STEP_T)
+        want.append({k: np.array(c.lf.field[k], copy=True) for k in c.outputs})
+        e.close()
+    streams = [torch.cuda.Stream() for _ in cases]
+    engines = [Engine(c.lf, 1, c.methods, corrections=c.corrections, stream=s.cuda_stream)
+               for c, s in zip(cases, streams)]
+    inputs = []
+    for c in cases:
+        seen = set()
+        for k, a in c.lf.field.items():
+            if k not in c.outputs and id(a) not in seen:
+                seen.add(id(a))
+                inputs.append((a, a.copy()))
+        for k in c.outputs:
+            c.lf.field[k][:] = np.nan
+    for e in engines:
+        e.step_async(PHASE_ALL, STEP_T)
+    for a, _ in inputs:  # the host reuses its input arrays before the steps are waited for
+        a *= 2.0
+    for e in engines:
+        e.synchronize()
+    got = [{k: np.array(c.lf.field[k], copy=True) for k in c.outputs} for c in cases]
+    for e in engines:
+        e.close()
+    for a, orig in inputs:
+        a[:] = orig
+    for g, w in zip(got, want):
+        same_bits(g, w)
