@@ -1,0 +1,90 @@
+#!/usr/bin/env python3
+"""The Baltic-size drop-in (32,768 cells, caller heap arrays) under several transports, to
+find the one closest to the host-link bound (link_probe.py): median wall time of fcx_step
+of each variant alone, and of the three variants started with fcx_step_async from one host
+thread then synchronised.
+
+  python components.flux_calculator_amd/bench/baltic_probe.py [--cells 32768] [--steps 400]
+    [--mode NAME:opt=val,opt=val ...]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.join(ROOT, "components.flux_calculator_amd", "python"))
+
+VARIANTS = ("CCLM", "MOM5", "RCO")
+MODES = [
+    "default:",
+    "zc_chunks4:zero_copy=1,pipeline_min_chunk=8192,pipeline_chunks=4",
+    "zc_chunks8:zero_copy=1,pipeline_min_chunk=4096,pipeline_chunks=8",
+    "dma_chunks4:zero_copy=0,pipeline_min_chunk=8192,pipeline_chunks=4",
+    "dma_seq:zero_copy=0",
+]
+
+
+def parse_mode(m):
+    name, _, rest = m.partition(":")
+    opts = {}
+    for kv in filter(None, rest.split(",")):
+        k, v = kv.split("=")
+        opts[k] = int(v)
+    return name, opts
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--cells", type=int, default=32_768)
+    ap.add_argument("--steps", type=int, default=400)
+    ap.add_argument("--mode", action="append", default=[])
+    a = ap.parse_args()
+
+    import torch
+    from fcx.basic import PHASE_ALL
+    from fcx.engine import Engine
+    from fcx.synthetic import build_case, inputs_for_bench
+
+    n = a.cells
+    data = inputs_for_bench(n)
+    out = {"cells": n, "steps": a.steps, "modes": {}}
+    for m in a.mode or MODES:
+        name, opts = parse_mode(m)
+        cases = [build_case(v, n=n, T=1, bias=True, data=data) for v in VARIANTS]
+        streams = [torch.cuda.Stream() for _ in cases]
+        engines = [Engine(c.lf, 1, c.methods, corrections=c.corrections, stream=s.cuda_stream, options=opts)
+                   for c, s in zip(cases, streams)]
+        res = {"options": opts}
+        for v, e in zip(VARIANTS, engines):
+            for k in range(50):
+                e.step(PHASE_ALL, k * 3600)
+            ts = []
+            for k in range(a.steps):
+                t0 = time.perf_counter()
+                e.step(PHASE_ALL, k * 3600)
+                ts.append(time.perf_counter() - t0)
+            res[v] = round(float(np.median(ts)) * 1e6, 1)
+        res["sequential_sum_us"] = round(sum(res[v] for v in VARIANTS), 1)
+        ts = []
+        for k in range(50 + a.steps):
+            t0 = time.perf_counter()
+            for e in engines:
+                e.step_async(PHASE_ALL, k * 3600)
+            for e in engines:
+                e.synchronize()
+            if k >= 50:
+                ts.append(time.perf_counter() - t0)
+        res["async_three_us"] = round(float(np.median(ts)) * 1e6, 1)
+        for e in engines:
+            e.close()
+        out["modes"][name] = res
+        print(name, json.dumps(res), flush=True)
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
