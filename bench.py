@@ -293,7 +293,11 @@ def e2e_concurrent(args, variants, n=32_768, steps=500):
 def e2e_async(args, variants, n=32_768, steps=500):
     """The variants' steps started one after the other from ONE host thread with
     fcx_step_async (each engine on its own stream), then every engine synchronised: the
-    asynchronous phase, no host threads of the caller's.  Wall time per step."""
+    asynchronous phase, no host threads of the caller's.  Transport: the staging arena with
+    DMA (FCX_OPT_ZERO_COPY 0) -- one engine's host copies then overlap the others' DMAs;
+    with the kernels reading the arena over the link (zero-copy, the one-engine default)
+    the three steps take 320 us instead of 258 (bench/baltic_probe.py,
+    profiles/r05/baltic_probe.json).  Wall time per step."""
     import torch
     from fcx.basic import PHASE_ALL
     from fcx.engine import Engine
@@ -304,7 +308,7 @@ def e2e_async(args, variants, n=32_768, steps=500):
     cases = [build_case(v, n=n, T=args.types, bias=args.bias, data=data if args.types == 1 else None)
              for v in variants]
     engines = [Engine(c.lf, c.num_surface_types, c.methods, corrections=c.corrections, averages=c.averages,
-                      stream=st.cuda_stream) for c, st in zip(cases, streams)]
+                      stream=st.cuda_stream, options={"zero_copy": 0}) for c, st in zip(cases, streams)]
     ts = []
     for k in range(50 + steps):
         t0 = time.perf_counter()
@@ -319,6 +323,7 @@ def e2e_async(args, variants, n=32_768, steps=500):
     med = float(np.median(ts))
     return {"us_per_step_median": round(med * 1e6, 1), "us_per_step_p90": round(float(np.percentile(ts, 90)) * 1e6, 1),
             "steps": steps, "engines": len(engines),
+            "transport": "staging arena + DMA (FCX_OPT_ZERO_COPY 0)",
             "rule": "fcx_step_async of every variant's engine (own stream) from one host thread, then fcx_synchronize "
                     "of each; a step = first start to the last engine synchronised"}
 
