@@ -699,9 +699,25 @@ __device__ __forceinline__ int lds_slot(int e) { return e + 2 * (e >> 4); }
 // order, in 4 instead of 6 row-lengths of fp64 per wave (more waves per CU).
 template <int C>
 constexpr int xrows_doubles() { return kFusedFields * tile_cells<C>() / 2; }
+// fp32 (C = 4, up to 4 segment starts per lane): the tile's segments are summed by ordinal --
+// segment s of the tile by lane s % 64 in round s / 64 -- so that each round's atmosphere
+// stores are ONE contiguous run of atmosphere cells per field.  Summed by the lane holding
+// its first cell (the fp64 rule, at most one start per lane there) the rounds interleave:
+// round 1 takes every lane's first segment, round 2 the second ones in between, and each
+// 128-B output line is written piecewise by two store instructions.  The list of the tile's
+// segments sits behind the weights row: per segment its first cell and length - 1 (one byte
+// each: a tile has 256 cells) and its atmosphere cell, room for one segment per cell (6 B x
+// 256 = 192 doubles).  16 waves per CU then hold 156 KiB of LDS.
+#ifndef FCX_F32_SEG_ORDINAL
+#define FCX_F32_SEG_ORDINAL 1
+#endif
+constexpr int kSegCap = 192;  // doubles of the list (tile_cells<4>() x (2 + 4) bytes)
+template <class R, int C>
+constexpr bool seg_ordinal() { return FCX_F32_SEG_ORDINAL && sizeof(R) == 4 && C == 4; }
 template <class R, int C>
 constexpr int wave_lds_doubles(int rows) {
-  return sizeof(R) == 4 ? xrows_doubles<C>() + row_len<C>() : rows * row_len<C>();
+  return sizeof(R) == 4 ? xrows_doubles<C>() + row_len<C>() + (seg_ordinal<R, C>() ? kSegCap : 0)
+                        : rows * row_len<C>();
 }
 
 template <int C>
@@ -756,8 +772,10 @@ constexpr uint32_t kXcds = 8;
 #define FCX_XCD_CHUNK 64
 #endif
 #ifndef FCX_XCD_CHUNK_F32  // ... and of the fp32 kernels (256-cell tiles): 16 against 64,
-#define FCX_XCD_CHUNK_F32 16  // step -0.7 % (shared arrays) / -4.0 % (own mirrors),
-#endif                        // profiles/r03/xcd_map_ab/f32_*
+#define FCX_XCD_CHUNK_F32 32  // step -0.7 % (shared arrays) / -4.0 % (own mirrors),
+#endif                        // profiles/r03/xcd_map_ab/f32_*; round 5, the fp32 group launch:
+                              // 32 against 16 -1.0 / -1.2 % (two boxes), 64 -0.2 %, and with
+                              // the ordinal segment rounds -2.1 % (profiles/r05/ord/)
 template <uint32_t K>
 __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb) {
   constexpr uint32_t row = K * kXcds;  // runs of K workgroups per XCD, the XCDs side by side
@@ -927,6 +945,58 @@ __device__ __forceinline__ void atmos_tile(const Params *__restrict__ P, const d
 #pragma unroll
     for (int i = 0; i < C; ++i)
       if (st[i] && a[i] >= 0 && (!HALO || lane < own_lanes)) rem |= 1u << i;
+    // the end of the segment starting at cell C*lane+i: the next start of any kind (own,
+    // halo, past the grid end), or the tile end
+    auto seg_end = [&](int i) {
+      int e_end = kT;
+#pragma unroll
+      for (int q = 0; q < C; ++q) e_end = min(e_end, C * first_bit(m[q] & (q > i ? at_or_above : above)) + q);
+      return min(e_end, kT);
+    };
+    // ... of the segment starting at any cell c of the tile (the lane summing it need not hold it)
+    auto seg_end_of = [&](int c) {
+      const int l = c / C, i = c % C;
+      const uint64_t ge = ~0ull << l, gt = l == 63 ? 0ull : (~0ull << (l + 1));
+      int e_end = kT;
+#pragma unroll
+      for (int q = 0; q < C; ++q) e_end = min(e_end, C * first_bit(m[q] & (q > i ? ge : gt)) + q);
+      return min(e_end, kT);
+    };
+    if constexpr (seg_ordinal<R, C>()) {
+      static_assert(kT == 256 && kSegCap * 8 == kT * 6, "one list entry per cell of the tile");
+      uint16_t *seg = reinterpret_cast<uint16_t *>(wp + xrows_doubles<C>() + row_len<C>());  // [kT]
+      int32_t *seg_a = reinterpret_cast<int32_t *>(seg + kT);                                 // [kT]
+      const uint64_t lower = (1ull << lane) - 1;
+      int total = 0, o = 0;  // the tile's segments; this lane's first one's ordinal
+#pragma unroll
+      for (int q = 0; q < C; ++q) {
+        const uint64_t b = __ballot((rem >> q) & 1u);
+        total += __popcll(b);
+        o += __popcll(b & lower);
+      }
+#pragma unroll
+      for (int i = 0; i < C; ++i)
+        if ((rem >> i) & 1u) {
+          seg[o] = (uint16_t)(C * lane + i);
+          seg_a[o] = a[i];
+          ++o;
+        }
+      wave_sync();
+      for (int base = 0; base < total; base += 64) {
+        const int sg = base + lane;
+        if (sg < total) {
+          const int c = seg[sg];
+          const int end = seg_end_of(c);
+          const int32_t ai = seg_a[sg];
+          double acc[kFusedFields];
+#pragma unroll
+          for (int k = 0; k < kFusedFields; ++k) acc[k] = 0.0;
+          for (int e = c; e < end; ++e) add_cell(acc, e);
+          segment_done<R>(af, tile, ai, acc, !HALO && end == kT && next_a == ai);
+        }
+      }
+      rem = 0;
+    }
     while (__ballot(rem != 0)) {
       if (rem) {
         const int i = __builtin_ctz(rem);
@@ -937,10 +1007,7 @@ __device__ __forceinline__ void atmos_tile(const Params *__restrict__ P, const d
           if (q == i) ai = a[q];
         const int c = C * lane + i;
         // next start after cell c: cell C*j+i' with j > l, or j == l and i' > i
-        int e_end = kT;
-#pragma unroll
-        for (int q = 0; q < C; ++q) e_end = min(e_end, C * first_bit(m[q] & (q > i ? at_or_above : above)) + q);
-        const int end = min(e_end, kT);
+        const int end = seg_end(i);
         double acc[kFusedFields];
 #pragma unroll
         for (int k = 0; k < kFusedFields; ++k) acc[k] = 0.0;
