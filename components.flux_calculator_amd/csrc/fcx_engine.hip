@@ -2217,18 +2217,12 @@ struct GroupLaunchMember {
 };
 static int launch_group(const GroupLaunchMember *mem, int nm);
 
-// fcx_run of several engines (e.g. one per bottom-model variant) in the order given, with
-// the flux passes of those whose whole phase is one fused T = 1 launch of the same shape on
-// the same stream merged into ONE launch (cells_atmos_group_kernel).  Each engine then does
-// what follows its launch in fcx_run (fix-up, accumulation, exchange, remaps).  The others
-// run as fcx_run.  Same results, bit for bit, as fcx_run of each.
-extern "C" int fcx_run_group(fcx_engine *const *es, int n, int phase, int32_t t) {
-  if (n < 0 || (n > 0 && !es)) return fail(FCX_E_ARG, "bad engine list");
-  if (phase < 1 || phase > 3) return fail(FCX_E_ARG, "phase %d unknown", phase);
-  for (int i = 0; i < n; ++i)
-    if (int r = check(es[i])) return r;
-  std::vector<GroupLaunchMember> mem;
-  std::vector<int> member_of(n, -1);  // list position -> member index (-1: runs as fcx_run)
+// the engines of a list that can share one merged launch (fcx_run_group's rule): member_of[i]
+// = their index in mem, -1 for the engines that run as fcx_run.  A single one is kept.
+static int select_group(fcx_engine *const *es, int n, int phase, int32_t t, std::vector<GroupLaunchMember> &mem,
+                        std::vector<int> &member_of) {
+  mem.clear();
+  member_of.assign((size_t)n, -1);
   for (int i = 0; i < n; ++i) {
     fcx_engine *e = es[i];
     bool ok = !e->any_regrid && !e->timing && (int)mem.size() < kMaxGroup;
@@ -2255,6 +2249,22 @@ extern "C" int fcx_run_group(fcx_engine *const *es, int n, int phase, int32_t t)
       mem.push_back(m);
     }
   }
+  return FCX_OK;
+}
+
+// fcx_run of several engines (e.g. one per bottom-model variant) in the order given, with
+// the flux passes of those whose whole phase is one fused T = 1 launch of the same shape on
+// the same stream merged into ONE launch (cells_atmos_group_kernel).  Each engine then does
+// what follows its launch in fcx_run (fix-up, accumulation, exchange, remaps).  The others
+// run as fcx_run.  Same results, bit for bit, as fcx_run of each.
+extern "C" int fcx_run_group(fcx_engine *const *es, int n, int phase, int32_t t) {
+  if (n < 0 || (n > 0 && !es)) return fail(FCX_E_ARG, "bad engine list");
+  if (phase < 1 || phase > 3) return fail(FCX_E_ARG, "phase %d unknown", phase);
+  for (int i = 0; i < n; ++i)
+    if (int r = check(es[i])) return r;
+  std::vector<GroupLaunchMember> mem;
+  std::vector<int> member_of;  // list position -> member index (-1: runs as fcx_run)
+  if (int r = select_group(es, n, phase, t, mem, member_of)) return r;
   if (mem.size() == 1) {  // nothing to merge
     std::fill(member_of.begin(), member_of.end(), -1);
     mem.clear();
@@ -2277,10 +2287,8 @@ extern "C" int fcx_run_group(fcx_engine *const *es, int n, int phase, int32_t t)
   return FCX_OK;
 }
 
-// the merged launch of fcx_run_group's members, their crossing-record fix-ups as one launch
-// and their empty-cell stores (what precedes run_tail in fcx_run)
-static int launch_group(const GroupLaunchMember *mem, int nm) {
-  GroupMember gm[kMaxGroup];
+// the members' group arguments (af.n_tiles: each member's tile count) and their run state reset
+static void group_members(const GroupLaunchMember *mem, int nm, GroupMember *gm) {
   for (int k = 0; k < nm; ++k) {
     const GroupLaunchMember &m = mem[k];
     fcx_engine *e = m.e;
@@ -2292,6 +2300,13 @@ static int launch_group(const GroupLaunchMember *mem, int nm) {
     gm[k] = GroupMember{m.pl->dev, m.corr_m, 0, m.lc.variant, 0, m.pl->af};
     gm[k].af.n_tiles = (m.pl->host.n_max + own - 1) / own;
   }
+}
+
+// the merged launch of fcx_run_group's members, their crossing-record fix-ups as one launch
+// and their empty-cell stores (what precedes run_tail in fcx_run)
+static int launch_group(const GroupLaunchMember *mem, int nm) {
+  GroupMember gm[kMaxGroup];
+  group_members(mem, nm, gm);
   const int r = launch_cells_group(gm, nm, mem[0].lc, mem[0].e->stream);
   if (r) return fail(FCX_E_HIP, "cells_atmos_group_kernel launch: %s", hipGetErrorString((hipError_t)r));
   // the members' crossing-record fix-ups (launch_fixup's rule) as one launch
@@ -3079,6 +3094,11 @@ struct fcx_comm {
   double *agree = nullptr;  // 2 * kSigWords doubles (device)
   std::vector<double> agreed;
   bool verify_every = false;  // fcx_comm_verify: the agreement before every exchange
+  // fcx_run_group_exchange: the boundary tiles' launch and the all-reduce run on this stream
+  // beside the engines' main launch
+  hipStream_t side = nullptr;
+  hipEvent_t ev_side = nullptr;
+  int64_t overlapped = 0;  // exchanges that ran beside a main launch (fcx_comm_overlapped)
 };
 
 extern "C" int fcx_comm_unique_id(void *id) {
@@ -3112,6 +3132,9 @@ extern "C" int fcx_comm_create(int device, int nranks, int rank, const void *id,
 extern "C" int fcx_comm_destroy(fcx_comm *c) {
   if (!c) return FCX_OK;
   for (hipEvent_t ev : c->events) (void)hipEventDestroy(ev);
+  if (c->side) (void)hipStreamSynchronize(c->side);
+  if (c->ev_side) (void)hipEventDestroy(c->ev_side);
+  if (c->side) (void)hipStreamDestroy(c->side);
   (void)hipFree(c->scratch);
   (void)hipFree(c->agree);
   if (c->comm) (void)rccl().CommDestroy(c->comm);
@@ -3179,7 +3202,10 @@ extern "C" int fcx_comm_verify(fcx_comm *c, int every_exchange) {
   return FCX_OK;
 }
 
-static int atmos_exchange(fcx_comm *c, fcx_engine *const *es, int n) {
+// s_coll: the stream of the collective (default: the first engine's, joined with the others'
+// before it); given, the slots are already complete in its order (fcx_run_group_exchange) and
+// only the finishes join the engines' streams after it
+static int atmos_exchange(fcx_comm *c, fcx_engine *const *es, int n, hipStream_t s_coll = nullptr) {
   std::vector<fcx_engine *> v;  // the engines with boundary slots, in list order
   for (int i = 0; i < n; ++i)
     if (es[i]->atm_shared && es[i]->atm_nb > 0 && es[i]->atm_stride > 0) v.push_back(es[i]);
@@ -3189,10 +3215,10 @@ static int atmos_exchange(fcx_comm *c, fcx_engine *const *es, int n) {
     total += (size_t)e->atm_nb * e->atm_stride;
     hash = (hash * 1000003ull + (uint64_t)e->atm_nb * 4099ull + (uint64_t)e->atm_stride) & ((1ull << 48) - 1);
   }
-  hipStream_t s0 = n > 0 ? es[0]->stream : nullptr;
+  hipStream_t s0 = s_coll ? s_coll : n > 0 ? es[0]->stream : nullptr;
   if (int r = exchange_agree(c, {(double)v.size(), (double)total, (double)hash}, s0)) return r;
   if (v.empty()) return FCX_OK;
-  s0 = v[0]->stream;
+  if (!s_coll) s0 = v[0]->stream;
   std::vector<char> fresh(v.size());
   int stale = -1;  // first engine with no accumulation since its last exchange
   bool inplace = true;
@@ -3204,6 +3230,7 @@ static int atmos_exchange(fcx_comm *c, fcx_engine *const *es, int n) {
   }
   size_t joins = 0;
   for (auto *e : v) joins += e->stream != s0 ? 2 : 0;
+  const bool pre_join = s_coll == nullptr;
   while (c->events.size() < joins) {
     hipEvent_t ev;
     HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
@@ -3211,7 +3238,7 @@ static int atmos_exchange(fcx_comm *c, fcx_engine *const *es, int n) {
   }
   size_t k = 0;
   for (auto *e : v)
-    if (e->stream != s0) {  // the all-reduce waits for that engine's accumulation
+    if (e->stream != s0 && pre_join) {  // the all-reduce waits for that engine's accumulation
       HIP_TRY(hipEventRecord(c->events[k], e->stream));
       HIP_TRY(hipStreamWaitEvent(s0, c->events[k++], 0));
     }
@@ -3258,6 +3285,102 @@ static int atmos_exchange(fcx_comm *c, fcx_engine *const *es, int n) {
                 "boundary exchange: engine %d of the list has no accumulation since its last exchange (fcx_run or "
                 "fcx_run_atmos first); it took part with zeros",
                 stale);
+  return FCX_OK;
+}
+
+// fcx_run_group + fcx_atmos_allreduce with the exchange overlapped: the tiles that write
+// boundary slots (the segment of each engine's first and last atmosphere cell) go out first,
+// as their own small group launch on the communicator's side stream, followed there by the
+// all-reduce; the other tiles run meanwhile as the main group launch on the engines' stream,
+// and the finishes wait for both.  The collective sequence is that of fcx_atmos_allreduce
+// (same agreement, same all-reduce), so ranks that take the sequential fallback -- some
+// engine cannot merge, no halo tiles, remaps, an attached communicator -- stay matched.
+static int run_group_exchange(fcx_comm *c, fcx_engine *const *es, int n, int phase, int32_t t) {
+  std::vector<GroupLaunchMember> mem;
+  std::vector<int> member_of;
+  if (int r = select_group(es, n, phase, t, mem, member_of)) return r;
+  bool split = (int)mem.size() == n && n >= 1;
+  for (size_t k = 0; split && k < mem.size(); ++k) {
+    const fcx_engine *e = mem[k].e;
+    split = member_of[k] == (int)k && !e->comm && mem[k].lc.halo > 0 && e->remaps.empty() && e->atm_shared &&
+            e->atm_nb > 0 && e->atm_stride > 0 && e->n_atmos > 0 && (int64_t)e->atm_row.size() > e->n_atmos;
+  }
+  if (!split) {
+    if (int r = fcx_run_group(es, n, phase, t)) return r;
+    return atmos_exchange(c, es, n);
+  }
+  const int nm = (int)mem.size();
+  GroupMember gm[kMaxGroup];
+  group_members(mem.data(), nm, gm);
+  // each member's boundary tiles: tile 0 (its first atmosphere cell's segment starts at cell
+  // 0) when that cell is shared, and the tile where its last atmosphere cell's segment starts
+  int64_t brange[2 * kMaxGroup][3], mrange[3 * kMaxGroup][3];
+  int nb = 0, nmr = 0;
+  for (int k = 0; k < nm; ++k) {
+    const fcx_engine *e = mem[k].e;
+    const int64_t own = (mem[k].lc.f32 ? kF32Cpl : 2) * (64 - mem[k].lc.halo), nt = gm[k].af.n_tiles;
+    int64_t b[2];
+    int cnt = 0;
+    if (e->atm_left >= 0) b[cnt++] = 0;
+    if (e->atm_right >= 0) {
+      const int64_t r = std::min<int64_t>(e->atm_row[(size_t)e->n_atmos - 1] / own, nt - 1);
+      if (!cnt || r != b[0]) b[cnt++] = r;
+    }
+    int64_t at = 0;
+    for (int j = 0; j < cnt; ++j) {
+      brange[nb][0] = k, brange[nb][1] = b[j], brange[nb++][2] = 1;
+      if (b[j] > at) mrange[nmr][0] = k, mrange[nmr][1] = at, mrange[nmr++][2] = b[j] - at;
+      at = b[j] + 1;
+    }
+    if (nt > at) mrange[nmr][0] = k, mrange[nmr][1] = at, mrange[nmr++][2] = nt - at;
+  }
+  hipStream_t s_eng = mem[0].e->stream;
+  if (!c->side) {
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreateWithFlags(&c->ev_side, hipEventDisableTiming));
+  }
+  HIP_TRY(hipEventRecord(c->ev_side, s_eng));  // the engines' earlier work (uploads) first
+  HIP_TRY(hipStreamWaitEvent(c->side, c->ev_side, 0));
+  if (nb) {
+    const int r = launch_cells_group(gm, nm, mem[0].lc, c->side, brange, nb);
+    if (r) return fail(FCX_E_HIP, "cells_atmos_group_kernel (boundary tiles) launch: %s", hipGetErrorString((hipError_t)r));
+  }
+  if (nmr) {
+    const int r = launch_cells_group(gm, nm, mem[0].lc, s_eng, mrange, nmr);
+    if (r) return fail(FCX_E_HIP, "cells_atmos_group_kernel launch: %s", hipGetErrorString((hipError_t)r));
+  }
+  for (int k = 0; k < nm; ++k) {
+    if (int r = launch_empty_cells(mem[k].e, mem[k].pl, mem[k].lc)) return r;
+    fcx_engine *e = mem[k].e;
+    e->group_members = nm;
+    e->atm_done_fused = true;
+    e->atm_done = true;
+  }
+  // the collective on the side stream (after the boundary tiles), the finishes on the engines'
+  // stream (after the main launch and the collective)
+  if (int r = atmos_exchange(c, es, n, c->side)) return r;
+  ++c->overlapped;
+  for (int k = 0; k < nm; ++k) {
+    fcx_engine *e = mem[k].e;
+    if (e->timing) HIP_TRY(hipEventRecord(e->ev1, e->stream));
+    e->timed = e->timing;
+  }
+  return FCX_OK;
+}
+
+extern "C" int fcx_run_group_exchange(fcx_comm *c, fcx_engine *const *es, int n, int phase, int32_t t) {
+  if (!c) return fail(FCX_E_ARG, "NULL communicator");
+  if (n < 0 || (n > 0 && !es)) return fail(FCX_E_ARG, "bad engine list");
+  if (phase < 1 || phase > 3) return fail(FCX_E_ARG, "phase %d unknown", phase);
+  for (int i = 0; i < n; ++i)
+    if (int r = check(es[i])) return r;
+  return run_group_exchange(c, es, n, phase, t);
+}
+
+extern "C" int fcx_comm_overlapped(fcx_comm *c, int64_t *count) {
+  if (!c || !count) return fail(FCX_E_ARG, "NULL argument");
+  *count = c->overlapped;
   return FCX_OK;
 }
 

@@ -1128,16 +1128,18 @@ cells_atmos_group_kernel(const GroupArgs g, const Params *__restrict__ P0, const
   const int64_t wave0 =
       (int64_t)xcd_block<C == 4 ? FCX_XCD_CHUNK_F32 : FCX_XCD_CHUNK>(blockIdx.x, gridDim.x) * (blockDim.x >> 6) + wv;
   for (int64_t t = wave0; t < g.total_tiles; t += waves) {
-    // the member of tile t: wave-uniform, said so to the compiler (readfirstlane), so that
-    // its parameters are scalar loads -- derived from threadIdx.x >> 6, the index would be
-    // taken for a per-lane value and every member field would occupy VGPRs
-    int k = 0;
-    for (int q = 1; q < g.n; ++q)
-      if (t >= g.m[q].tile0) k = q;
-    k = __builtin_amdgcn_readfirstlane(k);
+    // the range and member of tile t: wave-uniform, said so to the compiler (readfirstlane),
+    // so that their parameters are scalar loads -- derived from threadIdx.x >> 6, the index
+    // would be taken for a per-lane value and every member field would occupy VGPRs
+    int q = 0;
+    for (int j = 1; j < g.n_ranges; ++j)
+      if (t >= g.r[j].t0) q = j;
+    q = __builtin_amdgcn_readfirstlane(q);
+    const GroupRange &rg = g.r[q];
+    const int k = __builtin_amdgcn_readfirstlane(rg.member);
     const GroupMember &m = g.m[k];
     const Params *__restrict__ P = k == 0 ? P0 : k == 1 ? P1 : k == 2 ? P2 : P3;
-    const int64_t tile = t - m.tile0;
+    const int64_t tile = t - rg.t0 + rg.first;
     switch (m.var) {
       case 1: atmos_tile<C, R, 1, NT, TM, RAVG, false, HALO>(P, m.corr_m, m.af, tile, wp); break;
       case 2: atmos_tile<C, R, 2, NT, TM, RAVG, false, HALO>(P, m.corr_m, m.af, tile, wp); break;
@@ -1614,7 +1616,8 @@ static void launch_group_h(bool halo, bool ravg, int blocks, hipStream_t s, cons
                        g, p[0], p[1], p[2], p[3]);
 }
 
-int launch_cells_group(GroupMember *members, int n, const LaunchConfig &lc, void *stream) {
+int launch_cells_group(GroupMember *members, int n, const LaunchConfig &lc, void *stream,
+                       const int64_t (*ranges)[3], int n_ranges) {
   if (n < 1 || n > kMaxGroup) return (int)hipErrorInvalidValue;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   GroupArgs g{};
@@ -1625,8 +1628,26 @@ int launch_cells_group(GroupMember *members, int n, const LaunchConfig &lc, void
     if (m.var < 1 || m.var > 3 || (m.af.halo > 0) != (lc.halo > 0) || m.af.n_tiles < 0)
       return (int)hipErrorInvalidValue;
     m.tile0 = total;
-    total += m.af.n_tiles;
     g.m[k] = m;
+    if (!ranges) {
+      g.r[k] = GroupRange{total, 0, k, 0};
+      total += m.af.n_tiles;
+    }
+  }
+  if (ranges) {  // the caller's ranges, each inside its member's tiles
+    if (n_ranges < 1 || n_ranges > kMaxGroupRanges) return (int)hipErrorInvalidValue;
+    int used = 0;
+    for (int j = 0; j < n_ranges; ++j) {
+      const int64_t mk = ranges[j][0], first = ranges[j][1], cnt = ranges[j][2];
+      if (mk < 0 || mk >= n || first < 0 || cnt < 0 || first + cnt > members[mk].af.n_tiles)
+        return (int)hipErrorInvalidValue;
+      if (cnt == 0) continue;
+      g.r[used++] = GroupRange{total, first, (int32_t)mk, 0};
+      total += cnt;
+    }
+    g.n_ranges = used;
+  } else {
+    g.n_ranges = n;
   }
   g.total_tiles = total;
   if (total == 0) return 0;

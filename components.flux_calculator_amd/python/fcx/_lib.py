@@ -93,6 +93,8 @@ SIGNATURES = [
     ("fcx_memcpy", _I, [_P, _P, _c.c_size_t, _I]),
     ("fcx_last_group_size", _I, [_P, _c.POINTER(_I32)]),
     ("fcx_step_async", _I, [_P, _I, _I32]),
+    ("fcx_run_group_exchange", _I, [_P, _c.POINTER(_P), _I, _I, _I32]),
+    ("fcx_comm_overlapped", _I, [_P, _c.POINTER(_I64)]),
     ("fcx_comm_verify", _I, [_P, _I]),
     ("fcx_set_abort_handler", _I, [_P]),
     ("fcx_abort", _I, [_c.c_char_p]),

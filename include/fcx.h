@@ -281,6 +281,19 @@ int fcx_atmos_allreduce(fcx_comm *c, fcx_engine *const *engines, int n_engines);
 /* 1: the signature agreement before every exchange of the communicator; 0 (default): before
  * the first exchange of each signature */
 int fcx_comm_verify(fcx_comm *c, int every_exchange);
+/* fcx_run_group of the engines followed by fcx_atmos_allreduce over them, with the exchange
+ * overlapped: the wave tiles that write boundary slots (each engine's first and last
+ * atmosphere cell) run first as a small launch on the communicator's own stream, the
+ * all-reduce follows there while the other tiles run as the main launch on the engines'
+ * stream, and the finishes wait for both -- a step costs the flux pass plus the finish
+ * instead of the flux pass plus the all-reduce latency.  Results and the collective sequence
+ * are those of fcx_run_group + fcx_atmos_allreduce; engines that cannot take the split (not
+ * all merged into one T = 1 launch with halo tiles, remaps, an attached communicator) run
+ * exactly that way. */
+int fcx_run_group_exchange(fcx_comm *c, fcx_engine *const *engines, int n_engines, int phase,
+                           int32_t current_step_time);
+/* how many exchanges of the communicator ran beside a main launch (the split above) */
+int fcx_comm_overlapped(fcx_comm *c, int64_t *count);
 
 /* ---- exchange-grid -> model remaps ----
  * The SCRIP weight application OASIS3-MCT performs on the 'S' fields sent to a model
