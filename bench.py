@@ -587,6 +587,8 @@ def main():
             traffic = None
 
     mg = multi_gpu_check(wl, world, rank, dist) if la is not None else None
+    if mg is not None and comm is not None and hasattr(comm, "overlapped"):
+        mg["exchanges_overlapped"] = comm.overlapped()  # fcx_run_group_exchange steps that split
 
     out = {
         "metric": METRIC,
