@@ -17,6 +17,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <mutex>
 #include <set>
@@ -3205,7 +3206,10 @@ extern "C" int fcx_comm_verify(fcx_comm *c, int every_exchange) {
 // s_coll: the stream of the collective (default: the first engine's, joined with the others'
 // before it); given, the slots are already complete in its order (fcx_run_group_exchange) and
 // only the finishes join the engines' streams after it
-static int atmos_exchange(fcx_comm *c, fcx_engine *const *es, int n, hipStream_t s_coll = nullptr) {
+// between: work to queue after the collective and before the finishes (the main launch of
+// fcx_run_group_exchange, so that the all-reduce is queued first)
+static int atmos_exchange(fcx_comm *c, fcx_engine *const *es, int n, hipStream_t s_coll = nullptr,
+                          const std::function<int()> &between = nullptr) {
   std::vector<fcx_engine *> v;  // the engines with boundary slots, in list order
   for (int i = 0; i < n; ++i)
     if (es[i]->atm_shared && es[i]->atm_nb > 0 && es[i]->atm_stride > 0) v.push_back(es[i]);
@@ -3270,6 +3274,8 @@ static int atmos_exchange(fcx_comm *c, fcx_engine *const *es, int n, hipStream_t
       off += cnt;
     }
   }
+  if (between)
+    if (int r = between()) return r;
   for (size_t i = 0; i < v.size(); ++i) {
     fcx_engine *e = v[i];
     if (e->stream != s0) {  // the finish of that engine waits for the all-reduce
@@ -3340,26 +3346,45 @@ static int run_group_exchange(fcx_comm *c, fcx_engine *const *es, int n, int pha
     HIP_TRY(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
     HIP_TRY(hipEventCreateWithFlags(&c->ev_side, hipEventDisableTiming));
   }
-  HIP_TRY(hipEventRecord(c->ev_side, s_eng));  // the engines' earlier work (uploads) first
-  HIP_TRY(hipStreamWaitEvent(c->side, c->ev_side, 0));
+#ifndef FCX_OVERLAP_BOUNDARY_ON_SIDE
+#define FCX_OVERLAP_BOUNDARY_ON_SIDE 0
+#endif
+  // the boundary tiles go first on the engines' stream (alone on the GPU for the few
+  // microseconds they take), the all-reduce on the side stream after them, then the main
+  // launch: run beside the main launch from the start, the boundary launch measured 55 us
+  // per step slower (profiles/r05/overlap/)
+  hipStream_t s_b = FCX_OVERLAP_BOUNDARY_ON_SIDE ? c->side : s_eng;
+  if (FCX_OVERLAP_BOUNDARY_ON_SIDE) {
+    HIP_TRY(hipEventRecord(c->ev_side, s_eng));  // the engines' earlier work (uploads) first
+    HIP_TRY(hipStreamWaitEvent(c->side, c->ev_side, 0));
+  }
   if (nb) {
-    const int r = launch_cells_group(gm, nm, mem[0].lc, c->side, brange, nb);
+    const int r = launch_cells_group(gm, nm, mem[0].lc, s_b, brange, nb);
     if (r) return fail(FCX_E_HIP, "cells_atmos_group_kernel (boundary tiles) launch: %s", hipGetErrorString((hipError_t)r));
   }
-  if (nmr) {
-    const int r = launch_cells_group(gm, nm, mem[0].lc, s_eng, mrange, nmr);
-    if (r) return fail(FCX_E_HIP, "cells_atmos_group_kernel launch: %s", hipGetErrorString((hipError_t)r));
+  if (!FCX_OVERLAP_BOUNDARY_ON_SIDE) {
+    HIP_TRY(hipEventRecord(c->ev_side, s_eng));
+    HIP_TRY(hipStreamWaitEvent(c->side, c->ev_side, 0));
   }
   for (int k = 0; k < nm; ++k) {
-    if (int r = launch_empty_cells(mem[k].e, mem[k].pl, mem[k].lc)) return r;
     fcx_engine *e = mem[k].e;
     e->group_members = nm;
     e->atm_done_fused = true;
     e->atm_done = true;
   }
-  // the collective on the side stream (after the boundary tiles), the finishes on the engines'
-  // stream (after the main launch and the collective)
-  if (int r = atmos_exchange(c, es, n, c->side)) return r;
+  // the collective on the side stream (after the boundary tiles) is queued before the main
+  // launch, so that its kernel is dispatched before the main launch fills the CUs; the
+  // finishes go on the engines' stream after both
+  auto main_launch = [&]() -> int {
+    if (nmr) {
+      const int r = launch_cells_group(gm, nm, mem[0].lc, s_eng, mrange, nmr);
+      if (r) return fail(FCX_E_HIP, "cells_atmos_group_kernel launch: %s", hipGetErrorString((hipError_t)r));
+    }
+    for (int k = 0; k < nm; ++k)
+      if (int r = launch_empty_cells(mem[k].e, mem[k].pl, mem[k].lc)) return r;
+    return FCX_OK;
+  };
+  if (int r = atmos_exchange(c, es, n, c->side, main_launch)) return r;
   ++c->overlapped;
   for (int k = 0; k < nm; ++k) {
     fcx_engine *e = mem[k].e;
