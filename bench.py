@@ -93,10 +93,11 @@ def parse():
                    help="1: every step runs the variants' engines through fcx_run_group, their fused flux "
                         "passes as ONE launch (one event pair around it in the timed steps); 0: one launch "
                         "per engine")
-    p.add_argument("--overlap", type=int, default=1,
-                   help="N > 1 with the libfcx communicator and --group 1: the step is fcx_run_group_exchange "
-                        "(the boundary tiles and the all-reduce beside the main launch); 0: fcx_run_group, "
-                        "then fcx_atmos_allreduce")
+    p.add_argument("--overlap", type=int, default=0,
+                   help="N > 1 with the libfcx communicator and --group 1: 1 = the step is "
+                        "fcx_run_group_exchange (the boundary tiles and the all-reduce beside the main launch); "
+                        "0 (default) = fcx_run_group, then fcx_atmos_allreduce on the same stream -- the split's "
+                        "two cross-stream edges cost more than a small all-reduce hides (DESIGN.md section 6)")
     p.add_argument("--kernel-events", choices=("dominant", "all"), default="dominant",
                    help="HIP event pairs inside the timed steps: around the dominant engine's launch only "
                         "(picked in an event-timed warm-up block), or around every engine's")

@@ -3232,18 +3232,22 @@ static int atmos_exchange(fcx_comm *c, fcx_engine *const *es, int n, hipStream_t
     inplace = inplace && fresh[i] &&
               (i == 0 || v[i - 1]->atm_shared + (size_t)v[i - 1]->atm_nb * v[i - 1]->atm_stride == v[i]->atm_shared);
   }
-  size_t joins = 0;
-  for (auto *e : v) joins += e->stream != s0 ? 2 : 0;
+  // the engines' streams other than the collective's, each once: a cross-stream edge costs
+  // ~10 us of device time on MI355X (profiles/r05/ovprobe/), so one per stream, not per engine
+  std::vector<hipStream_t> others;
+  for (auto *e : v)
+    if (e->stream != s0 && std::find(others.begin(), others.end(), e->stream) == others.end())
+      others.push_back(e->stream);
   const bool pre_join = s_coll == nullptr;
-  while (c->events.size() < joins) {
+  while (c->events.size() < 2 * others.size()) {
     hipEvent_t ev;
     HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     c->events.push_back(ev);
   }
   size_t k = 0;
-  for (auto *e : v)
-    if (e->stream != s0 && pre_join) {  // the all-reduce waits for that engine's accumulation
-      HIP_TRY(hipEventRecord(c->events[k], e->stream));
+  if (pre_join)
+    for (hipStream_t so : others) {  // the all-reduce waits for those engines' accumulation
+      HIP_TRY(hipEventRecord(c->events[k], so));
       HIP_TRY(hipStreamWaitEvent(s0, c->events[k++], 0));
     }
   if (inplace) {
@@ -3276,16 +3280,35 @@ static int atmos_exchange(fcx_comm *c, fcx_engine *const *es, int n, hipStream_t
   }
   if (between)
     if (int r = between()) return r;
-  for (size_t i = 0; i < v.size(); ++i) {
-    fcx_engine *e = v[i];
-    if (e->stream != s0) {  // the finish of that engine waits for the all-reduce
-      HIP_TRY(hipEventRecord(c->events[k], s0));
-      HIP_TRY(hipStreamWaitEvent(e->stream, c->events[k++], 0));
-    }
-    if (!fresh[i]) continue;
-    if (int r = fcx_atmos_finish(e)) return r;
-    e->exchanged = true;
+  for (hipStream_t so : others) {  // the finishes on that stream wait for the all-reduce
+    HIP_TRY(hipEventRecord(c->events[k], s0));
+    HIP_TRY(hipStreamWaitEvent(so, c->events[k++], 0));
   }
+  // the finishes: the engines of one stream and precision in launches of up to kMaxGroup
+  // (one block each), in list order; an engine without cells re-zeroes its slots itself
+  std::vector<char> done(v.size(), 0);
+  for (size_t i = 0; i < v.size(); ++i) {
+    if (!fresh[i] || done[i]) continue;
+    fcx_engine *e = v[i];
+    if (e->n_atmos <= 0) {
+      if (int r = fcx_atmos_finish(e)) return r;
+      done[i] = 1;
+      continue;
+    }
+    AtmosArgs as[kMaxGroup];
+    int32_t nbs[kMaxGroup];
+    int ng = 0;
+    for (size_t j = i; j < v.size() && ng < kMaxGroup; ++j)
+      if (fresh[j] && !done[j] && v[j]->n_atmos > 0 && v[j]->stream == e->stream && v[j]->f32 == e->f32) {
+        as[ng] = atmos_args(v[j], FCX_PHASE_ALL);
+        nbs[ng++] = v[j]->atm_nb;
+        done[j] = 1;
+      }
+    const int r = launch_atmos_finish_group(as, nbs, ng, e->stream);
+    if (r) return fail(FCX_E_HIP, "atmos_finish_group launch: %s", hipGetErrorString((hipError_t)r));
+  }
+  for (size_t i = 0; i < v.size(); ++i)
+    if (fresh[i]) v[i]->exchanged = true;
   if (stale >= 0)
     return fail(FCX_E_STATE,
                 "boundary exchange: engine %d of the list has no accumulation since its last exchange (fcx_run or "

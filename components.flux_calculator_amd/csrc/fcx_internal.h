@@ -180,6 +180,9 @@ struct AtmosArgs {
                                   // the same for every phase and for the fused kernel
 };
 int launch_atmos(const AtmosArgs &a, void *stream);
+// atmos_finish of several engines (same precision, one stream) in one launch
+struct FinishGroup;
+int launch_atmos_finish_group(const AtmosArgs *as, const int32_t *n_boundaries, int n, void *stream);
 // remap records: rec[j * P + f] = x[f][tiled(j)] for f < nf, 0 for nf <= f < P, cells
 // j < n (P a multiple of the 16-B vector length); aligned16: every x is 16-B aligned;
 // nontemporal: streaming hint on the field loads (off for host-mapped fields)
@@ -226,6 +229,11 @@ struct AtmosFused {
 // Several engines' fused T = 1 launches in ONE launch (fcx_run_group): member k's wave tiles
 // are tiles [tile0, tile0 + af.n_tiles) of the grid.  Passed by value (kernel arguments).
 constexpr int kMaxGroup = 4;
+struct FinishGroup {
+  int32_t n;
+  int32_t nb[kMaxGroup];
+  AtmosArgs a[kMaxGroup];
+};
 // cells per lane of the fp32 engine's fused kernels (16-B lanes of 4 floats; A/B builds: 2,
 // 8-B lanes of 2 floats in 128-cell tiles like the fp64 kernels, half the registers per lane)
 #ifndef FCX_F32_CPL

@@ -1395,6 +1395,22 @@ __global__ void atmos_finish_kernel(const AtmosArgs a, int32_t n_boundaries) {
   for (int64_t i = t; i < (int64_t)n_boundaries * a.stride; i += blockDim.x) a.shared[i] = 0.0;
 }
 
+// the finishes of several engines after one exchange, one block per engine (one launch: each
+// launch is ~5 us on the step's critical path after the all-reduce)
+template <class R>
+__global__ void atmos_finish_group_kernel(const FinishGroup g) {
+  const AtmosArgs &a = g.a[blockIdx.x];
+  const int32_t n_boundaries = g.nb[blockIdx.x];
+  const int t = threadIdx.x;
+  if (t < a.nf) {
+    R *out = reinterpret_cast<R *>(a.out[t]);
+    if (a.left >= 0) out[0] = (R)a.shared[(int64_t)a.left * a.stride + a.scol[t]];
+    if (a.right >= 0) out[tiled(a.n_atmos - 1, a.out_tpad)] = (R)a.shared[(int64_t)a.right * a.stride + a.scol[t]];
+  }
+  __syncthreads();
+  for (int64_t i = t; i < (int64_t)n_boundaries * a.stride; i += blockDim.x) a.shared[i] = 0.0;
+}
+
 __global__ void zero_kernel(double *x, int64_t n) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += stride) x[j] = 0.0;
@@ -1715,6 +1731,23 @@ int launch_atmos_finish(const AtmosArgs &a, int32_t n_boundaries, void *stream) 
   else
     hipLaunchKernelGGL(atmos_finish_kernel<double>, dim3(1), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
                        a, n_boundaries);
+  return (int)hipGetLastError();
+}
+
+int launch_atmos_finish_group(const AtmosArgs *as, const int32_t *nbs, int n, void *stream) {
+  if (n < 1 || n > kMaxGroup) return (int)hipErrorInvalidValue;
+  FinishGroup g{};
+  g.n = n;
+  for (int k = 0; k < n; ++k) {
+    if (!as[k].shared || as[k].f32 != as[0].f32) return (int)hipErrorInvalidValue;
+    g.a[k] = as[k];
+    g.nb[k] = nbs[k];
+  }
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (as[0].f32)
+    hipLaunchKernelGGL(atmos_finish_group_kernel<float>, dim3(n), dim3(256), 0, s, g);
+  else
+    hipLaunchKernelGGL(atmos_finish_group_kernel<double>, dim3(n), dim3(256), 0, s, g);
   return (int)hipGetLastError();
 }
 
