@@ -289,7 +289,9 @@ int fcx_comm_verify(fcx_comm *c, int every_exchange);
  * instead of the flux pass plus the all-reduce latency.  Results and the collective sequence
  * are those of fcx_run_group + fcx_atmos_allreduce; engines that cannot take the split (not
  * all merged into one T = 1 launch with halo tiles, remaps, an attached communicator) run
- * exactly that way. */
+ * exactly that way.  Measured on MI355X the split's two cross-stream edges (~10 us each) and
+ * its boundary launch cost more than a small all-reduce hides: it pays
+ * only where the collective is slow (many ranks, a slow fabric). */
 int fcx_run_group_exchange(fcx_comm *c, fcx_engine *const *engines, int n_engines, int phase,
                            int32_t current_step_time);
 /* how many exchanges of the communicator ran beside a main launch (the split above) */
