@@ -13,8 +13,9 @@ weak scaling); the one cross-rank exchange is the all-reduce of the atmosphere c
 by neighbouring ranks (libfcx's RCCL communicator), once per step.
 
 Also reported:
-  roofline      algorithmic bytes of the dominant kernel / its mean HIP-event duration in
-                the timed steps (one event pair per step, around that kernel only)
+  roofline      algorithmic bytes of the step's one launch (fcx_run_group) / its mean device
+                time per timed step (one HIP event pair around the timed steps; --group 0: an
+                event pair per step around the dominant engine's launch)
   cpu_baseline  the reference path on this box's host cores (rank 0, N=1 only; cpu_legs.py):
                 the reference flux_lib compiled from source (oracle/_ref, kind "reference";
                 the C restatement oracle/fco.c, kind "port", where it was not built) on one
@@ -91,7 +92,7 @@ def parse():
                         "(fp32 fluxes, fp64 weights, products and sums, fp32 outputs)")
     p.add_argument("--group", type=int, default=1,
                    help="1: every step runs the variants' engines through fcx_run_group, their fused flux "
-                        "passes as ONE launch (one event pair around it in the timed steps); 0: one launch "
+                        "passes as ONE launch (one event pair around the timed steps); 0: one launch "
                         "per engine")
     p.add_argument("--overlap", type=int, default=0,
                    help="N > 1 with the libfcx communicator and --group 1: 1 = the step is "
@@ -407,7 +408,11 @@ def measure(wl, args, world, dist, comm, steps, warmup, t_base=0, cold=False):
     # the timed steps' events exist before the warm-up starts: nothing host-side sits between
     # the warm-up and the timed region (an idle GPU drops its clocks)
     ev = pairs(steps)
-    ev_group = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    # the grouped step's one launch: ONE event pair around the whole timed region, not a pair per
+    # step -- an event recorded between two launches on a stream holds the next launch back
+    # ~10.5 us (the kernel trace of round 5: 10.5 us between timed launches with per-step
+    # pairs, none between the warm-up's, profiles/r05/ev/), 1.4 % of the step
+    ev_region = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
     step(t_base)  # builds the engines' plans
     torch.cuda.synchronize()
     cold_ms = None
@@ -458,8 +463,12 @@ def measure(wl, args, world, dist, comm, steps, warmup, t_base=0, cold=False):
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    if group:
+        ev_region[0].record(stream)
     for k in range(steps):
-        step(t_base + k * 3600, ev_group[k] if group else ev[k])
+        step(t_base + k * 3600, None if group else ev[k])
+    if group:
+        ev_region[1].record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -469,7 +478,9 @@ def measure(wl, args, world, dist, comm, steps, warmup, t_base=0, cold=False):
     kern_mean = probe_ms.mean(axis=0)
     timed = {} if group else {i: np.array([row[i][0].elapsed_time(row[i][1]) for row in ev])
                               for i in range(nv) if ev and ev[0][i] is not None}
-    group_ms = float(np.mean([a.elapsed_time(b) for a, b in ev_group])) if group and steps else None
+    # device time per grouped step: the launch plus the kernel boundary to the next (~0-1.5 us;
+    # the rocprof trace's mean launch duration is the cross-check)
+    group_ms = ev_region[0].elapsed_time(ev_region[1]) / steps if group and steps else None
     for i, x in timed.items():
         kern_mean[i] = x.mean()
     t_max = elapsed
@@ -652,8 +663,9 @@ def main():
             "traffic_source": traffic_source,
             "alg_bytes_per_launch": dom_bytes,
             "mean_kernel_ms": round(dom_ms, 4),
-            "events": ("one HIP event pair per timed step around the step's one launch (fcx_run_group: the "
-                       "variants' fused flux passes in one grid), on its stream" if grouped else
+            "events": ("one HIP event pair around the timed steps on the launches' stream, mean per step: the "
+                       "step's one launch (fcx_run_group: the variants' fused flux passes in one grid) and its "
+                       "kernel boundary; no events between the timed launches" if grouped else
                        "one HIP event pair per timed step, around the dominant engine's launch on its stream "
                        "(picked in an event-timed warm-up block of every engine)" if args.kernel_events == "dominant"
                        else "HIP event pairs around every engine's launch in every timed step"),
