@@ -199,7 +199,14 @@ constexpr int kRecHead = 4;     // head products kept per crossing record (longe
 constexpr int kXRec = 32;       // doubles per crossing record (256 B, two lines)
 constexpr int kTile = 128;  // cells per wave iteration (64 lanes x 2)
 struct AtmosFused {
-  const int32_t *idx;  // local atmosphere cell of every exchange cell (non-decreasing)
+  // the exchange -> atmosphere map of a contiguous (sorted) map, compacted (round 5): bit x of
+  // seg_bits[x / 32] is set where exchange cell x starts a segment (its atmosphere cell
+  // differs from cell x-1's); seg_pre[w] counts the starts in cells < 32 w; seg_atm[s] is the
+  // atmosphere cell of segment s.  1/8 + 1/8 + 4/(cells per segment) bytes per cell instead
+  // of a 4-B index per cell.
+  const uint32_t *seg_bits;
+  const int32_t *seg_pre;
+  const int32_t *seg_atm;
   const double *w;
   double *out[kFusedFields];
   const double *x[kFusedFields];  // the stored outputs (read by the fix-up only)

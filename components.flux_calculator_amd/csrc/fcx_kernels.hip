@@ -870,21 +870,29 @@ __device__ __forceinline__ void atmos_tile(const Params *__restrict__ P, const d
     const int64_t t0 = tile * kO;
     const int64_t j0 = t0 + C * lane;
     LdsEmitT<C> emit{wp, {}, lds_slot(C * lane)};
-    int32_t a[C];  // -1: past the grid end
-#pragma unroll
-    for (int i = 0; i < C; ++i) a[i] = -1;
-    if (j0 + C <= n) {
-      if constexpr (C == 2) {
-        const i2v ii = *gptr(reinterpret_cast<const i2v *>(af.idx + j0));
-        a[0] = ii.x;
-        a[1] = ii.y;
-      } else {
-        const i4v ii = *gptr(reinterpret_cast<const i4v *>(af.idx + j0));
-        a[0] = ii.x;
-        a[1] = ii.y;
-        a[2] = ii.z;
-        a[3] = ii.w;
+    // the lane's cells in the compacted map: which start a segment (cells past the grid end
+    // count as starts: they end the last real segment) and, for those, the segment's
+    // atmosphere cell; the lane's C cells share one bit word (j0 is a multiple of C)
+    int32_t a[C];  // atmosphere cell of a segment-start cell (-1 elsewhere)
+    bool st[C];
+    int32_t before = 0;  // segments starting before cell j0
+    {
+      uint32_t word = 0;
+      const int sh = (int)(j0 & 31);
+      if (j0 < n) {
+        word = gptr(af.seg_bits)[j0 >> 5];
+        before = gptr(af.seg_pre)[j0 >> 5] + __builtin_popcount(word & ((1u << sh) - 1u));
       }
+      int32_t ord = before;
+#pragma unroll
+      for (int i = 0; i < C; ++i) {
+        const bool valid = j0 + i < n;
+        st[i] = !valid || ((word >> (sh + i)) & 1u);
+        a[i] = -1;
+        if (valid && st[i]) a[i] = gptr(af.seg_atm)[ord++];
+      }
+    }
+    if (j0 + C <= n) {
 #pragma unroll
       for (int h = 0; h < C / 2; ++h) {
         const d2 ww = __builtin_nontemporal_load(gptr(reinterpret_cast<const d2 *>(af.w + j0) + h));
@@ -894,14 +902,11 @@ __device__ __forceinline__ void atmos_tile(const Params *__restrict__ P, const d
     } else {
 #pragma unroll
       for (int i = 0; i < C; ++i)
-        if (j0 + i < n) {
-          a[i] = gptr(af.idx)[j0 + i];
-          emit.w[i] = gptr(af.w)[j0 + i];
-        }
+        if (j0 + i < n) emit.w[i] = gptr(af.w)[j0 + i];
     }
-    const int32_t prev_tile = t0 > 0 ? gptr(af.idx)[t0 - 1] : -2;  // wave-uniform loads
     const int64_t tend = t0 + kT;
-    const int32_t next_a = (tend < n) ? gptr(af.idx)[tend] : -3;
+    // the segment running to the tile end continues past it (wave-uniform load)
+    const bool next_cont = tend < n && !((gptr(af.seg_bits)[tend >> 5] >> (tend & 31)) & 1u);
     if (j0 < n)
       process<C, true, VAR, NT, R, TM, RAVG, LdsEmitT<C>, REC, HALO>(
           P, corr_m, j0, emit, AccLds<C, R>{reinterpret_cast<R *>(wp + emit.s), kR}, t0 + kO);
@@ -924,17 +929,10 @@ __device__ __forceinline__ void atmos_tile(const Params *__restrict__ P, const d
       }
     };
     // segment starts: cell C*l+i begins a segment when its atmosphere cell differs from the
-    // previous cell's (the first cell past the grid end also "starts", which ends the last
-    // real segment)
-    int32_t prev = __shfl_up(a[C - 1], 1);
-    if (lane == 0) prev = prev_tile;
-    bool st[C];
+    // previous cell's (cells past the grid end also "start", which ends the last real segment)
     uint64_t m[C];
 #pragma unroll
-    for (int i = 0; i < C; ++i) {
-      st[i] = a[i] != (i ? a[i - 1] : prev);
-      m[i] = __ballot(st[i]);
-    }
+    for (int i = 0; i < C; ++i) m[i] = __ballot(st[i]);
     wave_sync();  // the wave's LDS products are visible to all its lanes
     // Rounds of one segment start per lane (round 2): every lane with a start sums its
     // segment and stores the six values in the same round, so a tile's atmosphere stores are
@@ -944,7 +942,7 @@ __device__ __forceinline__ void atmos_tile(const Params *__restrict__ P, const d
     uint32_t rem = 0;  // bit i: cell C*lane+i starts a segment not summed yet (an own cell)
 #pragma unroll
     for (int i = 0; i < C; ++i)
-      if (st[i] && a[i] >= 0 && (!HALO || lane < own_lanes)) rem |= 1u << i;
+      if (st[i] && j0 + i < n && (!HALO || lane < own_lanes)) rem |= 1u << i;
     // the end of the segment starting at cell C*lane+i: the next start of any kind (own,
     // halo, past the grid end), or the tile end
     auto seg_end = [&](int i) {
@@ -992,7 +990,7 @@ __device__ __forceinline__ void atmos_tile(const Params *__restrict__ P, const d
 #pragma unroll
           for (int k = 0; k < kFusedFields; ++k) acc[k] = 0.0;
           for (int e = c; e < end; ++e) add_cell(acc, e);
-          segment_done<R>(af, tile, ai, acc, !HALO && end == kT && next_a == ai);
+          segment_done<R>(af, tile, ai, acc, !HALO && end == kT && next_cont);
         }
       }
       rem = 0;
@@ -1013,7 +1011,7 @@ __device__ __forceinline__ void atmos_tile(const Params *__restrict__ P, const d
         for (int k = 0; k < kFusedFields; ++k) acc[k] = 0.0;
         for (int e = c; e < end; ++e) add_cell(acc, e);
         // (HALO: the segment ends inside the wave's own + halo cells by the engine's rule)
-        segment_done<R>(af, tile, ai, acc, !HALO && end == kT && next_a == ai);
+        segment_done<R>(af, tile, ai, acc, !HALO && end == kT && next_cont);
       }
     }
     // the number of head cells (continuing the previous tile's segment) for
@@ -1024,7 +1022,10 @@ __device__ __forceinline__ void atmos_tile(const Params *__restrict__ P, const d
       for (int q = 0; q < C; ++q) head = min(head, C * first_bit(m[q]) + q);
       if (FCX_DBG_NO_HEAD >= 2) head = 0;
       double *xr0 = af.xrec + tile * kXRec;
-      if (lane == 0 && FCX_DBG_NO_HEAD < 2) *gptr(reinterpret_cast<i2v *>(xr0 + 30)) = i2v{head, a[0]};
+      if (lane == 0 && FCX_DBG_NO_HEAD < 2) {  // the tile's first cell: its atmosphere cell
+        const int32_t a0 = st[0] ? a[0] : gptr(af.seg_atm)[before - 1];
+        *gptr(reinterpret_cast<i2v *>(xr0 + 30)) = i2v{head, a0};
+      }
       if (FCX_DBG_NO_HEAD) head = 0;
       // the products of the first kRecHead head cells, one lane per cell, 16-B stores
       if (lane < min(head, kRecHead)) {
