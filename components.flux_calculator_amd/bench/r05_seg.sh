@@ -5,7 +5,6 @@
 set -euo pipefail
 O=gpurun_out/r05/seg; mkdir -p $O
 B=components.flux_calculator_amd/bench
-timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > $O/tests.log 2>&1
 export FCX_LIBRARY=ab/ref5/libfcx.so
 timeout -k 10 300 python3 -u $B/inproc_ab.py --group --rounds 8 --steps 20 --warmup 40 --lib seg=ab/seg/libfcx.so > $O/t1.json
 timeout -k 10 300 python3 -u $B/inproc_ab.py --group --precision f32 --rounds 8 --steps 20 --warmup 40 --lib seg=ab/seg/libfcx.so > $O/f32.json

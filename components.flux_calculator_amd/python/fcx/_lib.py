@@ -127,10 +127,8 @@ def load():
         if not os.path.exists(LIB_PATH):
             raise FcxError(-1, f"{LIB_PATH} is not built (run __graft_entry__.build())")
         lib = ctypes.CDLL(LIB_PATH)
-        for name, res, args in SIGNATURES:
-            fn = getattr(lib, name)
-            fn.restype = res
-            fn.argtypes = args
+        # an FCX_LIBRARY override (A/B of an older build) may predate some entry points
+        _bind(lib, strict=not os.environ.get("FCX_LIBRARY"))
         _lib = lib
     return _lib
 
@@ -140,11 +138,20 @@ def load_path(path):
     over the same arrays).  The process's own library is still load()'s."""
     load()
     lib = ctypes.CDLL(os.path.abspath(path))
+    _bind(lib, strict=False)
+    return lib
+
+
+def _bind(lib, strict=True):
     for name, res, args in SIGNATURES:
-        fn = getattr(lib, name)
+        try:
+            fn = getattr(lib, name)
+        except AttributeError:
+            if strict:
+                raise
+            continue
         fn.restype = res
         fn.argtypes = args
-    return lib
 
 
 def check(status):
