@@ -873,24 +873,14 @@ __device__ __forceinline__ void atmos_tile(const Params *__restrict__ P, const d
     // the lane's cells in the compacted map: which start a segment (cells past the grid end
     // count as starts: they end the last real segment) and, for those, the segment's
     // atmosphere cell; the lane's C cells share one bit word (j0 is a multiple of C)
-    int32_t a[C];  // atmosphere cell of a segment-start cell (-1 elsewhere)
-    bool st[C];
+    // (the bit word and prefix count are loaded with the inputs; the dependent loads of the
+    // segments' atmosphere cells follow the flux pass, so they add no round trip before it)
+    const int sh = (int)(j0 & 31);
+    uint32_t word = 0;
     int32_t before = 0;  // segments starting before cell j0
-    {
-      uint32_t word = 0;
-      const int sh = (int)(j0 & 31);
-      if (j0 < n) {
-        word = gptr(af.seg_bits)[j0 >> 5];
-        before = gptr(af.seg_pre)[j0 >> 5] + __builtin_popcount(word & ((1u << sh) - 1u));
-      }
-      int32_t ord = before;
-#pragma unroll
-      for (int i = 0; i < C; ++i) {
-        const bool valid = j0 + i < n;
-        st[i] = !valid || ((word >> (sh + i)) & 1u);
-        a[i] = -1;
-        if (valid && st[i]) a[i] = gptr(af.seg_atm)[ord++];
-      }
+    if (j0 < n) {
+      word = gptr(af.seg_bits)[j0 >> 5];
+      before = gptr(af.seg_pre)[j0 >> 5];
     }
     if (j0 + C <= n) {
 #pragma unroll
@@ -930,9 +920,21 @@ __device__ __forceinline__ void atmos_tile(const Params *__restrict__ P, const d
     };
     // segment starts: cell C*l+i begins a segment when its atmosphere cell differs from the
     // previous cell's (cells past the grid end also "start", which ends the last real segment)
+    int32_t a[C];  // atmosphere cell of a segment-start cell (-1 elsewhere)
+    bool st[C];
     uint64_t m[C];
+    before += __builtin_popcount(word & ((1u << sh) - 1u));
+    {
+      int32_t ord = before;
 #pragma unroll
-    for (int i = 0; i < C; ++i) m[i] = __ballot(st[i]);
+      for (int i = 0; i < C; ++i) {
+        const bool valid = j0 + i < n;
+        st[i] = !valid || ((word >> (sh + i)) & 1u);
+        a[i] = -1;
+        if (valid && st[i]) a[i] = gptr(af.seg_atm)[ord++];
+        m[i] = __ballot(st[i]);
+      }
+    }
     wave_sync();  // the wave's LDS products are visible to all its lanes
     // Rounds of one segment start per lane (round 2): every lane with a start sums its
     // segment and stores the six values in the same round, so a tile's atmosphere stores are
