@@ -198,9 +198,10 @@ struct fcx_engine {
   std::vector<int32_t> atm_row, atm_col;
   std::vector<double> atm_w;
   bool atm_contiguous = true;
-  int32_t *d_atm_row = nullptr, *d_atm_col = nullptr;
-  // the fused path's compacted map (AtmosFused::seg_*): [words] start bits, [words + 1]
-  // prefix counts, [segments] atmosphere cells, one allocation
+  int32_t *d_atm_row = nullptr, *d_atm_col = nullptr, *d_atm_idx = nullptr;
+  // the fused path's map: fp64 engines a 4-B index per cell (d_atm_idx), fp32 engines the
+  // compacted map (AtmosFused::seg_*: [words] start bits, [words + 1] prefix counts,
+  // [segments] atmosphere cells, one allocation)
   void *d_atm_seg = nullptr;
   int64_t atm_seg_words = 0, atm_segments = 0;
   std::vector<int32_t> atm_idx;
@@ -402,6 +403,7 @@ extern "C" int fcx_destroy(fcx_engine *e) {
   (void)hipFree(e->corr_dev);
   (void)hipFree(e->d_atm_row);
   (void)hipFree(e->d_atm_seg);
+  (void)hipFree(e->d_atm_idx);
   (void)hipFree(e->d_atm_empty);
   (void)hipFree(e->d_atm_xrec);
   (void)hipFree(e->d_atm_col);
@@ -696,7 +698,7 @@ static void plan_fused_atmos(fcx_engine *e, Plan &pl, uint32_t stages, int phase
   // go to atmos_kernel: one lane summing a long segment would hold up its whole wave; the
   // fp32 engine uses atmos_kernel too)
   // (fp32 engine: T = 1 only, the register averages of several types are fp64-only)
-  if (!pl.variant || !e->d_atm_seg || e->atm_maxseg > kTile / 2 || e->any_regrid || phase <= 0 ||
+  if (!pl.variant || !(e->f32 ? e->d_atm_seg : (void *)e->d_atm_idx) || e->atm_maxseg > kTile / 2 || e->any_regrid || phase <= 0 ||
       phase >= 1000 || !e->specialize || (e->f32 && e->T >= 2))
     return;
   const TypeParams &tp = pl.host.type[0];
@@ -736,9 +738,12 @@ static void plan_fused_atmos(fcx_engine *e, Plan &pl, uint32_t stages, int phase
     ++nf;
   }
   if (nf == 0) return;
-  af.seg_bits = reinterpret_cast<const uint32_t *>(e->d_atm_seg);
-  af.seg_pre = reinterpret_cast<const int32_t *>(af.seg_bits + e->atm_seg_words);
-  af.seg_atm = af.seg_pre + e->atm_seg_words + 1;
+  if (e->d_atm_seg) {
+    af.seg_bits = reinterpret_cast<const uint32_t *>(e->d_atm_seg);
+    af.seg_pre = reinterpret_cast<const int32_t *>(af.seg_bits + e->atm_seg_words);
+    af.seg_atm = af.seg_pre + e->atm_seg_words + 1;
+  }
+  af.idx = e->d_atm_idx;
   af.w = e->d_atm_w;
   af.xrec = e->d_atm_xrec;
   af.xrec_on = e->atm_crossings > 0;
@@ -1766,7 +1771,12 @@ extern "C" int fcx_commit(fcx_engine *e) {
     HIP_TRY(hipMalloc(&e->d_atm_w, std::max<size_t>(e->atm_w.size(), 1) * sizeof(double)));
     if (!e->atm_w.empty())
       HIP_TRY(hipMemcpy(e->d_atm_w, e->atm_w.data(), e->atm_w.size() * sizeof(double), hipMemcpyHostToDevice));
-    if (e->atm_contiguous && !e->atm_idx.empty()) {  // the compacted map of the fused path
+    if (e->atm_contiguous && !e->atm_idx.empty() && !e->f32) {  // fp64: the per-cell index
+      HIP_TRY(hipMalloc(&e->d_atm_idx, e->atm_idx.size() * sizeof(int32_t)));
+      HIP_TRY(hipMemcpy(e->d_atm_idx, e->atm_idx.data(), e->atm_idx.size() * sizeof(int32_t),
+                        hipMemcpyHostToDevice));
+    }
+    if (e->atm_contiguous && !e->atm_idx.empty() && e->f32) {  // fp32: the compacted map
       const int64_t nx = (int64_t)e->atm_idx.size(), nw = (nx + 31) / 32;
       std::vector<uint32_t> seg((size_t)(2 * nw + 1), 0u);  // bits, then prefix counts (int32)
       std::vector<int32_t> atm;
@@ -1787,6 +1797,8 @@ extern "C" int fcx_commit(fcx_engine *e) {
       HIP_TRY(hipMemcpy(e->d_atm_seg, seg.data(), head, hipMemcpyHostToDevice));
       if (!atm.empty())
         HIP_TRY(hipMemcpy((char *)e->d_atm_seg + head, atm.data(), atm.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    }
+    if (e->atm_contiguous && !e->atm_idx.empty()) {  // the fused path's crossing records
       const int64_t tiles = (e->n[0] + kTile - 1) / kTile;
       HIP_TRY(hipMalloc(&e->d_atm_xrec, (size_t)std::max<int64_t>(tiles, 1) * kXRec * sizeof(double)));
       // tile boundaries a segment runs across: none (a map whose runs never cross a wave
@@ -2712,7 +2724,8 @@ extern "C" int fcx_algorithmic_bytes(fcx_engine *e, int phase, int64_t *bytes) {
       (!e->f32 || e->launch.max_blocks <= 0)) {
     nf = 0;  // fused: the compacted map and a weight per cell, the atmosphere outputs (fluxes
              // not re-read)
-    extra = e->n[0] * 8 + (2 * e->atm_seg_words + 1 + e->atm_segments) * 4 + (int64_t)pl->atm_nf * e->n_atmos * es;
+    extra = e->n[0] * 8 + (e->f32 ? (2 * e->atm_seg_words + 1 + e->atm_segments) * 4 : e->n[0] * 4) +
+            (int64_t)pl->atm_nf * e->n_atmos * es;
   } else if (nf && e->n_atmos >= 0 && e->atmos_in_run) {
     extra += e->n[0] * 8 + (e->atm_contiguous ? 0 : e->n[0] * 4) + (e->n_atmos + 1) * 4;
     extra += (int64_t)nf * (e->n[0] + e->n_atmos) * es;

@@ -203,10 +203,11 @@ struct AtmosFused {
   // seg_bits[x / 32] is set where exchange cell x starts a segment (its atmosphere cell
   // differs from cell x-1's); seg_pre[w] counts the starts in cells < 32 w; seg_atm[s] is the
   // atmosphere cell of segment s.  1/8 + 1/8 + 4/(cells per segment) bytes per cell instead
-  // of a 4-B index per cell.
+  // of a 4-B index per cell.  The fp32 engines' kernels read this; the fp64 ones read idx.
   const uint32_t *seg_bits;
   const int32_t *seg_pre;
   const int32_t *seg_atm;
+  const int32_t *idx;  // fp64 engines: the local atmosphere cell of every exchange cell
   const double *w;
   double *out[kFusedFields];
   const double *x[kFusedFields];  // the stored outputs (read by the fix-up only)

@@ -873,14 +873,31 @@ __device__ __forceinline__ void atmos_tile(const Params *__restrict__ P, const d
     // the lane's cells in the compacted map: which start a segment (cells past the grid end
     // count as starts: they end the last real segment) and, for those, the segment's
     // atmosphere cell; the lane's C cells share one bit word (j0 is a multiple of C)
-    // (the bit word and prefix count are loaded with the inputs; the dependent loads of the
-    // segments' atmosphere cells follow the flux pass, so they add no round trip before it)
+    // fp32 (kCompact): the compacted map -- the bit word and prefix count are loaded with
+    // the inputs, the dependent loads of the segments' atmosphere cells follow the flux pass,
+    // so they add no round trip before it.  fp64: one 4-B index per cell, loaded with the
+    // inputs (the compacted map measured -2.3 % per fp32 step, -0.4 % at T = 1 fp64 and +1.7 %
+    // at T = 2, in one process over the same arrays: profiles/r05/seg/)
+    constexpr bool kCompact = sizeof(R) == 4;
     const int sh = (int)(j0 & 31);
     uint32_t word = 0;
-    int32_t before = 0;  // segments starting before cell j0
-    if (j0 < n) {
-      word = gptr(af.seg_bits)[j0 >> 5];
-      before = gptr(af.seg_pre)[j0 >> 5];
+    int32_t before = 0;  // kCompact: segments starting before cell j0
+    int32_t a[C];        // atmosphere cell (kCompact: of a segment-start cell only; -1 elsewhere)
+#pragma unroll
+    for (int i = 0; i < C; ++i) a[i] = -1;
+    if constexpr (kCompact) {
+      if (j0 < n) {
+        word = gptr(af.seg_bits)[j0 >> 5];
+        before = gptr(af.seg_pre)[j0 >> 5];
+      }
+    } else if (j0 + C <= n) {
+      const i2v ii = *gptr(reinterpret_cast<const i2v *>(af.idx + j0));
+      a[0] = ii.x;
+      a[1] = ii.y;
+    } else {
+#pragma unroll
+      for (int i = 0; i < C; ++i)
+        if (j0 + i < n) a[i] = gptr(af.idx)[j0 + i];
     }
     if (j0 + C <= n) {
 #pragma unroll
@@ -895,8 +912,15 @@ __device__ __forceinline__ void atmos_tile(const Params *__restrict__ P, const d
         if (j0 + i < n) emit.w[i] = gptr(af.w)[j0 + i];
     }
     const int64_t tend = t0 + kT;
-    // the segment running to the tile end continues past it (wave-uniform load)
-    const bool next_cont = tend < n && !((gptr(af.seg_bits)[tend >> 5] >> (tend & 31)) & 1u);
+    // the segment running to the tile end continues past it (wave-uniform loads)
+    bool next_cont;
+    int32_t prev_tile = -2;
+    if constexpr (kCompact) {
+      next_cont = tend < n && !((gptr(af.seg_bits)[tend >> 5] >> (tend & 31)) & 1u);
+    } else {
+      prev_tile = t0 > 0 ? gptr(af.idx)[t0 - 1] : -2;
+      next_cont = tend < n && gptr(af.idx)[tend] == gptr(af.idx)[tend - 1];
+    }
     if (j0 < n)
       process<C, true, VAR, NT, R, TM, RAVG, LdsEmitT<C>, REC, HALO>(
           P, corr_m, j0, emit, AccLds<C, R>{reinterpret_cast<R *>(wp + emit.s), kR}, t0 + kO);
@@ -920,18 +944,24 @@ __device__ __forceinline__ void atmos_tile(const Params *__restrict__ P, const d
     };
     // segment starts: cell C*l+i begins a segment when its atmosphere cell differs from the
     // previous cell's (cells past the grid end also "start", which ends the last real segment)
-    int32_t a[C];  // atmosphere cell of a segment-start cell (-1 elsewhere)
     bool st[C];
     uint64_t m[C];
-    before += __builtin_popcount(word & ((1u << sh) - 1u));
-    {
+    if constexpr (kCompact) {
+      before += __builtin_popcount(word & ((1u << sh) - 1u));
       int32_t ord = before;
 #pragma unroll
       for (int i = 0; i < C; ++i) {
         const bool valid = j0 + i < n;
         st[i] = !valid || ((word >> (sh + i)) & 1u);
-        a[i] = -1;
         if (valid && st[i]) a[i] = gptr(af.seg_atm)[ord++];
+        m[i] = __ballot(st[i]);
+      }
+    } else {
+      int32_t prev = __shfl_up(a[C - 1], 1);
+      if (lane == 0) prev = prev_tile;
+#pragma unroll
+      for (int i = 0; i < C; ++i) {
+        st[i] = a[i] != (i ? a[i - 1] : prev);
         m[i] = __ballot(st[i]);
       }
     }
@@ -1025,7 +1055,7 @@ __device__ __forceinline__ void atmos_tile(const Params *__restrict__ P, const d
       if (FCX_DBG_NO_HEAD >= 2) head = 0;
       double *xr0 = af.xrec + tile * kXRec;
       if (lane == 0 && FCX_DBG_NO_HEAD < 2) {  // the tile's first cell: its atmosphere cell
-        const int32_t a0 = st[0] ? a[0] : gptr(af.seg_atm)[before - 1];
+        const int32_t a0 = (!kCompact || st[0]) ? a[0] : gptr(af.seg_atm)[before - 1];
         *gptr(reinterpret_cast<i2v *>(xr0 + 30)) = i2v{head, a0};
       }
       if (FCX_DBG_NO_HEAD) head = 0;
