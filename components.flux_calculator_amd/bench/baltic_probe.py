@@ -21,7 +21,9 @@ sys.path.insert(0, os.path.join(ROOT, "components.flux_calculator_amd", "python"
 VARIANTS = ("CCLM", "MOM5", "RCO")
 MODES = [
     "default:",
-    "zc_outputs:zero_copy=3",
+    "zc_chunks4:zero_copy=1,pipeline_min_chunk=8192,pipeline_chunks=4",
+    "zc_chunks8:zero_copy=1,pipeline_min_chunk=4096,pipeline_chunks=8",
+    "dma_chunks4:zero_copy=0,pipeline_min_chunk=8192,pipeline_chunks=4",
     "dma_seq:zero_copy=0",
 ]
 

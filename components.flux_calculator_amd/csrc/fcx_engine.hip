@@ -1592,16 +1592,8 @@ static Xfer xfer_of(const StageRef &st, void *host, int64_t n) {
 // place -- the library's own memory, as fcx_host_malloc blocks are -- so a small step makes
 // no copy call at all: the host copies the inputs into the arena, the launch reads and
 // writes it over the host link, the host copies the outputs back after the synchronisation.
-// outputs_only (FCX_OPT_ZERO_COPY 3): only the arrays the path writes -- the flux outputs,
-// the atmosphere and remap outputs -- live in the mapped arena; the inputs keep device
-// mirrors fed by the staging DMAs
-static int map_staged(fcx_engine *e, int *count, bool outputs_only = false) {
+static int map_staged(fcx_engine *e, int *count) {
   *count = 0;
-  std::vector<char> out_buf(e->bufs.size(), 0);
-  for (int s = 0; s <= kMaxTypes; ++s)
-    for (int g = 1; g <= 3; ++g)
-      for (int v : {FCX_QSUR, FCX_MEVA, FCX_HLAT, FCX_HSEN, FCX_RBBR, FCX_UMOM, FCX_VMOM, FCX_RSDR})
-        if (e->buf(s, g, v) >= 0) out_buf[(size_t)e->buf(s, g, v)] = 1;
   const size_t es = e->esize;
   auto heap = [&](const void *h, int64_t n) { return h && !lib_block_device_ptr(h, (size_t)std::max<int64_t>(n, 1) * es); };
   auto span = [&](int64_t n) { return ((size_t)std::max<int64_t>(n, 1) * es + 255) / 256 * 256; };
@@ -1618,10 +1610,8 @@ static int map_staged(fcx_engine *e, int *count, bool outputs_only = false) {
     items.push_back(Item{dev, ext, st, n, total});
     total += span(n);
   };
-  for (size_t b = 0; b < e->bufs.size(); ++b) {
-    Buffer &bf = e->bufs[b];
-    if (!bf.external && heap(bf.host, bf.n) && (!outputs_only || out_buf[b])) add(&bf.dev, &bf.external, &bf.st, bf.n);
-  }
+  for (auto &bf : e->bufs)
+    if (!bf.external && heap(bf.host, bf.n)) add(&bf.dev, &bf.external, &bf.st, bf.n);
   for (auto &f : e->atm_fields)
     if (!f.external && heap(f.out_host, e->n_atmos)) add(&f.out_dev, &f.external, &f.st, std::max<int64_t>(e->n_atmos, 0));
   for (auto &rm : e->remaps)
@@ -1724,10 +1714,6 @@ extern "C" int fcx_commit(fcx_engine *e) {
     if (e->staging)
       if (int r = map_staged(e, &staged)) return r;
     e->zc_active = e->zc_active || staged > 0;
-  } else if (e->zero_copy == 3 && e->staging) {  // outputs in place, inputs by DMA
-    int staged = 0;
-    if (int r = map_staged(e, &staged, true)) return r;
-    e->zc_active = staged > 0;
   }
   bool any_external = false;
   for (auto &bf : e->bufs) any_external = any_external || bf.external;
@@ -2820,7 +2806,7 @@ extern "C" int fcx_set_option(fcx_engine *e, int option, int64_t value) {
       return FCX_OK;
     case FCX_OPT_ZERO_COPY:
       if (e->committed) return fail(FCX_E_STATE, "zero_copy is applied at fcx_commit");
-      if (value < 0 || value > 3) return fail(FCX_E_ARG, "zero_copy: 0 off, 1 on, 2 auto, 3 outputs only");
+      if (value < 0 || value > 2) return fail(FCX_E_ARG, "zero_copy: 0 off, 1 on, 2 auto");
       e->zero_copy = (int)value;
       return FCX_OK;
     case FCX_OPT_PIPELINE_MIN_CHUNK:

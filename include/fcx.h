@@ -333,11 +333,8 @@ enum fcx_option {
   FCX_OPT_ZERO_COPY = 9,        /* fields in fcx_host_malloc memory read/written by the
                                    kernels in place through the host link: no mirrors, no
                                    copy calls.  2 auto (default): when every grid is below
-                                   2 x PIPELINE_MIN_CHUNK cells; 1: at any size; 0: never;
-                                   3: only the arrays the path writes (outputs in place,
-                                   inputs by the staging DMAs: the link's two directions
-                                   busy at once when several engines step side by side).
-                                   Caller heap arrays go through the staging arena */
+                                   2 x PIPELINE_MIN_CHUNK cells; 1: at any size; 0: never.
+                                   Caller heap arrays always take device mirrors */
   FCX_OPT_TIMING = 10,          /* record the events behind fcx_last_kernel_ms (default 0:
                                    two event records per run cost ~8 us on small grids) */
   FCX_OPT_HOST_STAGING = 15,    /* caller heap arrays (not fcx_host_malloc memory) reach
