@@ -232,3 +232,35 @@ def test_one_cell_shared_on_both_sides_takes_one_slot():
                 assert b"one boundary slot" in lib.fcx_last_error()
         finally:
             lib.fcx_destroy(h)
+
+
+def test_abort_handler_receives_the_message():
+    """fcx_set_abort_handler / fcx_abort (the oasis_abort hook of the drop-in,
+    flux_calculator.F90:883-887): without a handler fcx_abort reports FCX_E_STATE; a
+    registered one gets the message; NULL unregisters.  Host-side only."""
+    lib = _lib.load()
+    got = []
+    proto = ctypes.CFUNCTYPE(None, ctypes.c_char_p)
+    cb = proto(lambda msg: got.append(msg.decode()))
+    assert lib.fcx_set_abort_handler(None) == 0
+    assert lib.fcx_abort(b"nobody listens") == 2
+    assert lib.fcx_set_abort_handler(ctypes.cast(cb, ctypes.c_void_p)) == 0
+    try:
+        assert lib.fcx_abort(b"flux engine error in fcx_step: boom") == 0
+    finally:
+        assert lib.fcx_set_abort_handler(None) == 0
+    assert got == ["flux engine error in fcx_step: boom"]
+    assert lib.fcx_abort(b"again") == 2 and len(got) == 1
+
+
+def test_group_and_comm_queries_validate_arguments():
+    """fcx_last_group_size / fcx_comm_verify / fcx_comm_overlapped / fcx_run_group_exchange
+    reject NULL handles with FCX_E_ARG (no GPU needed)."""
+    lib = _lib.load()
+    m = ctypes.c_int32()
+    n = ctypes.c_int64()
+    assert lib.fcx_last_group_size(None, ctypes.byref(m)) == 1
+    assert lib.fcx_comm_verify(None, 1) == 1
+    assert lib.fcx_comm_overlapped(None, ctypes.byref(n)) == 1
+    assert lib.fcx_run_group_exchange(None, None, 0, 3, 0) == 1
+    assert lib.fcx_step_async(None, 3, 0) != 0
