@@ -17,8 +17,10 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <functional>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <set>
 #include <string>
@@ -155,6 +157,21 @@ int default_host_threads() {
 
 }  // namespace
 
+// fcx_upload_field: one host thread per engine that stages the fields the host hands over one
+// by one (gather into the arena, DMA on the engine stream) while the host receives the next
+struct FieldUploader {
+  std::thread th;
+  std::mutex mu;
+  std::condition_variable cv, idle;
+  std::deque<int> q;  // buffer ids
+  int busy = 0;
+  bool stop = false;
+  bool prepared = false;  // this step's arena preconditions are met (stage_in's waits)
+  bool dma = false;       // a DMA out of the arena was queued since the last join
+  int err = 0;
+  std::string msg;
+};
+
 struct fcx_engine {
   int device = 0;
   int T = 0;
@@ -227,6 +244,8 @@ struct fcx_engine {
   bool atmos_in_run = true;
   bool atm_done_fused = false;  // the last fcx_run already accumulated the atmosphere fields
   int group_members = 0;        // engines in the merged launch of its last run (0: fcx_run)
+  std::unique_ptr<FieldUploader> uploader;  // fcx_upload_field
+  std::vector<char> field_sent;             // buffers fcx_upload_field staged for the coming run
   // exchange -> model remaps (SCRIP links, CSR by destination in link order)
   struct RemapField {
     int phase, s, g, var;
@@ -383,8 +402,11 @@ extern "C" int fcx_create(int device, int num_surface_types, const int32_t grid_
   return FCX_OK;
 }
 
+static void uploader_stop(fcx_engine *e);
+
 extern "C" int fcx_destroy(fcx_engine *e) {
   if (!e) return FCX_OK;
+  uploader_stop(e);
   if (!e->gpu_ready) {
     delete e;
     return FCX_OK;
@@ -1908,10 +1930,13 @@ static const uint32_t kEarly = S_RBBR;
 static const uint32_t kNormal = S_QSUR_T | S_QSUR_U | S_QSUR_V | S_MEVA | S_HLAT | S_HSEN | S_UMOM |
                                 S_VMOM | S_RSDR;
 
+static int uploader_join(fcx_engine *e);
+
+// every call but fcx_upload_field first waits for the fields fcx_upload_field handed over
 static int check(fcx_engine *e) {
   if (!e) return fail(FCX_E_ARG, "NULL engine");
   if (!e->committed) return fail(FCX_E_STATE, "fcx_commit has not been called");
-  return FCX_OK;
+  return uploader_join(e);
 }
 
 static const double *month_slice(fcx_engine *e, int32_t t, int *rc) {
@@ -1930,6 +1955,7 @@ static int copy_bufs(fcx_engine *e, const std::vector<int> &ids, bool h2d, std::
   for (int b : ids) {
     const Buffer &bf = e->bufs[b];
     if (bf.n == 0) continue;
+    if (h2d && (size_t)b < e->field_sent.size() && e->field_sent[(size_t)b]) continue;  // fcx_upload_field
     if (bf.st.sp >= 0) {  // (also a heap array whose mirror is a mapped arena image)
       xs.push_back(xfer_of(bf.st, bf.host, bf.n));
       continue;
@@ -2043,6 +2069,119 @@ static uint32_t phase_stages(int phase) {
   if (phase & FCX_PHASE_EARLY) st |= kEarly;
   if (phase & FCX_PHASE_NORMAL) st |= kNormal;
   return st;
+}
+
+// ---- fcx_upload_field: the inputs of a phase handed over one at a time
+
+// one field: its heap array into the arena and the DMA to its mirror (or its direct copy) on
+// the engine stream -- stage_in for one buffer, on the uploader thread
+static int upload_one(fcx_engine *e, int b) {
+  FieldUploader &u = *e->uploader;
+  const Buffer &bf = e->bufs[(size_t)b];
+  if (bf.n == 0) return FCX_OK;
+  if (bf.st.sp >= 0) {
+    if (!u.prepared) {  // stage_in's waits, once per step
+      bool mapped = false;
+      for (const StagePool &p : e->spools) mapped = mapped || p.mapped;
+      if (!e->pending_out.empty() || mapped) {
+        HIP_TRY(hipStreamSynchronize(e->stream));
+        if (int r = stage_flush(e)) return r;
+      }
+      if (e->stage_in_live) HIP_TRY(hipEventSynchronize(e->ev_stage_in));
+      u.prepared = true;
+    }
+    const std::vector<Xfer> xs{xfer_of(bf.st, bf.host, bf.n)};
+    if (int r = stage_alloc(e, xs)) return r;
+    stage_copy(e, xs, 0, -1, true);
+    if (!e->spools[(size_t)bf.st.sp].mapped) {
+      HIP_TRY(stage_dma(e, xs, 0, -1, true, e->stream));
+      u.dma = true;
+    }
+  } else if (!bf.external) {
+    HIP_TRY(copy_cells(e, bf, 0, bf.n, true, e->stream));
+  }
+  return FCX_OK;
+}
+
+static void uploader_loop(fcx_engine *e) {
+  FieldUploader &u = *e->uploader;
+  (void)hipSetDevice(e->device);
+  std::unique_lock<std::mutex> lk(u.mu);
+  for (;;) {
+    u.cv.wait(lk, [&] { return u.stop || !u.q.empty(); });
+    if (u.q.empty()) return;  // stop
+    const int b = u.q.front();
+    u.q.pop_front();
+    u.busy = 1;
+    lk.unlock();
+    const int r = upload_one(e, b);
+    lk.lock();
+    if (r && !u.err) {
+      u.err = r;
+      u.msg = g_err;
+    }
+    u.busy = 0;
+    if (u.q.empty()) u.idle.notify_all();
+  }
+}
+
+// the handed-over fields are staged and their DMAs queued (before anything else runs)
+static int uploader_join(fcx_engine *e) {
+  if (!e->uploader) return FCX_OK;
+  FieldUploader &u = *e->uploader;
+  std::unique_lock<std::mutex> lk(u.mu);
+  u.idle.wait(lk, [&] { return u.q.empty() && u.busy == 0; });
+  if (u.dma) {  // the next upload into the arena waits for these DMAs (stage_in's rule)
+    u.dma = false;
+    if (!e->ev_stage_in) HIP_TRY(hipEventCreateWithFlags(&e->ev_stage_in, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(e->ev_stage_in, e->stream));
+    e->stage_in_live = true;
+  }
+  if (u.err) {
+    const int r = u.err;
+    u.err = 0;
+    return fail(r, "fcx_upload_field: %s", u.msg.c_str());
+  }
+  return FCX_OK;
+}
+
+static void uploader_stop(fcx_engine *e) {
+  if (!e->uploader) return;
+  {
+    std::lock_guard<std::mutex> lk(e->uploader->mu);
+    e->uploader->stop = true;
+  }
+  e->uploader->cv.notify_all();
+  if (e->uploader->th.joinable()) e->uploader->th.join();
+  e->uploader.reset();
+}
+
+// a run takes the handed-over fields: the next step's fields start afresh
+static void fields_taken(fcx_engine *e) {
+  std::fill(e->field_sent.begin(), e->field_sent.end(), 0);
+  if (e->uploader) e->uploader->prepared = false;  // (joined: the thread is idle)
+}
+
+extern "C" int fcx_upload_field(fcx_engine *e, int s, int g, int var) {
+  if (!e) return fail(FCX_E_ARG, "NULL engine");
+  if (!e->committed) return fail(FCX_E_STATE, "fcx_commit has not been called");
+  if (s < 0 || s > kMaxTypes || g < 1 || g > 3 || var < 1 || var > kNumVars)
+    return fail(FCX_E_ARG, "field (%d, %d, %d) outside the data model", s, g, var);
+  const int b = e->buf(s, g, var);
+  if (b < 0) return fail(FCX_E_ARG, "local_field(%d,%d)%%var(%s) is not bound", s, g, kVarNames[var - 1]);
+  if (e->field_sent.size() != e->bufs.size()) e->field_sent.assign(e->bufs.size(), 0);
+  if (e->field_sent[(size_t)b]) return FCX_OK;  // an alias of a field already handed over
+  e->field_sent[(size_t)b] = 1;
+  if (!e->uploader) {
+    e->uploader.reset(new FieldUploader());
+    e->uploader->th = std::thread(uploader_loop, e);
+  }
+  {
+    std::lock_guard<std::mutex> lk(e->uploader->mu);
+    e->uploader->q.push_back(b);
+  }
+  e->uploader->cv.notify_one();
+  return FCX_OK;
 }
 
 extern "C" int fcx_upload(fcx_engine *e, int phase) {
@@ -2223,6 +2362,7 @@ extern "C" int fcx_run(fcx_engine *e, int phase, int32_t t) {
   e->atm_done = e->exchanged = false;
   e->rec_plan = nullptr;
   e->group_members = 0;
+  fields_taken(e);
   if (!e->any_regrid) {
     Plan *pl;
     if (int r = get_plan(e, phase_stages(phase), phase, &pl)) return r;
@@ -2332,6 +2472,7 @@ static void group_members(const GroupLaunchMember *mem, int nm, GroupMember *gm)
     e->atm_done = e->exchanged = false;
     e->rec_plan = nullptr;
     e->rec_written = false;
+    fields_taken(e);
     const int64_t own = (m.lc.f32 ? kF32Cpl : 2) * (64 - m.lc.halo);
     gm[k] = GroupMember{m.pl->dev, m.corr_m, 0, m.lc.variant, 0, m.pl->af};
     gm[k].af.n_tiles = (m.pl->host.n_max + own - 1) / own;
@@ -2523,7 +2664,8 @@ static bool host_bound(const fcx_engine *e, const Plan *pl) {
 extern "C" int fcx_step(fcx_engine *e, int phase, int32_t t) {
   if (int r = check(e)) return r;
   if (phase < 1 || phase > 3) return fail(FCX_E_ARG, "phase %d unknown", phase);
-  if (e->chunks > 1 && !e->any_regrid) {
+  const bool handed = std::find(e->field_sent.begin(), e->field_sent.end(), 1) != e->field_sent.end();
+  if (e->chunks > 1 && !e->any_regrid && !handed) {  // (fields handed over: the sequential step)
     Plan *pl;
     if (int r = get_plan(e, phase_stages(phase), phase, &pl)) return r;
     if (host_bound(e, pl) && pl->host.n_max >= 2 * e->min_chunk) return step_pipelined(e, phase, t, pl);
@@ -2542,7 +2684,8 @@ extern "C" int fcx_step(fcx_engine *e, int phase, int32_t t) {
 extern "C" int fcx_step_async(fcx_engine *e, int phase, int32_t t) {
   if (int r = check(e)) return r;
   if (phase < 1 || phase > 3) return fail(FCX_E_ARG, "phase %d unknown", phase);
-  if (e->chunks > 1 && !e->any_regrid) {
+  const bool handed = std::find(e->field_sent.begin(), e->field_sent.end(), 1) != e->field_sent.end();
+  if (e->chunks > 1 && !e->any_regrid && !handed) {  // (fields handed over: the sequential step)
     Plan *pl;
     if (int r = get_plan(e, phase_stages(phase), phase, &pl)) return r;
     if (host_bound(e, pl) && pl->host.n_max >= 2 * e->min_chunk) return step_pipelined(e, phase, t, pl);
@@ -2558,6 +2701,8 @@ extern "C" int fcx_step_async(fcx_engine *e, int phase, int32_t t) {
 
 extern "C" int fcx_synchronize(fcx_engine *e) {
   if (!e) return fail(FCX_E_ARG, "NULL engine");
+  if (e->committed)
+    if (int r = uploader_join(e)) return r;
   HIP_TRY(hipStreamSynchronize(e->stream));
   return stage_flush(e);
 }
@@ -2571,6 +2716,7 @@ static int per_call(fcx_engine *e, uint32_t stages, int avg_phases, int32_t t) {
   const double *corr_m = (stages & S_MEVA) ? month_slice(e, t, &rc) : nullptr;
   if ((stages & S_MEVA) && rc) return rc;
   if (int r = copy_bufs(e, pl->reads, true)) return r;
+  fields_taken(e);
   if (e->timing) HIP_TRY(hipEventRecord(e->ev0, e->stream));
   if (int r = launch_plan(e, pl, corr_m)) return r;
   if (e->timing) HIP_TRY(hipEventRecord(e->ev1, e->stream));

@@ -130,6 +130,13 @@ MODULE fcx_c_api
       INTEGER(c_int32_t), VALUE :: t
       INTEGER(c_int) :: fcx_step_async
     END FUNCTION
+    ! one input field handed over after its oasis_get (staged by the engine's upload thread)
+    FUNCTION fcx_upload_field(engine, surface_type, grid, var) BIND(C, name='fcx_upload_field')
+      IMPORT :: c_int, c_ptr
+      TYPE(c_ptr), VALUE :: engine
+      INTEGER(c_int), VALUE :: surface_type, grid, var
+      INTEGER(c_int) :: fcx_upload_field
+    END FUNCTION
     FUNCTION fcx_run(engine, phase, t) BIND(C, name='fcx_run')
       IMPORT :: c_int, c_int32_t, c_ptr
       TYPE(c_ptr), VALUE :: engine

@@ -41,7 +41,7 @@ MODULE flux_calculator_calculate
     PUBLIC distribute_shortwave_radiation_flux
     PUBLIC average_across_surface_types
     PUBLIC fcx_attach, fcx_register_average, fcx_commit_engine, fcx_run_phase, fcx_detach
-    PUBLIC fcx_register_abort, fcx_start_phase, fcx_finish_phase
+    PUBLIC fcx_register_abort, fcx_start_phase, fcx_finish_phase, fcx_hand_over_field
 
     TYPE(c_ptr), SAVE :: engine = c_null_ptr
     ! What fcx_attach bound.  The reference subroutines take the bottom model, the type count,
@@ -274,6 +274,16 @@ CONTAINS
         INTEGER(c_int), INTENT(IN) :: phase
         CALL check(fcx_step_async(engine, phase, INT(current_step_time, c_int32_t)), 'fcx_step_async')
     END SUBROUTINE fcx_start_phase
+
+    ! one input field right after its oasis_get (flux_calculator.F90:876-880, 946-950): the
+    ! engine's upload thread stages it while the host receives the next field; the phase that
+    ! follows moves only the inputs not handed over.  The array may be overwritten once the
+    ! next engine call returns.
+    SUBROUTINE fcx_hand_over_field(surface_type, which_grid, my_idx)
+        INTEGER, INTENT(IN) :: surface_type, which_grid, my_idx
+        CALL check(fcx_upload_field(engine, INT(surface_type, c_int), INT(which_grid, c_int), INT(my_idx, c_int)), &
+                   'fcx_upload_field')
+    END SUBROUTINE fcx_hand_over_field
 
     SUBROUTINE fcx_finish_phase()
         CALL check(fcx_synchronize(engine), 'fcx_synchronize')

@@ -93,6 +93,7 @@ SIGNATURES = [
     ("fcx_memcpy", _I, [_P, _P, _c.c_size_t, _I]),
     ("fcx_last_group_size", _I, [_P, _c.POINTER(_I32)]),
     ("fcx_step_async", _I, [_P, _I, _I32]),
+    ("fcx_upload_field", _I, [_P, _I, _I, _I]),
     ("fcx_run_group_exchange", _I, [_P, _c.POINTER(_P), _I, _I, _I32]),
     ("fcx_comm_overlapped", _I, [_P, _c.POINTER(_I64)]),
     ("fcx_comm_verify", _I, [_P, _I]),

@@ -145,6 +145,10 @@ class Engine:
         """fcx_step_async: the step queued; the host arrays hold the outputs after synchronize()."""
         _lib.check(self.lib.fcx_step_async(self.h, phase, int(current_step_time)))
 
+    def upload_field(self, surface_type, grid, name):
+        """fcx_upload_field: one input field handed over (staged by the engine's upload thread)."""
+        _lib.check(self.lib.fcx_upload_field(self.h, int(surface_type), int(grid), IDX[name]))
+
     def set_stream(self, stream):
         """fcx_set_stream: launch on this HIP stream (a raw hipStream_t, e.g. a torch
         stream's .cuda_stream) from now on, e.g. a capturing stream for a HIP graph."""

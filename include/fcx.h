@@ -168,6 +168,15 @@ int fcx_synchronize(fcx_engine *e);
  * on its own stream), or overlaps its own work -- another component's exchange -- with the
  * step.  Host-bound grids of at least two pipeline chunks complete inside the call. */
 int fcx_step_async(fcx_engine *e, int phase, int32_t current_step_time);
+/* One input field handed over as the host receives it (oasis_get of field j, then
+ * fcx_upload_field): its host array is copied into the staging arena and DMAed to its
+ * mirror by the engine's upload thread while the host goes on to receive the next field
+ * (flux_calculator.F90:872-897, 938-966: the reference gets the fields one by one).  The
+ * value at the call is what the next run uses; the host may overwrite the array once the
+ * next engine call (any but fcx_upload_field) returns -- every call first waits for the
+ * handed-over fields.  fcx_upload / fcx_step / fcx_step_async then move only the phase's
+ * remaining inputs.  Aliases (one array in several slots) are handed over once. */
+int fcx_upload_field(fcx_engine *e, int surface_type, int grid, int var);
 
 /* ---- per call: the reference subroutines one by one (exact drop-in semantics; each
  * call uploads what it reads, computes, downloads what it writes, and synchronises) ---- */

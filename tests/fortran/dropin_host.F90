@@ -8,7 +8,10 @@
 ! No regridding matrices are set, so the reference's do_regridding calls between the
 ! calc_* calls would be no-ops and are left out.
 !
-!   dropin_host <dir> percall|fused|async|noattach|badtable|badgrid|badtypes[+abort]
+!   dropin_host <dir> percall|fused|async|handover|noattach|badtable|badgrid|badtypes[+abort]
+!
+! handover: before each fused phase every bound input field is handed over one by one
+! (fcx_hand_over_field, as after each oasis_get), then the phase runs.
 !
 ! +abort: the host registers its abort routine (fcx_register_abort) first, as a coupled
 ! host registers one that calls oasis_abort; this one prints the message and stops with 3.
@@ -141,13 +144,18 @@ PROGRAM dropin_host
         CALL average_across_surface_types(1, 22, nsurf + 1, grid_size, local_field)
     ENDIF
 
-    IF (TRIM(mode) == 'fused' .OR. TRIM(mode) == 'async') THEN
+    IF (TRIM(mode) == 'fused' .OR. TRIM(mode) == 'async' .OR. TRIM(mode) == 'handover') THEN
         ! INTEGRATION.md: two phases replace :902-918 and :972-1008
         DO i = 1, nav
             CALL fcx_register_average(av(1, i) == 1, av(2, i), av(3, i))
         ENDDO
         CALL fcx_commit_engine()
-        IF (TRIM(mode) == 'async') THEN
+        IF (TRIM(mode) == 'handover') THEN
+            CALL hand_over_inputs()
+            CALL fcx_run_phase(FCX_PHASE_EARLY)
+            CALL hand_over_inputs()
+            CALL fcx_run_phase(FCX_PHASE_NORMAL)
+        ELSE IF (TRIM(mode) == 'async') THEN
             ! each phase started, then finished; the early phase's outputs are complete
             ! before the normal phase starts (its oasis_put precedes the normal oasis_get)
             CALL fcx_start_phase(FCX_PHASE_EARLY)
@@ -187,6 +195,22 @@ PROGRAM dropin_host
     WRITE (*, '(A)') 'DROPIN_HOST OK'
 
 CONTAINS
+
+    ! every bound field that no flux writes, handed over one by one as the host would after
+    ! each oasis_get
+    SUBROUTINE hand_over_inputs()
+        INTEGER :: ss, gg, vv
+        DO ss = 0, MAX_SURFACE_TYPES
+            DO gg = 1, 3
+                DO vv = 1, MAX_VARNAMES
+                    IF (.NOT. ASSOCIATED(local_field(ss, gg)%var(vv)%field)) CYCLE
+                    IF (ANY(vv == [idx_QSUR, idx_MEVA, idx_HLAT, idx_HSEN, idx_RBBR, idx_UMOM, idx_VMOM, &
+                                   idx_RSDR])) CYCLE
+                    CALL fcx_hand_over_field(ss, gg, vv)
+                ENDDO
+            ENDDO
+        ENDDO
+    END SUBROUTINE hand_over_inputs
 
     ! the P7 trigger of the main program: the type-0 slot is associated and surface type 2 exists
     SUBROUTINE averages(phase)

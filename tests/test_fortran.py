@@ -78,14 +78,16 @@ def write_manifest(case, d, step_time):
 
 @pytest.mark.gpu
 @pytest.mark.skipif(not os.path.exists(DROPIN), reason="Fortran drop-in host not built")
-@pytest.mark.parametrize("mode", ["percall", "fused", "async"])
+@pytest.mark.parametrize("mode", ["percall", "fused", "async", "handover"])
 @pytest.mark.parametrize("variant,T", [("CCLM", 2), ("MOM5", 3), ("RCO", 1)])
 def test_dropin_module_in_a_fortran_host(tmp_path, mode, variant, T):
     """The drop-in module flux_calculator_calculate driven by a Fortran host whose
     local_field is the reference's own flux_calculator_basic (tests/fortran/dropin_host.F90):
     the reference subroutines one by one (percall), the two fused phases (fused), or each
-    phase started and finished in two calls (async: fcx_step_async + fcx_synchronize),
-    against the oracle on the same inputs (tests/parity.py tolerance)."""
+    phase started and finished in two calls (async: fcx_step_async + fcx_synchronize), or
+    every input field handed over one by one before each phase (handover: fcx_upload_field,
+    as after each oasis_get), against the oracle on the same inputs (tests/parity.py
+    tolerance)."""
     import numpy as np
 
     import oracle_lib

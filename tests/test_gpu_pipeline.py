@@ -401,3 +401,42 @@ def test_step_async_engines_started_from_one_thread(n):
         a[:] = orig
     for g, w in zip(got, want):
         same_bits(g, w)
+
+
+@pytest.mark.parametrize("n", [32_768, 600_001])
+@pytest.mark.parametrize("variant", ["CCLM", "MOM5"])
+def test_fields_handed_over_one_by_one(variant, n):
+    """fcx_upload_field (the OASIS staging glue: each input field handed over after its
+    oasis_get, staged by the engine's upload thread): all of them, or every other one with
+    fcx_step moving the rest, over two steps with changed inputs -- the bits of fcx_step."""
+    case = build_case(variant, n=n, T=1, bias=True, seed=9)
+    outs = {id(case.lf.field[k]) for k in case.outputs}
+    slots, seen = [], set()
+    for (s, g, name), a in case.lf.field.items():
+        if id(a) not in outs and id(a) not in seen:
+            seen.add(id(a))
+            slots.append(((s, g, name), a))
+    orig = [a.copy() for _, a in slots]
+
+    def steps(hand_over):
+        res = []
+        eng = Engine(case.lf, 1, case.methods, corrections=case.corrections)
+        for step in range(2):
+            for (_, a), o in zip(slots, orig):
+                a[:] = o * (1.0 + 1e-3 * step)  # this step's inputs, as oasis_get writes them
+            for k in case.outputs:
+                case.lf.field[k][:] = np.nan
+            for i, (key, _) in enumerate(slots):
+                if hand_over == "all" or (hand_over == "half" and i % 2 == 0):
+                    eng.upload_field(*key)
+            eng.step(PHASE_ALL, STEP_T + 3600 * step)
+            res.append({k: np.array(case.lf.field[k], copy=True) for k in case.outputs})
+        eng.close()
+        return res
+
+    want = steps(None)
+    for mode in ("all", "half"):
+        for a, b in zip(steps(mode), want):
+            same_bits(a, b)
+    for (_, a), o in zip(slots, orig):
+        a[:] = o
