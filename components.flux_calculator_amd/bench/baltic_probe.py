@@ -83,7 +83,51 @@ def main():
             e.close()
         out["modes"][name] = res
         print(name, json.dumps(res), flush=True)
+    out["handover"] = handover(n, a.steps)
+    print("handover", json.dumps(out["handover"]), flush=True)
     print(json.dumps(out), flush=True)
+
+
+def handover(n, steps):
+    """The coupled host's step with OASIS's receives in it: every input field arrives by an
+    oasis_get, played here by a copy from a receive buffer into the field array (256 KB at
+    32,768 cells).  'after' = all receives, then fcx_step; 'handed' = each receive followed
+    by fcx_upload_field (the engine's thread stages the field while the next one arrives),
+    then fcx_step.  Median wall time per step of the three variants one after the other."""
+    from fcx.basic import PHASE_ALL
+    from fcx.engine import Engine
+    from fcx.synthetic import build_case
+
+    res = {}
+    cases = [build_case(v, n=n, T=1, bias=True) for v in VARIANTS]
+    per = []
+    for c in cases:
+        outs = {id(c.lf.field[k]) for k in c.outputs}
+        slots, seen = [], set()
+        for key, arr in c.lf.field.items():
+            if id(arr) not in outs and id(arr) not in seen:
+                seen.add(id(arr))
+                slots.append((key, arr, arr.copy()))  # (slot, field array, "received" data)
+        per.append(slots)
+    for mode in ("after", "handed"):
+        engines = [Engine(c.lf, 1, c.methods, corrections=c.corrections) for c in cases]
+        ts = []
+        for k in range(50 + steps):
+            t0 = time.perf_counter()
+            for e, slots in zip(engines, per):
+                for key, arr, recv in slots:
+                    np.copyto(arr, recv)  # oasis_get
+                    if mode == "handed":
+                        e.upload_field(*key)
+                e.step(PHASE_ALL, k * 3600)
+            if k >= 50:
+                ts.append(time.perf_counter() - t0)
+        for e in engines:
+            e.close()
+        res[mode + "_us"] = round(float(np.median(ts)) * 1e6, 1)
+    res["rule"] = ("three variants one after the other; each input field received by a copy from a receive buffer "
+                   "(the oasis_get), then fcx_step ('after') or each receive followed by fcx_upload_field ('handed')")
+    return res
 
 
 if __name__ == "__main__":
