@@ -98,6 +98,11 @@ def handover(n, steps):
     from fcx.engine import Engine
     from fcx.synthetic import build_case
 
+    def wait_us(us):  # a receive's wait for the sender (MPI progress), no memory traffic
+        t_end = time.perf_counter() + us * 1e-6
+        while time.perf_counter() < t_end:
+            pass
+
     res = {}
     cases = [build_case(v, n=n, T=1, bias=True) for v in VARIANTS]
     per = []
@@ -109,24 +114,29 @@ def handover(n, steps):
                 seen.add(id(arr))
                 slots.append((key, arr, arr.copy()))  # (slot, field array, "received" data)
         per.append(slots)
-    for mode in ("after", "handed"):
-        engines = [Engine(c.lf, 1, c.methods, corrections=c.corrections) for c in cases]
-        ts = []
-        for k in range(50 + steps):
-            t0 = time.perf_counter()
-            for e, slots in zip(engines, per):
-                for key, arr, recv in slots:
-                    np.copyto(arr, recv)  # oasis_get
-                    if mode == "handed":
-                        e.upload_field(*key)
-                e.step(PHASE_ALL, k * 3600)
-            if k >= 50:
-                ts.append(time.perf_counter() - t0)
-        for e in engines:
-            e.close()
-        res[mode + "_us"] = round(float(np.median(ts)) * 1e6, 1)
-    res["rule"] = ("three variants one after the other; each input field received by a copy from a receive buffer "
-                   "(the oasis_get), then fcx_step ('after') or each receive followed by fcx_upload_field ('handed')")
+    for recv_model in ("copy", "wait20"):
+        for mode in ("after", "handed"):
+            engines = [Engine(c.lf, 1, c.methods, corrections=c.corrections) for c in cases]
+            ts = []
+            for k in range(50 + steps):
+                t0 = time.perf_counter()
+                for e, slots in zip(engines, per):
+                    for key, arr, recv in slots:
+                        if recv_model == "copy":
+                            np.copyto(arr, recv)  # oasis_get: the message copied into the field
+                        else:
+                            wait_us(20)  # oasis_get: waiting 20 us for the sender
+                        if mode == "handed":
+                            e.upload_field(*key)
+                    e.step(PHASE_ALL, k * 3600)
+                if k >= 50:
+                    ts.append(time.perf_counter() - t0)
+            for e in engines:
+                e.close()
+            res[f"{recv_model}_{mode}_us"] = round(float(np.median(ts)) * 1e6, 1)
+    res["rule"] = ("three variants one after the other; each input field received (copy: a copy from a receive "
+                   "buffer into the field array; wait20: 20 us of waiting for the sender), then fcx_step ('after') or "
+                   "each receive followed by fcx_upload_field ('handed')")
     return res
 
 
