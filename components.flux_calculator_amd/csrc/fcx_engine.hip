@@ -403,6 +403,7 @@ extern "C" int fcx_create(int device, int num_surface_types, const int32_t grid_
 }
 
 static void uploader_stop(fcx_engine *e);
+static int uploader_join(fcx_engine *e);
 
 extern "C" int fcx_destroy(fcx_engine *e) {
   if (!e) return FCX_OK;
@@ -456,6 +457,8 @@ extern "C" int fcx_destroy(fcx_engine *e) {
 
 extern "C" int fcx_set_stream(fcx_engine *e, void *stream) {
   if (!e) return fail(FCX_E_ARG, "NULL engine");
+  if (e->committed)  // handed-over fields queue their DMAs on the current stream
+    if (int r = uploader_join(e)) return r;
   if (e->own_stream && e->stream) {
     (void)hipStreamSynchronize(e->stream);
     (void)hipStreamDestroy(e->stream);
