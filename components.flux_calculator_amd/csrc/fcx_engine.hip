@@ -1431,18 +1431,22 @@ static void stage_setup(fcx_engine *e) {
       if (!f.external && heap(f.out_host, rm.n_dst)) f.st = stage_ref(e, f.out_dev);
 }
 
-// at commit: the host image of every staging pool (page-locked, the pool's size: the pinned
-// footprint is fcx_staging_bytes).  A pool whose image cannot be page-locked (a memory-tight
-// node) falls back to the direct path -- its mirrors are copied one runtime copy per array
-// from the caller's pageable memory, as with FCX_OPT_HOST_STAGING 0 -- so a step never
-// meets an allocation failure.
-static void stage_alloc_all(fcx_engine *e) {
+// at commit: the host image of every staging pool a whole step transfers (page-locked, the
+// pool's size: the pinned footprint is fcx_staging_bytes).  A pool whose image cannot be
+// page-locked (a memory-tight node) falls back to the direct path -- its mirrors are copied
+// one runtime copy per array from the caller's pageable memory, as with
+// FCX_OPT_HOST_STAGING 0 -- so a step never meets an allocation failure.  Pools only other
+// calls transfer (eager[i] == 0: e.g. the tiled layout's pool of arrays no step reads or
+// writes) get their image at their first transfer (page-locking them up front
+// locked ~1 GB per 10M-cell engine that no step uses).
+static void stage_alloc_all(fcx_engine *e, const std::vector<char> &eager) {
   // FCX_TEST_PIN_FAIL=1 (tests only): every image fails, as on a node out of lockable memory
   const char *inject = std::getenv("FCX_TEST_PIN_FAIL");
   const bool fail_all = inject && *inject == '1';
   for (size_t i = 0; i < e->spools.size(); ++i) {
     StagePool &p = e->spools[i];
     if (p.host) continue;  // (a mapped arena has its image already)
+    if (i < eager.size() && !eager[i] && !fail_all) continue;  // at its first transfer
     if (!fail_all && hipHostMalloc((void **)&p.host, std::max<size_t>(p.bytes, 1), hipHostMallocDefault) == hipSuccess)
       continue;
     (void)hipGetLastError();
@@ -1458,10 +1462,20 @@ static void stage_alloc_all(fcx_engine *e) {
   }
 }
 
-// the host images of the pools these transfers use (allocated at commit)
+// the host images of the pools these transfers use (allocated at commit, or here at the
+// first transfer of a pool no whole step uses)
 static int stage_alloc(fcx_engine *e, const std::vector<Xfer> &xs) {
-  for (const Xfer &x : xs)
-    if (!e->spools[(size_t)x.sp].host) return fail(FCX_E_STATE, "staging pool %d has no host image", x.sp);
+  for (const Xfer &x : xs) {
+    StagePool &p = e->spools[(size_t)x.sp];
+    if (p.host) continue;
+    if (p.disabled) return fail(FCX_E_STATE, "staging pool %d has no host image", x.sp);
+    if (hipHostMalloc((void **)&p.host, std::max<size_t>(p.bytes, 1), hipHostMallocDefault) != hipSuccess) {
+      (void)hipGetLastError();
+      p.host = nullptr;
+      return fail(FCX_E_NOMEM, "staging pool %d (%zu bytes) could not be page-locked at its first transfer", x.sp,
+                  p.bytes);
+    }
+  }
   return FCX_OK;
 }
 
@@ -1922,8 +1936,25 @@ extern "C" int fcx_commit(fcx_engine *e) {
   }
   if (e->rec_bytes) HIP_TRY(hipMalloc(&e->d_rec, e->rec_bytes));
   stage_setup(e);
-  stage_alloc_all(e);
   e->committed = true;
+  // the pools a whole step transfers are page-locked now, the others at first use
+  std::vector<char> eager(e->spools.size(), e->any_regrid ? 1 : 0);
+  if (!e->any_regrid) {
+    Plan *pl = nullptr;
+    if (get_plan(e, phase_stages(FCX_PHASE_ALL), FCX_PHASE_ALL, &pl) == FCX_OK && pl) {
+      for (const std::vector<int> *ids : {&pl->reads, &pl->writes})
+        for (int b : *ids)
+          if (e->bufs[(size_t)b].st.sp >= 0) eager[(size_t)e->bufs[(size_t)b].st.sp] = 1;
+    } else {
+      std::fill(eager.begin(), eager.end(), 1);
+    }
+    for (auto &f : e->atm_fields)
+      if (f.st.sp >= 0) eager[(size_t)f.st.sp] = 1;
+    for (auto &rm : e->remaps)
+      for (auto &f : rm.fields)
+        if (f.st.sp >= 0) eager[(size_t)f.st.sp] = 1;
+  }
+  stage_alloc_all(e, eager);
   return FCX_OK;
 }
 

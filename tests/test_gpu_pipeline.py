@@ -440,3 +440,24 @@ def test_fields_handed_over_one_by_one(variant, n):
             same_bits(a, b)
     for (_, a), o in zip(slots, orig):
         a[:] = o
+
+
+def test_staging_pins_only_what_a_step_transfers():
+    """ADVICE r04: the staging arena page-locks, at fcx_commit, the pools a whole step moves;
+    the pool of bound arrays no step reads or writes (here CMOI, CHEA, CMOM, FARE, ALBE,
+    ALBA, RSDD of a CCLM case: 7 of its 24 arrays) is page-locked only if a call ever
+    transfers it.  The step's results are unchanged."""
+    n = 200_000
+    case = build_case("CCLM", n=n, T=1, bias=False, seed=4)
+    distinct = {id(a) for a in case.lf.field.values()}
+    eng = Engine(case.lf, 1, case.methods)
+    pinned = eng.staging_bytes()
+    assert 0 < pinned < 0.85 * len(distinct) * n * 8, (pinned, len(distinct))
+    for k in case.outputs:
+        case.lf.field[k][:] = np.nan
+    eng.step(PHASE_ALL, STEP_T)
+    got = {k: np.array(case.lf.field[k], copy=True) for k in case.outputs}
+    assert eng.staging_bytes() == pinned  # a whole step transfers nothing outside those pools
+    eng.close()
+    ref = oracle_lib.run_case(case, "c", current_step_time=STEP_T)
+    assert_parity(got, ref, label="lazy staging pools")
