@@ -446,11 +446,12 @@ def test_staging_pins_only_what_a_step_transfers():
     """ADVICE r04: the staging arena page-locks, at fcx_commit, the pools a whole step moves;
     the pool of bound arrays no step reads or writes (here CMOI, CHEA, CMOM, FARE, ALBE,
     ALBA, RSDD of a CCLM case: 7 of its 24 arrays) is page-locked only if a call ever
-    transfers it.  The step's results are unchanged."""
+    transfers it.  The step's results are unchanged.  (The grid is below the zero-copy size,
+    so that transport is switched off: its mapped arena holds every heap array by design.)"""
     n = 200_000
     case = build_case("CCLM", n=n, T=1, bias=False, seed=4)
     distinct = {id(a) for a in case.lf.field.values()}
-    eng = Engine(case.lf, 1, case.methods)
+    eng = Engine(case.lf, 1, case.methods, options={"zero_copy": 0})
     pinned = eng.staging_bytes()
     assert 0 < pinned < 0.85 * len(distinct) * n * 8, (pinned, len(distinct))
     for k in case.outputs:
