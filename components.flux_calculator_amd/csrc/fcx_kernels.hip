@@ -388,7 +388,7 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
   // atmosphere fields too, a * max(vel, u_min) * p_s (MEVA, HSEN) and a * vel * p_s
   // (momentum).  Same operations on the same values, so the same bits (fcx_physics.h); the
   // type loop loses its pow and PATM / AMOI / AMOM / the wind speed need not stay live.
-  // (round 4, in one process over the same arrays, profiles/r04/ab_derive_t2.json: T = 2 step
+  // (round 4, in one process over the same arrays, profiles/r04/ab/ab_derive_t2.json: T = 2 step
   // 1.665 -> 1.628 ms, MOM5 0.616 -> 0.582 ms, CCLM 0.595 -> 0.588 ms)
   constexpr bool kDerive = TM == 0 && (VAR == 1 || VAR == 2);
   Vec<C, R> taef = {}, amv = {}, mvp = {};
@@ -1152,7 +1152,7 @@ cells_atmos_group_kernel(const GroupArgs g, const Params *__restrict__ P0, const
   // launch and reads them with scalar loads, as in cells_atmos_kernel.  Read through a
   // pointer out of the argument struct, every field was a vector load (and a dependent
   // round trip before the field loads): the group kernel took 1.156 ms against 0.783 ms
-  // for the three launches it replaced (profiles/r04/gdiag/).
+  // for the three launches it replaced (a round-4 diagnostic build, not kept).
   constexpr int kRows = RAVG ? kAvgSlots : kFusedFields;
   __shared__ double s_p[atmos_waves<C>()][wave_lds_doubles<R, C>(kRows)];
   const int wv = threadIdx.x >> 6;
@@ -1193,7 +1193,7 @@ template <class R, int kT>
 __device__ __forceinline__ void fixup_one(const AtmosFused &af, int64_t t, int k) {
   // one crossing record (two lines) holds everything of the common case: every load issued
   // before the head count is known, one memory round trip.  (One thread per boundary with
-  // the whole record in 16-B loads measured the same: profiles/r04/inproc3/.)
+  // the whole record in 16-B loads measured the same: profiles/r04/crossings/inproc3/.)
   const int64_t x0 = t * kT;
   const double *rec = af.xrec + t * kXRec;
   const int2 ha = *reinterpret_cast<const int2 *>(rec + 30);
@@ -1227,7 +1227,7 @@ __global__ __launch_bounds__(256) void atmos_fixup_kernel(const AtmosFused af, i
 // (boundary, field) threads are [first[m], first[m + 1]).  Each dependent launch costs the
 // step its predecessor's drain, the dispatch and the ramp on top of its work: in one process
 // over the same arrays, T = 2 group step 1.560 against 1.566 ms with one fix-up launch per
-// member, T = 1 without halo tiles 0.759 against 0.766 ms (profiles/r04/inproc1/).
+// member, T = 1 without halo tiles 0.759 against 0.766 ms (profiles/r04/crossings/inproc1/).
 template <class R, int kT>
 __global__ __launch_bounds__(256) void atmos_fixup_group_kernel(const FixupGroup g) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
