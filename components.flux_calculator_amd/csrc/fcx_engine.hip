@@ -216,9 +216,9 @@ struct fcx_engine {
   std::vector<double> atm_w;
   bool atm_contiguous = true;
   int32_t *d_atm_row = nullptr, *d_atm_col = nullptr, *d_atm_idx = nullptr;
-  // the fused path's map: fp64 engines a 4-B index per cell (d_atm_idx), fp32 engines the
-  // compacted map (AtmosFused::seg_*: [words] start bits, [words + 1] prefix counts,
-  // [segments] atmosphere cells, one allocation)
+  // the fused path's map: a 4-B index per cell (d_atm_idx, fp64 launches with crossing
+  // records) and the compacted map (fp32 launches and fp64 halo launches; AtmosFused::seg_*:
+  // [words] start bits, [words + 1] prefix counts, [segments] atmosphere cells, one allocation)
   void *d_atm_seg = nullptr;
   int64_t atm_seg_words = 0, atm_segments = 0;
   std::vector<int32_t> atm_idx;
@@ -1815,7 +1815,8 @@ extern "C" int fcx_commit(fcx_engine *e) {
       HIP_TRY(hipMemcpy(e->d_atm_idx, e->atm_idx.data(), e->atm_idx.size() * sizeof(int32_t),
                         hipMemcpyHostToDevice));
     }
-    if (e->atm_contiguous && !e->atm_idx.empty() && e->f32) {  // fp32: the compacted map
+    // the compacted map: fp32 engines, and fp64 ones for their halo launches
+    if (e->atm_contiguous && !e->atm_idx.empty() && (e->f32 || FCX_F64_COMPACT)) {
       const int64_t nx = (int64_t)e->atm_idx.size(), nw = (nx + 31) / 32;
       std::vector<uint32_t> seg((size_t)(2 * nw + 1), 0u);  // bits, then prefix counts (int32)
       std::vector<int32_t> atm;
@@ -2004,6 +2005,19 @@ static int copy_bufs(fcx_engine *e, const std::vector<int> &ids, bool h2d, std::
 #define FCX_ZC_ONE_CELL 1
 #endif
 
+// halo lanes of a fused launch of plan pl over the whole grid (0: crossing records and the
+// fix-up launch): one surface type, on a map whose segments are short enough that `halo`
+// lanes of the next tile's head (at most 1/16 of a wave) cover every crossing
+static int full_range_halo(const fcx_engine *e, const Plan *pl) {
+  const int cpl = e->f32 ? kF32Cpl : 2;
+  const int h = (e->atm_maxseg - 1 + cpl - 1) / cpl;
+  const bool map = e->f32 || !FCX_F64_COMPACT || e->d_atm_seg;  // (the halo kernels' map)
+  if (e->atm_halo && e->atm_crossings > 0 && map &&
+      (pl->host.num_types == 1 || (FCX_HALO_RAVG && pl->host.ravg_on)) && h >= 1 && h <= (cpl == 4 ? 2 : 4))
+    return h;
+  return 0;
+}
+
 // the launch shape of plan pl over cells [lo, hi) (hi < 0: to the end); *fused: the
 // exchange -> atmosphere accumulation rides in the launch (pl->af is brought up to date)
 static LaunchConfig plan_launch(fcx_engine *e, Plan *pl, int64_t lo, int64_t hi, bool *fused) {
@@ -2034,14 +2048,8 @@ static LaunchConfig plan_launch(fcx_engine *e, Plan *pl, int64_t lo, int64_t hi,
     pl->af.left = e->atm_left;
     pl->af.right = e->atm_right;
     // halo tiles instead of crossing records + fix-up: a launch over the whole grid (not a
-    // pipelined chunk) of one surface type, on a map whose segments are short enough that
-    // `halo` lanes of the next tile's head (at most 1/16 of a wave) cover every crossing
-    lc.halo = 0;
-    const int cpl = e->f32 ? kF32Cpl : 2;
-    const int h = (e->atm_maxseg - 1 + cpl - 1) / cpl;
-    if (e->atm_halo && e->atm_crossings > 0 && lo == 0 && (hi < 0 || hi >= pl->host.n_max) &&
-        (pl->host.num_types == 1 || (FCX_HALO_RAVG && pl->host.ravg_on)) && h >= 1 && h <= (cpl == 4 ? 2 : 4))
-      lc.halo = h;
+    // pipelined chunk)
+    lc.halo = lo == 0 && (hi < 0 || hi >= pl->host.n_max) ? full_range_halo(e, pl) : 0;
     pl->af.halo = lc.halo;
   }
   return lc;
@@ -2902,9 +2910,10 @@ extern "C" int fcx_algorithmic_bytes(fcx_engine *e, int phase, int64_t *bytes) {
   const int64_t es = (int64_t)e->esize;
   if (pl->atm_fused && e->specialize && e->launch.cells_per_thread == 2 && e->aligned16 &&
       (!e->f32 || e->launch.max_blocks <= 0)) {
-    nf = 0;  // fused: the compacted map and a weight per cell, the atmosphere outputs (fluxes
-             // not re-read)
-    extra = e->n[0] * 8 + (e->f32 ? (2 * e->atm_seg_words + 1 + e->atm_segments) * 4 : e->n[0] * 4) +
+    nf = 0;  // fused: the map (compacted, or an index per cell) and a weight per cell, the
+             // atmosphere outputs (fluxes not re-read)
+    const bool compact = e->f32 || (FCX_F64_COMPACT && full_range_halo(e, pl) > 0);
+    extra = e->n[0] * 8 + (compact ? (2 * e->atm_seg_words + 1 + e->atm_segments) * 4 : e->n[0] * 4) +
             (int64_t)pl->atm_nf * e->n_atmos * es;
   } else if (nf && e->n_atmos >= 0 && e->atmos_in_run) {
     extra += e->n[0] * 8 + (e->atm_contiguous ? 0 : e->n[0] * 4) + (e->n_atmos + 1) * 4;

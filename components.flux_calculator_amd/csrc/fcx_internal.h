@@ -36,6 +36,11 @@
 #ifndef FCX_HALO_RAVG
 #define FCX_HALO_RAVG 0
 #endif
+// the compacted exchange -> atmosphere map also for the fp64 halo launches (fp32 always);
+// fp64 launches with crossing records keep the 4-B index per cell (A/B: 0 = index only)
+#ifndef FCX_F64_COMPACT
+#define FCX_F64_COMPACT 1
+#endif
 
 namespace fcx {
 

@@ -873,12 +873,13 @@ __device__ __forceinline__ void atmos_tile(const Params *__restrict__ P, const d
     // the lane's cells in the compacted map: which start a segment (cells past the grid end
     // count as starts: they end the last real segment) and, for those, the segment's
     // atmosphere cell; the lane's C cells share one bit word (j0 is a multiple of C)
-    // fp32 (kCompact): the compacted map -- the bit word and prefix count are loaded with
-    // the inputs, the dependent loads of the segments' atmosphere cells follow the flux pass,
-    // so they add no round trip before it.  fp64: one 4-B index per cell, loaded with the
-    // inputs (the compacted map measured -2.3 % per fp32 step, -0.4 % at T = 1 fp64 and +1.7 %
-    // at T = 2, in one process over the same arrays: profiles/r05/seg/)
-    constexpr bool kCompact = sizeof(R) == 4;
+    // fp32 and fp64 halo tiles (kCompact): the compacted map -- the bit word and prefix
+    // count are loaded with the inputs, the dependent loads of the segments' atmosphere cells
+    // follow the flux pass, so they add no round trip before it.  fp64 with crossing records:
+    // one 4-B index per cell, loaded with the inputs (the compacted map measured -2.3 % per
+    // fp32 step, -0.4 / -1.1 % at T = 1 fp64 and +1.7 % at T = 2 -- its records' first-cell
+    // load is a fourth dependent one -- in one process over the same arrays: profiles/r05/seg/)
+    constexpr bool kCompact = sizeof(R) == 4 || (HALO && FCX_F64_COMPACT);
     const int sh = (int)(j0 & 31);
     uint32_t word = 0;
     int32_t before = 0;  // kCompact: segments starting before cell j0
