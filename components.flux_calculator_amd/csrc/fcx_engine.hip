@@ -216,10 +216,11 @@ struct fcx_engine {
   std::vector<double> atm_w;
   bool atm_contiguous = true;
   int32_t *d_atm_row = nullptr, *d_atm_col = nullptr, *d_atm_idx = nullptr;
-  // the fused path's map: a 4-B index per cell (d_atm_idx, fp64 launches with crossing
-  // records) and the compacted map (fp32 launches and fp64 halo launches; AtmosFused::seg_*:
-  // [words] start bits, [words + 1] prefix counts, [segments] atmosphere cells, one allocation)
+  // the fused path's maps (which launch reads which: compact_map): a 4-B index per cell
+  // (d_atm_idx) and the compacted map (AtmosFused::seg_*: [words] start bits, [words + 1]
+  // prefix counts, [segments] atmosphere cells, one allocation)
   void *d_atm_seg = nullptr;
+  int32_t *d_atm_tile_a0 = nullptr;  // the compacted map's first cell of every wave tile
   int64_t atm_seg_words = 0, atm_segments = 0;
   std::vector<int32_t> atm_idx;
   // atmosphere cells without exchange cells (land, on a real intersection grid): the fused
@@ -426,6 +427,7 @@ extern "C" int fcx_destroy(fcx_engine *e) {
   (void)hipFree(e->corr_dev);
   (void)hipFree(e->d_atm_row);
   (void)hipFree(e->d_atm_seg);
+  (void)hipFree(e->d_atm_tile_a0);
   (void)hipFree(e->d_atm_idx);
   (void)hipFree(e->d_atm_empty);
   (void)hipFree(e->d_atm_xrec);
@@ -723,7 +725,10 @@ static void plan_fused_atmos(fcx_engine *e, Plan &pl, uint32_t stages, int phase
   // go to atmos_kernel: one lane summing a long segment would hold up its whole wave; the
   // fp32 engine uses atmos_kernel too)
   // (fp32 engine: T = 1 only, the register averages of several types are fp64-only)
-  if (!pl.variant || !(e->f32 ? e->d_atm_seg : (void *)e->d_atm_idx) || e->atm_maxseg > kTile / 2 || e->any_regrid || phase <= 0 ||
+  // (the maps its launches read: compact_map)
+  const bool maps = (!compact_map(e->f32, true) || e->d_atm_seg) && (!compact_map(e->f32, false) || e->d_atm_seg) &&
+                    (compact_map(e->f32, true) || e->d_atm_idx) && (compact_map(e->f32, false) || e->d_atm_idx);
+  if (!pl.variant || !maps || e->atm_maxseg > kTile / 2 || e->any_regrid || phase <= 0 ||
       phase >= 1000 || !e->specialize || (e->f32 && e->T >= 2))
     return;
   const TypeParams &tp = pl.host.type[0];
@@ -768,6 +773,7 @@ static void plan_fused_atmos(fcx_engine *e, Plan &pl, uint32_t stages, int phase
     af.seg_pre = reinterpret_cast<const int32_t *>(af.seg_bits + e->atm_seg_words);
     af.seg_atm = af.seg_pre + e->atm_seg_words + 1;
   }
+  af.tile_a0 = e->d_atm_tile_a0;
   af.idx = e->d_atm_idx;
   af.w = e->d_atm_w;
   af.xrec = e->d_atm_xrec;
@@ -1810,13 +1816,14 @@ extern "C" int fcx_commit(fcx_engine *e) {
     HIP_TRY(hipMalloc(&e->d_atm_w, std::max<size_t>(e->atm_w.size(), 1) * sizeof(double)));
     if (!e->atm_w.empty())
       HIP_TRY(hipMemcpy(e->d_atm_w, e->atm_w.data(), e->atm_w.size() * sizeof(double), hipMemcpyHostToDevice));
-    if (e->atm_contiguous && !e->atm_idx.empty() && !e->f32) {  // fp64: the per-cell index
+    // the per-cell index, where some fp64 launch reads it
+    if (e->atm_contiguous && !e->atm_idx.empty() && !(compact_map(e->f32, true) && compact_map(e->f32, false))) {
       HIP_TRY(hipMalloc(&e->d_atm_idx, e->atm_idx.size() * sizeof(int32_t)));
       HIP_TRY(hipMemcpy(e->d_atm_idx, e->atm_idx.data(), e->atm_idx.size() * sizeof(int32_t),
                         hipMemcpyHostToDevice));
     }
-    // the compacted map: fp32 engines, and fp64 ones for their halo launches
-    if (e->atm_contiguous && !e->atm_idx.empty() && (e->f32 || FCX_F64_COMPACT)) {
+    // the compacted map, where some launch reads it
+    if (e->atm_contiguous && !e->atm_idx.empty() && (compact_map(e->f32, true) || compact_map(e->f32, false))) {
       const int64_t nx = (int64_t)e->atm_idx.size(), nw = (nx + 31) / 32;
       std::vector<uint32_t> seg((size_t)(2 * nw + 1), 0u);  // bits, then prefix counts (int32)
       std::vector<int32_t> atm;
@@ -1837,6 +1844,12 @@ extern "C" int fcx_commit(fcx_engine *e) {
       HIP_TRY(hipMemcpy(e->d_atm_seg, seg.data(), head, hipMemcpyHostToDevice));
       if (!atm.empty())
         HIP_TRY(hipMemcpy((char *)e->d_atm_seg + head, atm.data(), atm.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+      // the first cell's atmosphere cell of every wave tile (the crossing records' entry)
+      const int64_t tc = (int64_t)(e->f32 ? kF32Cpl : 2) * 64, nt = (nx + tc - 1) / tc;
+      std::vector<int32_t> a0((size_t)nt);
+      for (int64_t t = 0; t < nt; ++t) a0[(size_t)t] = e->atm_idx[(size_t)(t * tc)];
+      HIP_TRY(hipMalloc(&e->d_atm_tile_a0, (size_t)std::max<int64_t>(nt, 1) * sizeof(int32_t)));
+      if (nt) HIP_TRY(hipMemcpy(e->d_atm_tile_a0, a0.data(), a0.size() * sizeof(int32_t), hipMemcpyHostToDevice));
     }
     if (e->atm_contiguous && !e->atm_idx.empty()) {  // the fused path's crossing records
       const int64_t tiles = (e->n[0] + kTile - 1) / kTile;
@@ -2011,8 +2024,7 @@ static int copy_bufs(fcx_engine *e, const std::vector<int> &ids, bool h2d, std::
 static int full_range_halo(const fcx_engine *e, const Plan *pl) {
   const int cpl = e->f32 ? kF32Cpl : 2;
   const int h = (e->atm_maxseg - 1 + cpl - 1) / cpl;
-  const bool map = e->f32 || !FCX_F64_COMPACT || e->d_atm_seg;  // (the halo kernels' map)
-  if (e->atm_halo && e->atm_crossings > 0 && map &&
+  if (e->atm_halo && e->atm_crossings > 0 &&
       (pl->host.num_types == 1 || (FCX_HALO_RAVG && pl->host.ravg_on)) && h >= 1 && h <= (cpl == 4 ? 2 : 4))
     return h;
   return 0;
@@ -2912,7 +2924,7 @@ extern "C" int fcx_algorithmic_bytes(fcx_engine *e, int phase, int64_t *bytes) {
       (!e->f32 || e->launch.max_blocks <= 0)) {
     nf = 0;  // fused: the map (compacted, or an index per cell) and a weight per cell, the
              // atmosphere outputs (fluxes not re-read)
-    const bool compact = e->f32 || (FCX_F64_COMPACT && full_range_halo(e, pl) > 0);
+    const bool compact = compact_map(e->f32, full_range_halo(e, pl) > 0);
     extra = e->n[0] * 8 + (compact ? (2 * e->atm_seg_words + 1 + e->atm_segments) * 4 : e->n[0] * 4) +
             (int64_t)pl->atm_nf * e->n_atmos * es;
   } else if (nf && e->n_atmos >= 0 && e->atmos_in_run) {

@@ -36,8 +36,9 @@
 #ifndef FCX_HALO_RAVG
 #define FCX_HALO_RAVG 0
 #endif
-// the compacted exchange -> atmosphere map also for the fp64 halo launches (fp32 always);
-// fp64 launches with crossing records keep the 4-B index per cell (A/B: 0 = index only)
+// the fp64 launches' exchange -> atmosphere map (fp32 launches always read the compacted
+// one): 0 = a 4-B index per cell; 1 = the compacted map in halo launches, the index in
+// launches with crossing records; 2 = the compacted map in every launch
 #ifndef FCX_F64_COMPACT
 #define FCX_F64_COMPACT 1
 #endif
@@ -203,16 +204,22 @@ constexpr int kFusedFields = 6;
 constexpr int kRecHead = 4;     // head products kept per crossing record (longer heads: recomputed)
 constexpr int kXRec = 32;       // doubles per crossing record (256 B, two lines)
 constexpr int kTile = 128;  // cells per wave iteration (64 lanes x 2)
+// the fused launches that read the compacted map (AtmosFused::seg_*) rather than idx
+constexpr bool compact_map(bool f32, bool halo) {
+  return f32 || FCX_F64_COMPACT == 2 || (FCX_F64_COMPACT == 1 && halo);
+}
 struct AtmosFused {
   // the exchange -> atmosphere map of a contiguous (sorted) map, compacted (round 5): bit x of
   // seg_bits[x / 32] is set where exchange cell x starts a segment (its atmosphere cell
   // differs from cell x-1's); seg_pre[w] counts the starts in cells < 32 w; seg_atm[s] is the
   // atmosphere cell of segment s.  1/8 + 1/8 + 4/(cells per segment) bytes per cell instead
-  // of a 4-B index per cell.  The fp32 engines' kernels read this; the fp64 ones read idx.
+  // of a 4-B index per cell.  Which launches read it and which read idx: compact_map().
   const uint32_t *seg_bits;
   const int32_t *seg_pre;
   const int32_t *seg_atm;
-  const int32_t *idx;  // fp64 engines: the local atmosphere cell of every exchange cell
+  const int32_t *tile_a0;  // compacted map: the atmosphere cell of each wave tile's first cell
+                           // (crossing records; a load that depends on nothing)
+  const int32_t *idx;  // the local atmosphere cell of every exchange cell
   const double *w;
   double *out[kFusedFields];
   const double *x[kFusedFields];  // the stored outputs (read by the fix-up only)

@@ -879,18 +879,20 @@ __device__ __forceinline__ void atmos_tile(const Params *__restrict__ P, const d
     // one 4-B index per cell, loaded with the inputs (the compacted map measured -2.3 % per
     // fp32 step, -0.4 / -1.1 % at T = 1 fp64 and +1.7 % at T = 2 -- its records' first-cell
     // load is a fourth dependent one -- in one process over the same arrays: profiles/r05/seg/)
-    constexpr bool kCompact = sizeof(R) == 4 || (HALO && FCX_F64_COMPACT);
+    constexpr bool kCompact = compact_map(sizeof(R) == 4, HALO);
     const int sh = (int)(j0 & 31);
     uint32_t word = 0;
     int32_t before = 0;  // kCompact: segments starting before cell j0
     int32_t a[C];        // atmosphere cell (kCompact: of a segment-start cell only; -1 elsewhere)
 #pragma unroll
     for (int i = 0; i < C; ++i) a[i] = -1;
+    int32_t a0_tile = 0;  // kCompact, crossing records: the tile's first cell's atmosphere cell
     if constexpr (kCompact) {
       if (j0 < n) {
         word = gptr(af.seg_bits)[j0 >> 5];
         before = gptr(af.seg_pre)[j0 >> 5];
       }
+      if (!HALO && af.xrec_on) a0_tile = gptr(af.tile_a0)[tile];
     } else if (j0 + C <= n) {
       const i2v ii = *gptr(reinterpret_cast<const i2v *>(af.idx + j0));
       a[0] = ii.x;
@@ -1056,7 +1058,7 @@ __device__ __forceinline__ void atmos_tile(const Params *__restrict__ P, const d
       if (FCX_DBG_NO_HEAD >= 2) head = 0;
       double *xr0 = af.xrec + tile * kXRec;
       if (lane == 0 && FCX_DBG_NO_HEAD < 2) {  // the tile's first cell: its atmosphere cell
-        const int32_t a0 = (!kCompact || st[0]) ? a[0] : gptr(af.seg_atm)[before - 1];
+        const int32_t a0 = kCompact ? a0_tile : a[0];
         *gptr(reinterpret_cast<i2v *>(xr0 + 30)) = i2v{head, a0};
       }
       if (FCX_DBG_NO_HEAD) head = 0;
