@@ -662,6 +662,10 @@ def main():
             "traffic": traffic,
             "traffic_source": traffic_source,
             "alg_bytes_per_launch": dom_bytes,
+            "alg_bytes_rule": ("every distinct field array read once and written once, the atmosphere outputs, "
+                               "a weight per exchange cell and the exchange->atmosphere map as the launch reads it "
+                               "(halo launches and fp32: start bits, prefix counts and one cell per segment; "
+                               "otherwise a 4-B index per cell; DESIGN.md section 3)"),
             "mean_kernel_ms": round(dom_ms, 4),
             "events": ("one HIP event pair around the timed steps on the launches' stream, mean per step: the "
                        "step's one launch (fcx_run_group: the variants' fused flux passes in one grid) and its "
