@@ -1322,6 +1322,13 @@ static int alloc_tiled(fcx_engine *e) {
   return FCX_OK;
 }
 
+// Host <-> device copies name no direction (hipMemcpyDefault): the runtime then looks the
+// host pointer up and moves page-locked memory by direct DMA, whereas an explicit
+// hipMemcpyDeviceToHost into hipHostMalloc memory took 166 us for 1.8 MB (40 us with
+// hipMemcpyDefault) and ran at half the rate at 256 MiB; uploads are the same either way
+// (components.flux_calculator_amd/bench/dma_probe.hip, profiles/r05/dma2/, ROCm 7.2).
+constexpr hipMemcpyKind kH2D = hipMemcpyDefault, kD2H = hipMemcpyDefault;
+
 // cells [a, z) of a mirror <-> the same cells of its host array.  Tiled: the whole tiles in
 // between as one 2-D copy (rows = tiles), the partial head / tail tiles as 1-D copies.
 static hipError_t copy_cells(const fcx_engine *e, const Buffer &bf, int64_t a, int64_t z, bool h2d,
@@ -1332,8 +1339,7 @@ static hipError_t copy_cells(const fcx_engine *e, const Buffer &bf, int64_t a, i
     char *dev = reinterpret_cast<char *>(bf.dev) + (size_t)tiled(lo, e->tpad) * es;
     char *host = reinterpret_cast<char *>(bf.host) + (size_t)lo * es;
     const size_t bytes = (size_t)(hi - lo) * es;
-    return h2d ? hipMemcpyAsync(dev, host, bytes, hipMemcpyHostToDevice, s)
-               : hipMemcpyAsync(host, dev, bytes, hipMemcpyDeviceToHost, s);
+    return h2d ? hipMemcpyAsync(dev, host, bytes, kH2D, s) : hipMemcpyAsync(host, dev, bytes, kD2H, s);
   };
   if (z <= a) return hipSuccess;
   if (e->tpad == 0) return one(a, z);
@@ -1348,8 +1354,8 @@ static hipError_t copy_cells(const fcx_engine *e, const Buffer &bf, int64_t a, i
   const size_t row = (size_t)kLayoutTile * es, pitch = (size_t)(kLayoutTile + e->tpad) * es;
   char *dev = reinterpret_cast<char *>(bf.dev) + (size_t)t0 * pitch;
   char *host = reinterpret_cast<char *>(bf.host) + (size_t)t0 * row;
-  hipError_t r = h2d ? hipMemcpy2DAsync(dev, pitch, host, row, row, (size_t)(t1 - t0), hipMemcpyHostToDevice, s)
-                     : hipMemcpy2DAsync(host, row, dev, pitch, row, (size_t)(t1 - t0), hipMemcpyDeviceToHost, s);
+  hipError_t r = h2d ? hipMemcpy2DAsync(dev, pitch, host, row, row, (size_t)(t1 - t0), kH2D, s)
+                     : hipMemcpy2DAsync(host, row, dev, pitch, row, (size_t)(t1 - t0), kD2H, s);
   if (r != hipSuccess || z == t1 * kLayoutTile) return r;
   return one(t1 * kLayoutTile, z);
 }
@@ -1537,7 +1543,7 @@ static hipError_t stage_dma(fcx_engine *e, std::vector<Xfer> xs, int64_t a, int6
   std::sort(xs.begin(), xs.end(), [](const Xfer &l, const Xfer &r) {
     return l.sp != r.sp ? l.sp < r.sp : l.soff < r.soff;
   });
-  const hipMemcpyKind kind = h2d ? hipMemcpyHostToDevice : hipMemcpyDeviceToHost;
+  const hipMemcpyKind kind = h2d ? kH2D : kD2H;
   size_t i = 0;
   while (i < xs.size()) {
     const StagePool &p = e->spools[(size_t)xs[i].sp];
@@ -2284,14 +2290,14 @@ extern "C" int fcx_download(fcx_engine *e, int phase) {
 // an atmosphere output mirror -> its host array (2-D copy of the whole tiles when tiled)
 static hipError_t get_atm(const fcx_engine *e, double *host, const double *dev, hipStream_t s) {
   const size_t es = e->esize, n = (size_t)e->n_atmos;
-  if (!e->atm_out_tpad) return hipMemcpyAsync(host, dev, n * es, hipMemcpyDeviceToHost, s);
+  if (!e->atm_out_tpad) return hipMemcpyAsync(host, dev, n * es, kD2H, s);
   const size_t row = (size_t)kLayoutTile * es, pitch = (size_t)(kLayoutTile + e->atm_out_tpad) * es;
   const size_t full = n / kLayoutTile;
   if (full)
-    if (hipError_t r = hipMemcpy2DAsync(host, row, dev, pitch, row, full, hipMemcpyDeviceToHost, s)) return r;
+    if (hipError_t r = hipMemcpy2DAsync(host, row, dev, pitch, row, full, kD2H, s)) return r;
   if (n > full * kLayoutTile)
     return hipMemcpyAsync((char *)host + full * row, (const char *)dev + full * pitch, (n - full * kLayoutTile) * es,
-                          hipMemcpyDeviceToHost, s);
+                          kD2H, s);
   return hipSuccess;
 }
 
@@ -2386,7 +2392,7 @@ static int download_remaps(fcx_engine *e, int phase, hipStream_t s, std::vector<
         if (f.st.sp >= 0)
           xs->push_back(xfer_of(f.st, f.out_host, rm.n_dst));
         else if (!f.external)
-          HIP_TRY(hipMemcpyAsync(f.out_host, f.out_dev, rm.n_dst * e->esize, hipMemcpyDeviceToHost, s));
+          HIP_TRY(hipMemcpyAsync(f.out_host, f.out_dev, rm.n_dst * e->esize, kD2H, s));
       }
   return FCX_OK;
 }
