@@ -789,11 +789,14 @@ def main():
             lk = link_rates(*link_bytes(variants, 32_768, args))
             both = lk["256MiB"]["both_GBps"]
             b_step = lk["step"]["h2d_bytes"] + lk["step"]["d2h_bytes"]
+            both = max(both, lk["step"]["both_GBps"])
             out["baltic_size"]["host_link"] = dict(lk, bound_us=round(b_step / both / 1e3, 1),
                                                    bound_vs_all_cores=round(cp["us_per_step"] / (b_step / both / 1e3), 2),
                                                    rule="bound_us: the step's input bytes up plus output bytes down at "
-                                                        "the rate of both directions at once (256 MiB copies); "
-                                                        "no step from host arrays can be faster")
+                                                        "the best rate of both directions at once (the step's sizes "
+                                                        "or 256 MiB copies); no step from host arrays can be faster "
+                                                        "(the host copies between the caller's arrays and page-locked "
+                                                        "memory come on top)")
     if rank == 0:
         print(json.dumps(out), flush=True)
     if comm is not None:

@@ -42,6 +42,7 @@ def main():
     ap.add_argument("--cells", type=int, default=32_768)
     ap.add_argument("--steps", type=int, default=400)
     ap.add_argument("--mode", action="append", default=[])
+    ap.add_argument("--handover", type=int, default=1, help="0: skip the hand-over comparison")
     a = ap.parse_args()
 
     import torch
@@ -83,8 +84,9 @@ def main():
             e.close()
         out["modes"][name] = res
         print(name, json.dumps(res), flush=True)
-    out["handover"] = handover(n, a.steps)
-    print("handover", json.dumps(out["handover"]), flush=True)
+    if a.handover:
+        out["handover"] = handover(n, a.steps)
+        print("handover", json.dumps(out["handover"]), flush=True)
     print(json.dumps(out), flush=True)
 
 

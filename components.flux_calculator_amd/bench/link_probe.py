@@ -48,23 +48,41 @@ def med_us(f, reps, warm=20):
 def link_rates(b_in, b_out, reps=200):
     """Page-locked host <-> device DMA of b_in bytes up and b_out bytes down, one copy per
     direction: each alone, and both at once on two streams; plus 256 MiB copies (the link's
-    asymptotic rate).  Median microseconds and GB/s."""
+    asymptotic rate).  Median microseconds and GB/s.  The copies are libfcx's: hipMemcpyAsync
+    with hipMemcpyDefault between hipHostMalloc memory and device memory (an explicit
+    device-to-host kind takes a slow path in this ROCm, profiles/r05/dma2/)."""
+    import ctypes
+
     import torch
+
+    # the process's one HIP runtime: torch's own copy (the file torch loaded), else the system's
+    own = os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so")
+    hip = ctypes.CDLL(own if os.path.exists(own) else "libamdhip64.so")
+    hip.hipHostMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t, ctypes.c_uint]
+    hip.hipHostFree.argtypes = [ctypes.c_void_p]
+    hip.hipMemcpyAsync.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]
+    hip_default = 4  # hipMemcpyDefault
+
+    def host_alloc(n):
+        p = ctypes.c_void_p()
+        if hip.hipHostMalloc(ctypes.byref(p), n, 0) != 0:
+            raise RuntimeError("hipHostMalloc failed")
+        return p
 
     dev = torch.device("cuda", 0)
     s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
     out = {}
     for name, bi, bo, r in (("step", b_in, b_out, reps), ("256MiB", 256 << 20, 256 << 20, 10)):
-        hi, ho = torch.empty(bi, dtype=torch.uint8).pin_memory(), torch.empty(bo, dtype=torch.uint8).pin_memory()
+        hi, ho = host_alloc(bi), host_alloc(bo)
         di, do = torch.empty(bi, dtype=torch.uint8, device=dev), torch.empty(bo, dtype=torch.uint8, device=dev)
 
         def up():
-            with torch.cuda.stream(s1):
-                di.copy_(hi, non_blocking=True)
+            if hip.hipMemcpyAsync(di.data_ptr(), hi, bi, hip_default, s1.cuda_stream) != 0:
+                raise RuntimeError("hipMemcpyAsync H2D failed")
 
         def down():
-            with torch.cuda.stream(s2):
-                ho.copy_(do, non_blocking=True)
+            if hip.hipMemcpyAsync(ho, do.data_ptr(), bo, hip_default, s2.cuda_stream) != 0:
+                raise RuntimeError("hipMemcpyAsync D2H failed")
 
         def run(fs):
             def f():
@@ -73,13 +91,18 @@ def link_rates(b_in, b_out, reps=200):
                 s1.synchronize()
                 s2.synchronize()
             return f
+        torch.cuda.synchronize()
         t_in = med_us(run([up]), r, warm=3)
         t_out = med_us(run([down]), r, warm=3)
         t_both = med_us(run([up, down]), r, warm=3)
         out[name] = {"h2d_bytes": bi, "d2h_bytes": bo, "h2d_us": t_in, "d2h_us": t_out, "both_us": t_both,
                      "h2d_GBps": round(bi / t_in / 1e3, 1), "d2h_GBps": round(bo / t_out / 1e3, 1),
                      "both_GBps": round((bi + bo) / t_both / 1e3, 1)}
-        del hi, ho, di, do
+        torch.cuda.synchronize()
+        hip.hipHostFree(hi)
+        hip.hipHostFree(ho)
+        del di, do
+    out["copies"] = "hipMemcpyAsync(hipMemcpyDefault), hipHostMalloc memory <-> device, two non-blocking streams"
     return out
 
 
