@@ -790,13 +790,18 @@ def main():
             both = lk["256MiB"]["both_GBps"]
             b_step = lk["step"]["h2d_bytes"] + lk["step"]["d2h_bytes"]
             both = max(both, lk["step"]["both_GBps"])
+            st = lk["step"]
+            duplex = max(st["h2d_bytes"] / st["h2d_GBps"], st["d2h_bytes"] / st["d2h_GBps"]) / 1e3
             out["baltic_size"]["host_link"] = dict(lk, bound_us=round(b_step / both / 1e3, 1),
                                                    bound_vs_all_cores=round(cp["us_per_step"] / (b_step / both / 1e3), 2),
+                                                   bound_duplex_us=round(duplex, 1),
                                                    rule="bound_us: the step's input bytes up plus output bytes down at "
-                                                        "the best rate of both directions at once (the step's sizes "
-                                                        "or 256 MiB copies); no step from host arrays can be faster "
-                                                        "(the host copies between the caller's arrays and page-locked "
-                                                        "memory come on top)")
+                                                        "the best rate this probe measured for both directions at once "
+                                                        "(the step's sizes or 256 MiB copies); bound_duplex_us: the "
+                                                        "slower direction alone, the floor if the two directions fully "
+                                                        "overlap (the engines' own copies do overlap them in part, "
+                                                        "DESIGN.md section 7); the host copies between the caller's "
+                                                        "arrays and page-locked memory come on top of either")
     if rank == 0:
         print(json.dumps(out), flush=True)
     if comm is not None:

@@ -43,9 +43,14 @@ def main():
     ap.add_argument("--steps", type=int, default=400)
     ap.add_argument("--mode", action="append", default=[])
     ap.add_argument("--handover", type=int, default=1, help="0: skip the hand-over comparison")
+    ap.add_argument("--no-torch", action="store_true",
+                    help="a process without torch, as a Fortran host: libfcx binds the system HIP "
+                         "runtime and every engine creates its own stream")
     a = ap.parse_args()
-
-    import torch
+    if a.no_torch:
+        os.environ["FCX_NO_TORCH"] = "1"
+    else:
+        import torch
     from fcx.basic import PHASE_ALL
     from fcx.engine import Engine
     from fcx.synthetic import build_case, inputs_for_bench
@@ -56,9 +61,14 @@ def main():
     for m in a.mode or MODES:
         name, opts = parse_mode(m)
         cases = [build_case(v, n=n, T=1, bias=True, data=data) for v in VARIANTS]
-        streams = [torch.cuda.Stream() for _ in cases]
-        engines = [Engine(c.lf, 1, c.methods, corrections=c.corrections, stream=s.cuda_stream, options=opts)
+        # own_stream=1: every engine creates its own non-blocking stream (as for a Fortran host)
+        # instead of running on a torch stream
+        own = bool(opts.pop("own_stream", 0)) or a.no_torch
+        streams = [None if own else torch.cuda.Stream().cuda_stream for _ in cases]
+        engines = [Engine(c.lf, 1, c.methods, corrections=c.corrections, stream=s, options=opts)
                    for c, s in zip(cases, streams)]
+        if own:
+            opts["own_stream"] = 1
         res = {"options": opts}
         for v, e in zip(VARIANTS, engines):
             for k in range(50):

@@ -61,6 +61,9 @@ def link_rates(b_in, b_out, reps=200):
     hip.hipHostMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t, ctypes.c_uint]
     hip.hipHostFree.argtypes = [ctypes.c_void_p]
     hip.hipMemcpyAsync.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]
+    hip.hipStreamCreateWithFlags.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint]
+    hip.hipStreamSynchronize.argtypes = [ctypes.c_void_p]
+    hip.hipStreamDestroy.argtypes = [ctypes.c_void_p]
     hip_default = 4  # hipMemcpyDefault
 
     def host_alloc(n):
@@ -70,26 +73,31 @@ def link_rates(b_in, b_out, reps=200):
         return p
 
     dev = torch.device("cuda", 0)
-    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    # two non-blocking streams of the runtime's own, as libfcx's engines create them (torch's
+    # pooled streams may share a hardware queue, which serialises the two directions)
+    s1, s2 = ctypes.c_void_p(), ctypes.c_void_p()
+    for st in (s1, s2):
+        if hip.hipStreamCreateWithFlags(ctypes.byref(st), 1) != 0:
+            raise RuntimeError("hipStreamCreateWithFlags failed")
     out = {}
     for name, bi, bo, r in (("step", b_in, b_out, reps), ("256MiB", 256 << 20, 256 << 20, 10)):
         hi, ho = host_alloc(bi), host_alloc(bo)
         di, do = torch.empty(bi, dtype=torch.uint8, device=dev), torch.empty(bo, dtype=torch.uint8, device=dev)
 
         def up():
-            if hip.hipMemcpyAsync(di.data_ptr(), hi, bi, hip_default, s1.cuda_stream) != 0:
+            if hip.hipMemcpyAsync(di.data_ptr(), hi, bi, hip_default, s1) != 0:
                 raise RuntimeError("hipMemcpyAsync H2D failed")
 
         def down():
-            if hip.hipMemcpyAsync(ho, do.data_ptr(), bo, hip_default, s2.cuda_stream) != 0:
+            if hip.hipMemcpyAsync(ho, do.data_ptr(), bo, hip_default, s2) != 0:
                 raise RuntimeError("hipMemcpyAsync D2H failed")
 
         def run(fs):
             def f():
                 for g in fs:
                     g()
-                s1.synchronize()
-                s2.synchronize()
+                hip.hipStreamSynchronize(s1)
+                hip.hipStreamSynchronize(s2)
             return f
         torch.cuda.synchronize()
         t_in = med_us(run([up]), r, warm=3)
@@ -102,6 +110,8 @@ def link_rates(b_in, b_out, reps=200):
         hip.hipHostFree(hi)
         hip.hipHostFree(ho)
         del di, do
+    hip.hipStreamDestroy(s1)
+    hip.hipStreamDestroy(s2)
     out["copies"] = "hipMemcpyAsync(hipMemcpyDefault), hipHostMalloc memory <-> device, two non-blocking streams"
     return out
 

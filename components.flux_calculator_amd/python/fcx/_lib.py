@@ -121,10 +121,11 @@ def load():
     can be handed to libfcx directly.  The GPU itself is not touched here."""
     global _lib
     if _lib is None:
-        try:
-            import torch  # noqa: F401
-        except ImportError:
-            pass
+        if not os.environ.get("FCX_NO_TORCH"):  # (measurement tools: a torch-free process, as a
+            try:                                 # Fortran host is, binds the system HIP runtime)
+                import torch  # noqa: F401
+            except ImportError:
+                pass
         if not os.path.exists(LIB_PATH):
             raise FcxError(-1, f"{LIB_PATH} is not built (run __graft_entry__.build())")
         lib = ctypes.CDLL(LIB_PATH)
