@@ -1323,10 +1323,10 @@ static int alloc_tiled(fcx_engine *e) {
 }
 
 // Host <-> device copies name no direction (hipMemcpyDefault): the runtime then looks the
-// host pointer up and moves page-locked memory by direct DMA, whereas an explicit
-// hipMemcpyDeviceToHost into hipHostMalloc memory took 166 us for 1.8 MB (40 us with
-// hipMemcpyDefault) and ran at half the rate at 256 MiB; uploads are the same either way
-// (components.flux_calculator_amd/bench/dma_probe.hip, profiles/r05/dma2/, ROCm 7.2).
+// host pointer up and moves page-locked memory by direct DMA, whereas in the system ROCm 7.2
+// runtime an explicit hipMemcpyDeviceToHost into hipHostMalloc memory took 166 us for 1.8 MB
+// (40 us with hipMemcpyDefault) and ran at half the rate at 256 MiB; uploads are the same
+// either way (components.flux_calculator_amd/bench/dma_probe.hip, profiles/r05/dma2/).
 constexpr hipMemcpyKind kH2D = hipMemcpyDefault, kD2H = hipMemcpyDefault;
 
 // cells [a, z) of a mirror <-> the same cells of its host array.  Tiled: the whole tiles in
