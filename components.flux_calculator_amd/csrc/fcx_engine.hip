@@ -1850,12 +1850,15 @@ extern "C" int fcx_commit(fcx_engine *e) {
       HIP_TRY(hipMemcpy(e->d_atm_seg, seg.data(), head, hipMemcpyHostToDevice));
       if (!atm.empty())
         HIP_TRY(hipMemcpy((char *)e->d_atm_seg + head, atm.data(), atm.size() * sizeof(int32_t), hipMemcpyHostToDevice));
-      // the first cell's atmosphere cell of every wave tile (the crossing records' entry)
-      const int64_t tc = (int64_t)(e->f32 ? kF32Cpl : 2) * 64, nt = (nx + tc - 1) / tc;
-      std::vector<int32_t> a0((size_t)nt);
-      for (int64_t t = 0; t < nt; ++t) a0[(size_t)t] = e->atm_idx[(size_t)(t * tc)];
-      HIP_TRY(hipMalloc(&e->d_atm_tile_a0, (size_t)std::max<int64_t>(nt, 1) * sizeof(int32_t)));
-      if (nt) HIP_TRY(hipMemcpy(e->d_atm_tile_a0, a0.data(), a0.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+      // the first cell's atmosphere cell of every wave tile: the crossing records' entry, where
+      // launches with records read the compacted map
+      if (compact_map(e->f32, false)) {
+        const int64_t tc = (int64_t)(e->f32 ? kF32Cpl : 2) * 64, nt = (nx + tc - 1) / tc;
+        std::vector<int32_t> a0((size_t)nt);
+        for (int64_t t = 0; t < nt; ++t) a0[(size_t)t] = e->atm_idx[(size_t)(t * tc)];
+        HIP_TRY(hipMalloc(&e->d_atm_tile_a0, (size_t)std::max<int64_t>(nt, 1) * sizeof(int32_t)));
+        if (nt) HIP_TRY(hipMemcpy(e->d_atm_tile_a0, a0.data(), a0.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+      }
     }
     if (e->atm_contiguous && !e->atm_idx.empty()) {  // the fused path's crossing records
       const int64_t tiles = (e->n[0] + kTile - 1) / kTile;
