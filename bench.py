@@ -786,22 +786,27 @@ def main():
             # the host link's bound: the step's fields must cross it once
             # each way; measured both directions at once on this box
             from link_probe import link_rates
-            lk = link_rates(*link_bytes(variants, 32_768, args))
-            both = lk["256MiB"]["both_GBps"]
-            b_step = lk["step"]["h2d_bytes"] + lk["step"]["d2h_bytes"]
-            both = max(both, lk["step"]["both_GBps"])
-            st = lk["step"]
-            duplex = max(st["h2d_bytes"] / st["h2d_GBps"], st["d2h_bytes"] / st["d2h_GBps"]) / 1e3
-            out["baltic_size"]["host_link"] = dict(lk, bound_us=round(b_step / both / 1e3, 1),
-                                                   bound_vs_all_cores=round(cp["us_per_step"] / (b_step / both / 1e3), 2),
-                                                   bound_duplex_us=round(duplex, 1),
-                                                   rule="bound_us: the step's input bytes up plus output bytes down at "
-                                                        "the best rate this probe measured for both directions at once "
-                                                        "(the step's sizes or 256 MiB copies); bound_duplex_us: the "
-                                                        "slower direction alone, the floor if the two directions fully "
-                                                        "overlap (the engines' own copies do overlap them in part, "
-                                                        "DESIGN.md section 7); the host copies between the caller's "
-                                                        "arrays and page-locked memory come on top of either")
+            try:
+                lk = link_rates(*link_bytes(variants, 32_768, args))
+            except Exception as ex:  # a measurement beside the line: never the line's end
+                out["baltic_size"]["host_link"] = {"error": f"{type(ex).__name__}: {ex}"}
+                lk = None
+            if lk is not None:
+                both = lk["256MiB"]["both_GBps"]
+                b_step = lk["step"]["h2d_bytes"] + lk["step"]["d2h_bytes"]
+                both = max(both, lk["step"]["both_GBps"])
+                st = lk["step"]
+                duplex = max(st["h2d_bytes"] / st["h2d_GBps"], st["d2h_bytes"] / st["d2h_GBps"]) / 1e3
+                out["baltic_size"]["host_link"] = dict(lk, bound_us=round(b_step / both / 1e3, 1),
+                                                       bound_vs_all_cores=round(cp["us_per_step"] / (b_step / both / 1e3), 2),
+                                                       bound_duplex_us=round(duplex, 1),
+                                                       rule="bound_us: the step's input bytes up plus output bytes down at "
+                                                            "the best rate this probe measured for both directions at once "
+                                                            "(the step's sizes or 256 MiB copies); bound_duplex_us: the "
+                                                            "slower direction alone, the floor if the two directions fully "
+                                                            "overlap (the engines' own copies do overlap them in part, "
+                                                            "DESIGN.md section 7); the host copies between the caller's "
+                                                            "arrays and page-locked memory come on top of either")
     if rank == 0:
         print(json.dumps(out), flush=True)
     if comm is not None:
