@@ -182,9 +182,9 @@ __device__ __forceinline__ void uv_grid(const TypeParams &tp, int k, uint32_t st
   if (g.tsur) ts = LD(g.tsur, j0, n);
   if (g.psur) ps = LD(g.psur, j0, n);
   if (do_q) fi = LD(g.fice, j0, n);
-  if (do_m) {
-    u = LD(g.uatm, j0, n);
-    v = LD(g.vatm, j0, n);
+  if (do_m) {  // ('zero' momentum binds no wind: the planner leaves uatm / vatm unset)
+    if (g.uatm) u = LD(g.uatm, j0, n);
+    if (g.vatm) v = LD(g.vatm, j0, n);
     if (tp.m_mom == FCX_CCLM) a = LD(g.amom, j0, n);
     if (tp.m_mom == FCX_MOM5) a = LD(g.cmom, j0, n);
     if (g.qsur_in && !do_q) qs = LD(g.qsur_in, j0, n);

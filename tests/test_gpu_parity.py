@@ -90,6 +90,17 @@ def test_separate_uv_grids(variant):
     assert_parity(fused(case), ref, label=case.name)
 
 
+@pytest.mark.parametrize("T", [1, 3])
+def test_zero_momentum_on_separate_grids(T):
+    """'zero' momentum on separate u/v grids (prepare binds no wind for it): the u/v pass
+    must not read the unbound wind arrays (found by tests/test_gpu_random_configs.py, seed 6:
+    the kernel loaded through a null pointer and faulted)."""
+    case = build_case("MOM5", n=4095, T=T, bias=False, sep_grids=(4097, 4097),
+                      per_type={1: dict(which_flux_momentum="zero")})
+    ref = oracle_lib.run_case(case, "c", current_step_time=STEP_T)
+    assert_parity(fused(case), ref, label=case.name)
+
+
 def test_early_then_normal_phase():
     case = build_case("CCLM", n=1500, T=3, bias=True)
     ref = oracle_lib.run_case(case, "c", current_step_time=STEP_T)
