@@ -60,7 +60,7 @@ def draw_case(seed):
                 two_phases=bool(r.random() < 0.4))
 
 
-def conditioned_parity(spec, got, ref, label, tol=1e-10, ulps=16, trials=2):
+def conditioned_parity(make_case, got, ref, label, tol=1e-10, ulps=16, trials=2, regrid=False):
     """The SURVEY 8d gate (tests/parity.py: |x - ref| <= 1e-10 max(|ref|, 1e-6 |ref|_inf)),
     with one allowance for ill-conditioned cells.  Where a flux cancels -- HSEN = F c_p (T_s -
     T_a EF) with T_s ~ T_a EF, MEVA = F (q_s - q_a) with q_s ~ q_a -- one ulp of a
@@ -73,7 +73,7 @@ def conditioned_parity(spec, got, ref, label, tol=1e-10, ulps=16, trials=2):
     eps = np.finfo(np.float64).eps
     delta = {k: np.zeros(np.shape(v)) for k, v in ref.items()}
     for t in range(trials):
-        c = build_case(**spec)
+        c = make_case()
         outs = {id(c.lf.field[k]) for k in c.outputs}
         r = np.random.default_rng([t, 99])
         seen = set()
@@ -82,7 +82,7 @@ def conditioned_parity(spec, got, ref, label, tol=1e-10, ulps=16, trials=2):
                 continue
             seen.add(id(a))
             a *= 1.0 + ulps * eps * r.choice([-1.0, 1.0], a.shape)
-        rp = oracle_lib.run_case(c, "c", current_step_time=STEP_T)
+        rp = oracle_lib.run_case(c, "c", current_step_time=STEP_T, regrid=regrid)
         for k in ref:
             with np.errstate(invalid="ignore"):
                 d = np.abs(np.asarray(rp[k], dtype=np.float64) - np.asarray(ref[k], dtype=np.float64))
@@ -103,7 +103,7 @@ def conditioned_parity(spec, got, ref, label, tol=1e-10, ulps=16, trials=2):
     assert not bad, f"{label}: " + "; ".join(bad)
 
 
-@pytest.mark.parametrize("seed", range(32))
+@pytest.mark.parametrize("seed", range(64))
 def test_random_configuration(seed):
     spec = draw_case(seed)
     two = spec.pop("two_phases")
@@ -115,7 +115,7 @@ def test_random_configuration(seed):
         eng.step(ph, STEP_T)
     got = {k: np.array(case.lf.field[k], copy=True) for k in case.outputs}
     eng.close()
-    conditioned_parity(spec, got, ref, label=f"seed {seed}: {spec} two_phases={two}")
+    conditioned_parity(lambda: build_case(**spec), got, ref, label=f"seed {seed}: {spec} two_phases={two}")
 
 
 def draw_transport(seed):
@@ -140,7 +140,7 @@ def draw_transport(seed):
     return opts
 
 
-@pytest.mark.parametrize("seed", range(24))
+@pytest.mark.parametrize("seed", range(48))
 def test_random_configuration_and_transport(seed):
     """A random configuration (draw_case) through random transport options: every transport
     and launch shape gives the oracle's results."""
@@ -158,10 +158,10 @@ def test_random_configuration_and_transport(seed):
         eng.step(ph, STEP_T)
     got = {k: np.array(case.lf.field[k], copy=True) for k in case.outputs}
     eng.close()
-    conditioned_parity(spec, got, ref, label=f"seed {seed}: {spec} {opts} two_phases={two}")
+    conditioned_parity(lambda: build_case(**spec), got, ref, label=f"seed {seed}: {spec} {opts} two_phases={two}")
 
 
-@pytest.mark.parametrize("seed", range(16))
+@pytest.mark.parametrize("seed", range(32))
 def test_random_configuration_fp32(seed):
     """The fp32 engine on a random configuration, against the fp64 oracle on the same
     (fp32-rounded) inputs: the norm-wise fp32 gate of tests/parity.py."""
@@ -183,7 +183,7 @@ def test_random_configuration_fp32(seed):
     assert not bad, f"seed {seed}: {spec}: fp32 norm-wise error over {FP32_NORM_GATE}: {bad}"
 
 
-@pytest.mark.parametrize("seed", range(16))
+@pytest.mark.parametrize("seed", range(32))
 def test_random_fused_accumulation(seed):
     """The exchange -> atmosphere accumulation fused into the flux pass, one surface type (the
     fluxes) or two (the type-0 averages), on random run-length maps (0..5 up to 1..400 cells
@@ -226,3 +226,45 @@ def test_random_fused_accumulation(seed):
             np.testing.assert_array_equal(outs[k].cpu().numpy(), want,
                                           err_msg=f"seed {seed}: {variant} T={T} n={n} {lengths} {opts} {k} step {step}")
     eng.close()
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_random_regridding(seed):
+    """do_regridding (basic:463-522) inside the step, on random separate t/u/v grids with all
+    four matrices in use (build_regrid_case: QSUR t->u, t->v; UMOM u->t; VMOM v->t), random
+    method sets, types, bias and phases, against the oracle's staged sequence."""
+    from fcx.synthetic import build_regrid_case
+
+    r = np.random.default_rng([seed, 13])
+    n = int(r.integers(1, 3000))
+    kw = dict(variant=str(r.choice(["CCLM", "MOM5", "RCO"])), n=n,
+              sep_grids=(max(1, n + int(r.integers(-40, 41))), max(1, n + int(r.integers(-40, 41)))),
+              T=int(r.integers(1, 4)), bias=bool(r.random() < 0.5), seed=5000 + seed)
+    two = bool(r.random() < 0.5)
+    case = build_regrid_case(**kw)
+    ref = oracle_lib.run_case(case, "c", current_step_time=STEP_T, regrid=True)
+    eng = Engine(case.lf, case.num_surface_types, case.methods, corrections=case.corrections,
+                 averages=case.averages, regrid=case.regrid)
+    for ph in ((PHASE_EARLY, PHASE_NORMAL) if two else (PHASE_ALL,)):
+        eng.step(ph, STEP_T)
+    got = {k: np.array(case.lf.field[k], copy=True) for k in case.outputs}
+    eng.close()
+    conditioned_parity(lambda: build_regrid_case(**kw), got, ref, label=f"seed {seed}: {kw} two_phases={two}",
+                       regrid=True)
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_random_group_launch(seed):
+    """fcx_run_group over a random member list (1-4 engines, repeats allowed), grid size,
+    precision, surface types and map: every flux and atmosphere value the bits of each
+    engine's own fcx_run (test_gpu_group.run_both)."""
+    from test_gpu_group import run_both, same_bits
+
+    r = np.random.default_rng([seed, 17])
+    variants = tuple(str(v) for v in r.choice(["CCLM", "MOM5", "RCO"], int(r.integers(1, 5))))
+    precision = "f32" if r.random() < 0.4 else "f64"
+    types = 1 if precision == "f32" else int(r.integers(1, 3))
+    n = int(r.integers(1_000, 200_000))
+    opts = {"atmos_halo": 0} if r.random() < 0.3 else None
+    a, b = run_both(n, variants, str(r.choice(["random", "periodic"])), precision, types=types, options=opts)
+    same_bits(a, b)
