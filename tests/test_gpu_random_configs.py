@@ -269,3 +269,56 @@ def test_random_group_launch(seed):
     opts = {"atmos_halo": 0} if r.random() < 0.3 else None
     a, b = run_both(n, variants, str(r.choice(["random", "periodic"])), precision, types=types, options=opts)
     same_bits(a, b)
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_random_sharded_accumulation(seed):
+    """The APPLE-sharded step (decomp_def.F90:23-31) on a random map: 2-6 engines in one
+    process, each its rank's cells, the boundary slots summed as the all-reduce would
+    (fused or separate accumulation).  Every atmosphere cell one rank owns is bit-identical to
+    the sequential sum of the GPU's own fluxes; a cell two ranks share is the sum of their two
+    partial sums, within 4 eps of the sum of the products' magnitudes."""
+    import torch
+    from fcx.parallel import local_atmos
+    from test_gpu_multirank import FIELDS, make_engine, random_run_map, shard_case
+
+    r = np.random.default_rng([seed, 19])
+    n = int(r.integers(2_000, 50_000))
+    world = int(r.integers(2, 7))
+    variant = str(r.choice(["CCLM", "MOM5", "RCO"]))
+    fused = bool(r.random() < 0.7)
+    lengths = [(1, 5), (1, 10), (20, 64), (0, 5)][int(r.integers(0, 4))]
+    full = build_case(variant, n=n, T=1, bias=True, seed=911)
+    amap = random_run_map(n, lengths, seed=6000 + seed)
+    stride = len(FIELDS)
+    engines = []
+    for rank in range(world):
+        la = local_atmos(amap, rank, world)
+        shared = torch.zeros(max(world - 1, 1) * stride, dtype=torch.float64, device="cuda:0")
+        case = shard_case(full, la.offset, la.offset + la.size, variant)
+        eng, outs = make_engine(case, la, shared, stride, fused=fused)
+        engines.append((la, shared, eng, outs, case))
+    for la, shared, eng, outs, case in engines:
+        eng.step(PHASE_ALL, 7200)
+    total = sum(e[1] for e in engines)  # the all-reduce (sum) of the boundary slots
+    for la, shared, eng, outs, case in engines:
+        shared.copy_(total)
+        eng.atmos_finish()
+        eng.synchronize()
+    owner = np.zeros(amap.n_atmos, np.int32)  # ranks holding part of each atmosphere cell
+    got = {name: np.full(amap.n_atmos, np.nan) for name, _ in FIELDS}
+    flux = {name: np.empty(n) for name, _ in FIELDS}
+    for la, shared, eng, outs, case in engines:
+        sl = slice(la.atmos_offset, la.atmos_offset + la.n_atmos)
+        owner[sl] += 1
+        for name, g in FIELDS:
+            got[name][sl] = outs[name].cpu().numpy()[: la.n_atmos]
+            flux[name][la.offset: la.offset + la.size] = np.asarray(case.lf.field[(1, g, name)])
+        eng.close()
+    eps = np.finfo(np.float64).eps
+    for name, _ in FIELDS:
+        want = oracle_lib.atmos_accumulate(amap.atmos_index, amap.weight, flux[name], amap.n_atmos)
+        mag = oracle_lib.atmos_accumulate(amap.atmos_index, np.abs(amap.weight), np.abs(flux[name]), amap.n_atmos)
+        one, two = owner == 1, owner >= 2
+        np.testing.assert_array_equal(got[name][one], want[one], err_msg=f"seed {seed}: {name} (owned cells)")
+        assert np.all(np.abs(got[name][two] - want[two]) <= 4 * eps * mag[two]), f"seed {seed}: {name} shared"
