@@ -322,3 +322,79 @@ def test_random_sharded_accumulation(seed):
         one, two = owner == 1, owner >= 2
         np.testing.assert_array_equal(got[name][one], want[one], err_msg=f"seed {seed}: {name} (owned cells)")
         assert np.all(np.abs(got[name][two] - want[two]) <= 4 * eps * mag[two]), f"seed {seed}: {name} shared"
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_random_per_call_sequence(seed):
+    """The reference subroutines one by one (calc:25-385, in flux_calculator.F90:902-1008's
+    order) through the C ABI on a random configuration: the drop-in's level-0 path."""
+    from fcx import flux_calculator_calculate as fcc
+
+    spec = draw_case(300 + seed)
+    spec.pop("two_phases")
+    case = build_case(**spec)
+    ref = oracle_lib.run_case(case, "c", current_step_time=STEP_T)
+    fcc.prepare(case.lf, 1, case.num_surface_types, case.methods, corrections=case.corrections)
+    m = fcc.methods_2d(case.methods)
+    T, gs, lf = case.num_surface_types, case.grid_size, case.lf
+    fcc.calc_flux_radiation_blackbody(1, T, m["which_flux_radiation_blackbody"], gs, lf)
+    for name, g in (("RBBR", 1), ("TSUR", 1)):
+        fcc.average_across_surface_types(g, name, T, gs, lf)
+    for g, tab in ((1, "which_spec_vapor_surface_t"), (2, "which_spec_vapor_surface_u"),
+                   (3, "which_spec_vapor_surface_v")):
+        fcc.calc_spec_vapor_surface(1, T, g, m[tab], gs, lf)
+    fcc.calc_flux_mass_evap(1, T, m["which_flux_mass_evap"], gs, lf, current_step_time=STEP_T)
+    fcc.calc_flux_heat_latent(1, T, m["which_flux_heat_latent"], gs, lf)
+    fcc.calc_flux_heat_sensible(1, T, m["which_flux_heat_sensible"], gs, lf)
+    fcc.calc_flux_momentum_east(1, T, 2, m["which_flux_momentum"], gs, lf)
+    fcc.calc_flux_momentum_north(1, T, 3, m["which_flux_momentum"], gs, lf)
+    fcc.distribute_shortwave_radiation_flux(1, T, gs, lf)
+    for name, g in (("MEVA", 1), ("HLAT", 1), ("HSEN", 1), ("UMOM", 2), ("VMOM", 3)):
+        fcc.average_across_surface_types(g, name, T, gs, lf)
+    got = {k: np.array(case.lf.field[k], copy=True) for k in case.outputs}
+    fcc.release(lf)
+    conditioned_parity(lambda: build_case(**spec), got, ref, label=f"seed {seed}: {spec} (per call)")
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_random_async_and_hand_over(seed):
+    """fcx_step_async + fcx_synchronize, and fields handed over one by one (fcx_upload_field,
+    a random subset, in random order) before fcx_step, on a random configuration and random
+    transport: the bits of the plain fcx_step, over two steps."""
+    spec = draw_case(400 + seed)
+    spec.pop("two_phases")
+    opts = draw_transport(400 + seed)
+    r = np.random.default_rng([seed, 23])
+    mode = str(r.choice(["async", "hand_over"]))
+
+    def run(special):
+        case = build_case(**spec)
+        outs = {id(case.lf.field[k]) for k in case.outputs}
+        slots, seen = [], set()
+        for key, a in case.lf.field.items():
+            if id(a) not in outs and id(a) not in seen:
+                seen.add(id(a))
+                slots.append(key)
+        eng = Engine(case.lf, case.num_surface_types, case.methods, corrections=case.corrections,
+                     averages=case.averages, options=opts)
+        res = []
+        for step in range(2):
+            for k in case.outputs:
+                case.lf.field[k][:] = np.nan
+            if special and mode == "async":
+                eng.step_async(PHASE_ALL, STEP_T + 3600 * step)
+                eng.synchronize()
+            else:
+                if special:
+                    pick = r.permutation(len(slots))[: int(r.integers(0, len(slots) + 1))]
+                    for i in pick:
+                        eng.upload_field(*slots[i])
+                eng.step(PHASE_ALL, STEP_T + 3600 * step)
+            res.append({k: np.array(case.lf.field[k], copy=True) for k in case.outputs})
+        eng.close()
+        return res
+
+    for a, b in zip(run(False), run(True)):
+        assert a.keys() == b.keys()
+        for k in a:
+            np.testing.assert_array_equal(a[k], b[k], err_msg=f"seed {seed}: {mode} {spec} {opts} {k}")
