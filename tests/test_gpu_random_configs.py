@@ -398,3 +398,43 @@ def test_random_async_and_hand_over(seed):
         assert a.keys() == b.keys()
         for k in a:
             np.testing.assert_array_equal(a[k], b[k], err_msg=f"seed {seed}: {mode} {spec} {opts} {k}")
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_random_remaps(seed):
+    """Exchange -> model remaps (fcx_add_remap) on random model grids,
+    link counts, surface types (type 1 fields, or the type-0 averages at T >= 2), packing
+    and transport: bit-identical to the sequential weight application on the GPU's own
+    fields."""
+    from fcx.parallel import synthetic_model_map
+
+    r = np.random.default_rng([seed, 29])
+    T = int(r.integers(1, 4))
+    n = int(r.integers(10, 60_000))
+    variant = str(r.choice(["CCLM", "MOM5", "RCO"]))
+    case = build_case(variant, n=n, T=T, bias=bool(r.random() < 0.5), seed=7000 + seed)
+    s = 0 if T >= 2 else 1
+    fields = (("MEVA", 1), ("HSEN", 1), ("UMOM", 2), ("VMOM", 3), ("HLAT", 1), ("RBBR", 1))
+    fields = tuple(fields[i] for i in sorted(r.choice(len(fields), int(r.integers(1, 7)), replace=False)))
+    maps, outs = [], []
+    for k in range(int(r.integers(1, 3))):
+        mm = synthetic_model_map(n, int(r.integers(1, max(2, n // 3))), links_per_cell=int(r.integers(1, 3)),
+                                 seed=8000 + 10 * seed + k)
+        oo = {name: np.full(mm.n_model, np.nan) for name, _ in fields}
+        maps.append(mm)
+        outs.append(oo)
+    remaps = [{"n_dst": mm.n_model, "src": mm.src, "dst": mm.dst, "w": mm.weight,
+               "fields": [(1 if name == "RBBR" else 2, s, g, name, oo[name]) for name, g in fields]}
+              for mm, oo in zip(maps, outs)]
+    opts = draw_transport(500 + seed)
+    opts["remap_pack"] = int(r.integers(0, 3))
+    eng = Engine(case.lf, T, case.methods, corrections=case.corrections, averages=case.averages, remaps=remaps,
+                 options=opts)
+    for step in range(2):
+        eng.step(PHASE_ALL, STEP_T + 3600 * step)
+        for mm, oo in zip(maps, outs):
+            for name, g in fields:
+                want = oracle_lib.remap_apply(mm.src, mm.dst, mm.weight, np.asarray(case.lf.field[(s, g, name)]),
+                                              mm.n_model)
+                np.testing.assert_array_equal(oo[name], want, err_msg=f"seed {seed}: {variant} T={T} {opts} {name}")
+    eng.close()
