@@ -438,3 +438,28 @@ def test_random_remaps(seed):
                                               mm.n_model)
                 np.testing.assert_array_equal(oo[name], want, err_msg=f"seed {seed}: {variant} T={T} {opts} {name}")
     eng.close()
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_random_fortran_dropin(seed, tmp_path):
+    """The Fortran drop-in module in a Fortran host (tests/fortran/dropin_host.F90, a process
+    without torch: the system HIP runtime) on a random configuration, each mode of
+    test_fortran.py (per call, fused phases, async phases, fields handed over)."""
+    import os
+    import subprocess
+
+    from test_fortran import DROPIN, write_manifest
+
+    if not os.path.exists(DROPIN):
+        pytest.skip("Fortran drop-in host not built")
+    spec = draw_case(600 + seed)
+    spec.pop("two_phases")
+    mode = ("percall", "fused", "async", "handover")[seed % 4]
+    case = build_case(**spec)
+    outs = write_manifest(case, str(tmp_path), STEP_T)
+    ref = oracle_lib.run_case(case, "c", current_step_time=STEP_T)
+    r = subprocess.run([DROPIN, str(tmp_path), mode], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "DROPIN_HOST OK" in r.stdout, r.stdout + r.stderr
+    got = {key: np.fromfile(os.path.join(tmp_path, f"o{i}.bin"), dtype=np.float64) for i, key in enumerate(outs)}
+    conditioned_parity(lambda: build_case(**spec), got, {k: ref[k] for k in outs},
+                       label=f"seed {seed}: {spec} ({mode})")
