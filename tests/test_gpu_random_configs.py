@@ -463,3 +463,41 @@ def test_random_fortran_dropin(seed, tmp_path):
     got = {key: np.fromfile(os.path.join(tmp_path, f"o{i}.bin"), dtype=np.float64) for i, key in enumerate(outs)}
     conditioned_parity(lambda: build_case(**spec), got, {k: ref[k] for k in outs},
                        label=f"seed {seed}: {spec} ({mode})")
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_random_fused_accumulation_fp32(seed):
+    """The fp32 engine's fused accumulation (4 cells per lane, products and sums in fp64,
+    outputs rounded once) on random maps, sizes and launch options: bit-identical to the
+    sequential fp64 sum of the GPU's own fp32 fluxes, rounded once."""
+    from fcx.parallel import local_atmos
+    from fcx.synthetic import as_dtype
+    from test_gpu_multirank import random_run_map
+
+    r = np.random.default_rng([seed, 31])
+    n = int(r.integers(1, 60_000))
+    lengths = [(1, 5), (1, 9), (1, 10), (40, 64), (1, 400), (0, 5)][int(r.integers(0, 6))]
+    opts = {}
+    if r.random() < 0.4:
+        opts["atmos_halo"] = 0
+    if r.random() < 0.3:
+        opts["max_blocks"] = int(r.choice([1, 16, 64]))
+    if r.random() < 0.3:
+        opts.update(pipeline_chunks=4, pipeline_min_chunk=4096, zero_copy=0)
+    variant = str(r.choice(["CCLM", "MOM5", "RCO"]))
+    c32 = as_dtype(build_case(variant, n=n, T=1, bias=bool(r.random() < 0.5), seed=9000 + seed), "float32")
+    amap = random_run_map(n, lengths, seed=9500 + seed)
+    la = local_atmos(amap, 0, 1)
+    fields = (("MEVA", 1), ("HLAT", 1), ("HSEN", 1), ("RBBR", 1), ("UMOM", 2), ("VMOM", 3))
+    outs = {k: np.full(la.n_atmos, np.nan, np.float32) for k, _ in fields}
+    eng = Engine(c32.lf, 1, c32.methods, corrections=c32.corrections,
+                 atmos={"local": la, "fields": [(2, 1, g, k, outs[k]) for k, g in fields]}, options=opts)
+    for step in range(2):
+        for o in outs.values():
+            o[:] = np.nan
+        eng.step(PHASE_ALL, STEP_T + 3600 * step)
+        for k, g in fields:
+            flux = np.asarray(c32.lf.field[(1, g, k)], dtype=np.float64)
+            want = oracle_lib.atmos_accumulate(amap.atmos_index, amap.weight, flux, amap.n_atmos).astype(np.float32)
+            np.testing.assert_array_equal(outs[k], want, err_msg=f"seed {seed}: {variant} n={n} {lengths} {opts} {k}")
+    eng.close()
