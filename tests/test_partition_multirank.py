@@ -347,3 +347,61 @@ def test_structured_maps_take_the_boundary_slot_rule(mapcls):
             a = mk.local(off, size, rank, p, n, ranges=ranges)
             b = local_atmos(g, rank, p, ranges=ranges)
             assert (a.left, a.right, a.n_atmos, a.atmos_offset) == (b.left, b.right, b.n_atmos, b.atmos_offset)
+
+
+def _random_run_map(n, lengths, rng):
+    """A sorted exchange -> atmosphere map with runs of `lengths` cells (0: atmosphere cells
+    no exchange cell maps to), normalised weights."""
+    from fcx.parallel import AtmosMap
+
+    runs = rng.integers(lengths[0], lengths[1] + 1, n + 1)
+    ends = np.cumsum(runs)
+    n_atmos = int(np.searchsorted(ends, n, side="left")) + 1
+    idx = np.repeat(np.arange(n_atmos, dtype=np.int32), runs[:n_atmos])[:n]
+    area = rng.uniform(0.5, 1.5, n)
+    w = area / np.maximum(np.bincount(idx, weights=area, minlength=n_atmos)[idx], 1e-300)
+    return AtmosMap(np.ascontiguousarray(idx), np.ascontiguousarray(w), n_atmos)
+
+
+@pytest.mark.parametrize("seed", range(40))
+def test_random_partitions_complete_every_cell(seed):
+    """Random maps (runs of 0..5 up to 1..300 cells), 1-16 ranks, APPLE ranges or random task
+    ranges with empty ranks anywhere: every rank's partial sums plus ONE sum over the ranks of
+    the packed boundary slots (what the all-reduce does) complete every atmosphere cell of
+    every rank, equal to the global sequential sum (exactly for the cells one rank owns)."""
+    rng = np.random.default_rng([seed, 41])
+    n = int(rng.integers(1, 5_000))
+    lengths = [(0, 5), (1, 5), (1, 10), (20, 64), (1, 300)][int(rng.integers(0, 5))]
+    amap = _random_run_map(n, lengths, rng)
+    p = int(rng.integers(1, 17))
+    if rng.random() < 0.5:
+        ranges = None  # APPLE (decomp_def.F90:23-31)
+    else:  # a task vector's ranges: sorted cuts, empty ranks allowed (io:101-104)
+        cuts = np.sort(rng.integers(0, n + 1, p - 1))
+        b = np.concatenate([[0], cuts, [n]])
+        ranges = [(int(b[r]), int(b[r + 1] - b[r])) for r in range(p)]
+    x = rng.normal(size=n)
+    want = oracle_lib.atmos_accumulate(amap.atmos_index, amap.weight, x, amap.n_atmos)
+    views = [local_atmos(amap, r, p, ranges=ranges) for r in range(p)]
+    total = np.zeros((max(p - 1, 1), 1))
+    parts = []
+    for la in views:
+        part = oracle_lib.atmos_accumulate(la.atmos_index, la.weight, x[la.offset: la.offset + la.size], la.n_atmos)
+        parts.append(part)
+        if p > 1:
+            total += pack_boundaries(la, [part], 1)
+    owners = np.zeros(amap.n_atmos, np.int32)
+    for la, part in zip(views, parts):
+        if p > 1:
+            unpack_boundaries(la, total, [part])
+        sl = slice(la.atmos_offset, la.atmos_offset + la.n_atmos)
+        owners[sl] += 1
+        np.testing.assert_allclose(part, want[sl], rtol=1e-12, atol=1e-12, err_msg=f"seed {seed} rank view {la}")
+    # every atmosphere cell some rank maps to is covered; a cell of one rank is exact
+    covered = np.zeros(amap.n_atmos, bool)
+    covered[np.unique(amap.atmos_index)] = True
+    assert np.all(owners[covered] >= 1), f"seed {seed}: atmosphere cells no rank completes"
+    for la, part in zip(views, parts):
+        sl = np.arange(la.atmos_offset, la.atmos_offset + la.n_atmos)
+        one = owners[sl] == 1
+        np.testing.assert_array_equal(part[one], want[sl][one], err_msg=f"seed {seed}")
