@@ -64,12 +64,20 @@ def link_rates(b_in, b_out, reps=200):
     hip.hipStreamCreateWithFlags.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint]
     hip.hipStreamSynchronize.argtypes = [ctypes.c_void_p]
     hip.hipStreamDestroy.argtypes = [ctypes.c_void_p]
+    hip.hipMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t]
+    hip.hipFree.argtypes = [ctypes.c_void_p]
     hip_default = 4  # hipMemcpyDefault
 
     def host_alloc(n):
         p = ctypes.c_void_p()
         if hip.hipHostMalloc(ctypes.byref(p), n, 0) != 0:
             raise RuntimeError("hipHostMalloc failed")
+        return p
+
+    def dev_alloc(n):  # plain hipMalloc, as libfcx's pools (not torch's caching allocator)
+        p = ctypes.c_void_p()
+        if hip.hipMalloc(ctypes.byref(p), n) != 0:
+            raise RuntimeError("hipMalloc failed")
         return p
 
     dev = torch.device("cuda", 0)
@@ -82,14 +90,14 @@ def link_rates(b_in, b_out, reps=200):
     out = {}
     for name, bi, bo, r in (("step", b_in, b_out, reps), ("256MiB", 256 << 20, 256 << 20, 10)):
         hi, ho = host_alloc(bi), host_alloc(bo)
-        di, do = torch.empty(bi, dtype=torch.uint8, device=dev), torch.empty(bo, dtype=torch.uint8, device=dev)
+        di, do = dev_alloc(bi), dev_alloc(bo)
 
         def up():
-            if hip.hipMemcpyAsync(di.data_ptr(), hi, bi, hip_default, s1) != 0:
+            if hip.hipMemcpyAsync(di, hi, bi, hip_default, s1) != 0:
                 raise RuntimeError("hipMemcpyAsync H2D failed")
 
         def down():
-            if hip.hipMemcpyAsync(ho, do.data_ptr(), bo, hip_default, s2) != 0:
+            if hip.hipMemcpyAsync(ho, do, bo, hip_default, s2) != 0:
                 raise RuntimeError("hipMemcpyAsync D2H failed")
 
         def run(fs):
@@ -109,10 +117,11 @@ def link_rates(b_in, b_out, reps=200):
         torch.cuda.synchronize()
         hip.hipHostFree(hi)
         hip.hipHostFree(ho)
-        del di, do
+        hip.hipFree(di)
+        hip.hipFree(do)
     hip.hipStreamDestroy(s1)
     hip.hipStreamDestroy(s2)
-    out["copies"] = "hipMemcpyAsync(hipMemcpyDefault), hipHostMalloc memory <-> device, two non-blocking streams"
+    out["copies"] = "hipMemcpyAsync(hipMemcpyDefault), hipHostMalloc memory <-> hipMalloc memory, two non-blocking streams"
     return out
 
 
