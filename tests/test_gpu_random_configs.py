@@ -501,3 +501,45 @@ def test_random_fused_accumulation_fp32(seed):
             want = oracle_lib.atmos_accumulate(amap.atmos_index, amap.weight, flux, amap.n_atmos).astype(np.float32)
             np.testing.assert_array_equal(outs[k], want, err_msg=f"seed {seed}: {variant} n={n} {lengths} {opts} {k}")
     eng.close()
+
+
+def draw_case_with_none(seed):
+    """draw_case with 'none' methods (the flux not computed for that type, its array not
+    allocated, prepare:36-42) for the independent fluxes: HSEN, momentum, RBBR, and MEVA with
+    HLAT (HLAT water / ice needs its type's MEVA)."""
+    spec = draw_case(seed)
+    r = np.random.default_rng([seed, 43])
+    per_type = dict(spec["per_type"] or {})
+    for s in range(1, spec["T"] + 1):
+        m = dict(per_type.get(s, {}))
+        for table in ("which_flux_heat_sensible", "which_flux_momentum", "which_flux_radiation_blackbody"):
+            if r.random() < 0.25:
+                m[table] = "none"
+        if r.random() < 0.2:
+            m["which_flux_mass_evap"] = "none"
+            m["which_flux_heat_latent"] = str(r.choice(["none", "zero"]))
+        per_type[s] = m
+    # 'copy' aliases the first type's array: none there, none here (prepare:36-38)
+    first = per_type.get(1, {})
+    for s in range(2, spec["T"] + 1):
+        for table, method in list(per_type[s].items()):
+            if method == "copy" and first.get(table) == "none":
+                per_type[s][table] = "none"
+    spec["per_type"] = per_type
+    return spec
+
+
+@pytest.mark.parametrize("seed", range(32))
+def test_random_configuration_with_none(seed):
+    """Random configurations in which some fluxes of some types are not computed at all."""
+    spec = draw_case_with_none(700 + seed)
+    two = spec.pop("two_phases")
+    case = build_case(**spec)
+    ref = oracle_lib.run_case(case, "c", current_step_time=STEP_T)
+    eng = Engine(case.lf, case.num_surface_types, case.methods, corrections=case.corrections,
+                 averages=case.averages, regrid=case.regrid, options=draw_transport(700 + seed))
+    for ph in ((PHASE_EARLY, PHASE_NORMAL) if two else (PHASE_ALL,)):
+        eng.step(ph, STEP_T)
+    got = {k: np.array(case.lf.field[k], copy=True) for k in case.outputs}
+    eng.close()
+    conditioned_parity(lambda: build_case(**spec), got, ref, label=f"seed {seed}: {spec} two_phases={two}")
