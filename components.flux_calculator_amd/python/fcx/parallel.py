@@ -303,6 +303,10 @@ def synthetic_model_map(n_exchange, n_model, links_per_cell=1, seed=20231016):
     links_per_cell=2 adds a second, distance-weighted link per exchange cell (the two weights
     summing to the conservative one), as a non-conservative remap has; links in a shuffled
     file order."""
+    if links_per_cell not in (1, 2):
+        raise ValueError(f"links_per_cell must be 1 or 2, got {links_per_cell}")
+    if n_model < links_per_cell:
+        raise ValueError(f"{links_per_cell} links per exchange cell need as many model cells, got {n_model}")
     rng = np.random.Generator(np.random.PCG64([seed, 7]))
     lengths = rng.integers(1, 9, n_exchange // 4 + 2)
     lengths = lengths[: int(np.searchsorted(np.cumsum(lengths), n_exchange)) + 1]
