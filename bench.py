@@ -21,7 +21,8 @@ Also reported:
                 the C restatement oracle/fco.c, kind "port", where it was not built) on one
                 core and on the box's CPU share as APPLE-range ranks, at 32,768 cells
                 (configs 1/2) and at this workload's size, on the same inputs
-  baltic_size   the drop-in from host arrays (e2e) against those host cores at 32,768 cells
+  baltic_size   the drop-in from host arrays (e2e) against those host cores at 32,768 cells,
+                from caller heap arrays and from fcx_host_malloc arrays
 """
 import argparse
 import json
@@ -332,6 +333,54 @@ def e2e_async(args, variants, n=32_768, steps=500):
             "transport": "staging arena + DMA (FCX_OPT_ZERO_COPY 0)",
             "rule": "fcx_step_async of every variant's engine (own stream) from one host thread, then fcx_synchronize "
                     "of each; a step = first start to the last engine synchronised"}
+
+
+def e2e_library_memory(args, variants, n=32_768, steps=500):
+    """The Baltic-size step with the fields in fcx_host_malloc memory -- a host that allocates
+    its local_field arrays from the library (c_f_pointer) instead of
+    its own heap: the default transport then reads and writes them in place over the link
+    (zero-copy), with no host copies and no DMA calls.  Median wall time per step of the
+    variants one after the other (fcx_step) and started together (fcx_step_async from one
+    thread, each engine on its own stream, then fcx_synchronize of each)."""
+    import torch
+    from fcx.basic import PHASE_ALL
+    from fcx.engine import Engine
+    from fcx.host_alloc import Arena
+    from fcx.synthetic import build_case, inputs_for_bench
+
+    data = inputs_for_bench(n)
+    streams = [torch.cuda.Stream() for _ in variants]
+    cases = [build_case(v, n=n, T=args.types, bias=args.bias, data=data if args.types == 1 else None)
+             for v in variants]
+    res = {}
+    with Arena() as arena:
+        for c in cases:
+            arena.adopt(c.lf)
+        engines = [Engine(c.lf, c.num_surface_types, c.methods, corrections=c.corrections, averages=c.averages,
+                          stream=st.cuda_stream) for c, st in zip(cases, streams)]
+        for mode in ("sequential", "async"):
+            ts = []
+            for k in range(50 + steps):
+                t0 = time.perf_counter()
+                if mode == "sequential":
+                    for e in engines:
+                        e.step(PHASE_ALL, k * 3600)
+                else:
+                    for e in engines:
+                        e.step_async(PHASE_ALL, k * 3600)
+                    for e in engines:
+                        e.synchronize()
+                if k >= 50:
+                    ts.append(time.perf_counter() - t0)
+            res[f"{mode}_us_per_step_median"] = round(float(np.median(ts)) * 1e6, 1)
+            res[f"{mode}_us_per_step_p90"] = round(float(np.percentile(ts, 90)) * 1e6, 1)
+        for e in engines:
+            e.close()
+    res.update(steps=steps, engines=len(cases), transport="fcx_host_malloc arrays, default options (zero-copy "
+               "in place at this size)", rule="sequential: fcx_step of each variant in turn; async: fcx_step_async "
+               "of each from one host thread, then fcx_synchronize of each; a step = first start to the last "
+               "engine done")
+    return res
 
 
 def link_bytes(variants, n, args):
@@ -783,6 +832,10 @@ def main():
             asy = e2e_async(args, variants)
             out["baltic_size"]["gpu_dropin_async"] = asy
             out["baltic_size"]["gpu_async_vs_all_cores"] = round(cp["us_per_step"] / asy["us_per_step_median"], 2)
+            lib = e2e_library_memory(args, variants)
+            out["baltic_size"]["gpu_dropin_library_memory"] = lib
+            out["baltic_size"]["gpu_library_memory_vs_all_cores"] = round(
+                cp["us_per_step"] / min(lib["sequential_us_per_step_median"], lib["async_us_per_step_median"]), 2)
             # the host link's bound: the step's fields must cross it once
             # each way; measured both directions at once on this box
             from link_probe import link_rates

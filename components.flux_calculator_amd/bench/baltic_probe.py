@@ -43,6 +43,9 @@ def main():
     ap.add_argument("--steps", type=int, default=400)
     ap.add_argument("--mode", action="append", default=[])
     ap.add_argument("--handover", type=int, default=1, help="0: skip the hand-over comparison")
+    ap.add_argument("--host-malloc", action="store_true",
+                    help="the fields in fcx_host_malloc memory (a Fortran host's c_f_pointer arrays, "
+                         "INTEGRATION.md) instead of caller heap arrays")
     ap.add_argument("--no-torch", action="store_true",
                     help="a process without torch, as a Fortran host: libfcx binds the system HIP "
                          "runtime and every engine creates its own stream")
@@ -53,14 +56,19 @@ def main():
         import torch
     from fcx.basic import PHASE_ALL
     from fcx.engine import Engine
+    from fcx.host_alloc import Arena
     from fcx.synthetic import build_case, inputs_for_bench
 
     n = a.cells
     data = inputs_for_bench(n)
-    out = {"cells": n, "steps": a.steps, "modes": {}}
+    out = {"cells": n, "steps": a.steps, "host_malloc": a.host_malloc, "modes": {}}
     for m in a.mode or MODES:
         name, opts = parse_mode(m)
         cases = [build_case(v, n=n, T=1, bias=True, data=data) for v in VARIANTS]
+        arena = Arena() if a.host_malloc else None
+        if arena:
+            for c in cases:
+                arena.adopt(c.lf)
         # own_stream=1: every engine creates its own non-blocking stream (as for a Fortran host)
         # instead of running on a torch stream
         own = bool(opts.pop("own_stream", 0)) or a.no_torch
@@ -92,6 +100,8 @@ def main():
         res["async_three_us"] = round(float(np.median(ts)) * 1e6, 1)
         for e in engines:
             e.close()
+        if arena:
+            arena.close()
         out["modes"][name] = res
         print(name, json.dumps(res), flush=True)
     if a.handover:
