@@ -403,6 +403,70 @@ def test_step_async_engines_started_from_one_thread(n):
         same_bits(g, w)
 
 
+def test_step_async_engines_on_library_memory():
+    """The Baltic-size step bench.py reports as baltic_size.gpu_dropin_library_memory: the
+    three variants' fields in fcx_host_malloc memory (read and written in place, zero-copy),
+    started with fcx_step_async from one thread on their own streams, then a second step on
+    changed inputs, asynchronous and again with fcx_step one engine after the other -- the
+    bits of the synchronous step on caller heap arrays every time.  (fcx_host_malloc inputs
+    are read in place until fcx_synchronize, so the host leaves them alone until then.)"""
+    import torch
+    from fcx.host_alloc import Arena
+
+    n = 32_768
+    variants = ("CCLM", "MOM5", "RCO")
+
+    def make():
+        return [build_case(v, n=n, T=1, bias=True, seed=30 + i) for i, v in enumerate(variants)]
+
+    def scale_inputs(c):  # every distinct input array once (aliases share it)
+        outs = {id(c.lf.field[k]) for k in c.outputs}
+        for a in {id(a): a for a in c.lf.field.values() if id(a) not in outs}.values():
+            a *= 1.001
+
+    def outputs(c):
+        return {k: np.array(c.lf.field[k], copy=True) for k in c.outputs}
+
+    want = [[], []]
+    for c in make():  # the reference: caller heap arrays, synchronous steps
+        e = Engine(c.lf, 1, c.methods, corrections=c.corrections)
+        e.step(PHASE_ALL, STEP_T)
+        want[0].append(outputs(c))
+        scale_inputs(c)
+        e.step(PHASE_ALL, STEP_T + 3600)
+        want[1].append(outputs(c))
+        e.close()
+    cases = make()
+    with Arena() as arena:
+        for c in cases:
+            arena.adopt(c.lf)
+            for k in c.outputs:
+                c.lf.field[k][:] = np.nan
+        streams = [torch.cuda.Stream() for _ in cases]
+        engines = [Engine(c.lf, 1, c.methods, corrections=c.corrections, stream=s.cuda_stream)
+                   for c, s in zip(cases, streams)]
+        assert all(e.staging_bytes() == 0 for e in engines)  # used in place: no staging arena
+        for step, t in enumerate((STEP_T, STEP_T + 3600)):
+            if step:
+                for c in cases:
+                    scale_inputs(c)
+            for e in engines:
+                e.step_async(PHASE_ALL, t)
+            for e in engines:
+                e.synchronize()
+            for c, w in zip(cases, want[step]):
+                same_bits(outputs(c), w)
+        for c in cases:
+            for k in c.outputs:
+                c.lf.field[k][:] = np.nan
+        for e in engines:
+            e.step(PHASE_ALL, STEP_T + 3600)
+        for c, w in zip(cases, want[1]):
+            same_bits(outputs(c), w)
+        for e in engines:
+            e.close()
+
+
 @pytest.mark.parametrize("n", [32_768, 600_001])
 @pytest.mark.parametrize("variant", ["CCLM", "MOM5"])
 def test_fields_handed_over_one_by_one(variant, n):
