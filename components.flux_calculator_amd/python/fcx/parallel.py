@@ -69,6 +69,8 @@ def synthetic_atmos_map(n_exchange, cells_per_atmos=4, seed=20231015):
     exchange cells ordered by atmosphere cell, weights = exchange area / atmosphere area."""
     rng = np.random.Generator(np.random.PCG64([seed, 99]))
     lengths = rng.integers(cells_per_atmos - 1, cells_per_atmos + 2, n_exchange // max(cells_per_atmos - 1, 1) + 2)
+    while lengths.sum() < n_exchange:  # (only with runs that may be empty: cells_per_atmos 1)
+        lengths = np.concatenate([lengths, rng.integers(cells_per_atmos - 1, cells_per_atmos + 2, n_exchange + 2)])
     ends = np.cumsum(lengths)
     n_atmos = int(np.searchsorted(ends, n_exchange, side="left")) + 1
     idx = np.repeat(np.arange(n_atmos, dtype=np.int32), lengths[:n_atmos])[:n_exchange]
@@ -309,6 +311,8 @@ def synthetic_model_map(n_exchange, n_model, links_per_cell=1, seed=20231016):
         raise ValueError(f"{links_per_cell} links per exchange cell need as many model cells, got {n_model}")
     rng = np.random.Generator(np.random.PCG64([seed, 7]))
     lengths = rng.integers(1, 9, n_exchange // 4 + 2)
+    while lengths.sum() < n_exchange:  # (short draws on small grids: more runs until they cover it)
+        lengths = np.concatenate([lengths, rng.integers(1, 9, n_exchange // 4 + 2)])
     lengths = lengths[: int(np.searchsorted(np.cumsum(lengths), n_exchange)) + 1]
     owner = np.repeat(rng.integers(0, n_model, lengths.size), lengths)[:n_exchange]
     area = rng.uniform(0.5, 1.5, n_exchange)

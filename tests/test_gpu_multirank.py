@@ -71,6 +71,8 @@ def random_run_map(n, lengths, seed):
 
     rng = np.random.default_rng(seed)
     runs = rng.integers(lengths[0], lengths[1] + 1, n)
+    while runs.sum() < n:  # (ranges with empty runs can fall short of n cells)
+        runs = np.concatenate([runs, rng.integers(lengths[0], lengths[1] + 1, n)])
     ends = np.cumsum(runs)
     n_atmos = int(np.searchsorted(ends, n, side="left")) + 1
     idx = np.repeat(np.arange(n_atmos, dtype=np.int32), runs[:n_atmos])[:n]

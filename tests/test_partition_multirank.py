@@ -355,6 +355,8 @@ def _random_run_map(n, lengths, rng):
     from fcx.parallel import AtmosMap
 
     runs = rng.integers(lengths[0], lengths[1] + 1, n + 1)
+    while runs.sum() < n:  # (ranges with empty runs can fall short of n cells)
+        runs = np.concatenate([runs, rng.integers(lengths[0], lengths[1] + 1, n + 1)])
     ends = np.cumsum(runs)
     n_atmos = int(np.searchsorted(ends, n, side="left")) + 1
     idx = np.repeat(np.arange(n_atmos, dtype=np.int32), runs[:n_atmos])[:n]
@@ -405,3 +407,31 @@ def test_random_partitions_complete_every_cell(seed):
         sl = np.arange(la.atmos_offset, la.atmos_offset + la.n_atmos)
         one = owners[sl] == 1
         np.testing.assert_array_equal(part[one], want[sl][one], err_msg=f"seed {seed}")
+
+
+def test_synthetic_maps_cover_every_exchange_cell():
+    """The synthetic exchange -> atmosphere and exchange -> model maps give every exchange
+    cell a link (a remap draw of 48 exchange cells, 3 model cells and 2 links per cell once
+    drew runs covering fewer cells than the grid: seed base 450000 of the random remap test),
+    and 2 links per cell need 2 model cells."""
+    from fcx.parallel import synthetic_atmos_map, synthetic_model_map
+
+    for n in list(range(1, 130)) + [4095, 4097]:
+        for seed in range(3):
+            m = 2 + seed
+            one = synthetic_model_map(n, m, links_per_cell=1, seed=seed)
+            two = synthetic_model_map(n, m, links_per_cell=2, seed=seed)
+            for mm, links in ((one, 1), (two, 2)):
+                assert mm.src.size == links * n and np.array_equal(np.unique(mm.src), np.arange(n))
+            # conservative: the weights of a model cell's exchange cells sum to 1; the second
+            # link splits each cell's weight, so the total stays the number of owner cells
+            np.testing.assert_allclose(one.weight.sum(), np.unique(one.dst).size, rtol=1e-12)
+            np.testing.assert_allclose(two.weight.sum(), one.weight.sum(), rtol=1e-12)
+            for cpa in (1, 4):
+                am = synthetic_atmos_map(n, cells_per_atmos=cpa, seed=seed)
+                assert am.atmos_index.size == n and np.all(np.diff(am.atmos_index) >= 0)
+    mm = synthetic_model_map(48, 3, links_per_cell=2, seed=4508101)
+    assert mm.src.size == 96
+    with pytest.raises(ValueError):
+        synthetic_model_map(10, 1, links_per_cell=2)
+
