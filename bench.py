@@ -95,11 +95,6 @@ def parse():
                    help="1: every step runs the variants' engines through fcx_run_group, their fused flux "
                         "passes as ONE launch (one event pair around the timed steps); 0: one launch "
                         "per engine")
-    p.add_argument("--overlap", type=int, default=0,
-                   help="N > 1 with the libfcx communicator and --group 1: 1 = the step is "
-                        "fcx_run_group_exchange (the boundary tiles and the all-reduce beside the main launch); "
-                        "0 (default) = fcx_run_group, then fcx_atmos_allreduce on the same stream -- the split's "
-                        "two cross-stream edges cost more than a small all-reduce hides (DESIGN.md section 6)")
     p.add_argument("--kernel-events", choices=("dominant", "all"), default="dominant",
                    help="HIP event pairs inside the timed steps: around the dominant engine's launch only "
                         "(picked in an event-timed warm-up block), or around every engine's")
@@ -427,16 +422,7 @@ def measure(wl, args, world, dist, comm, steps, warmup, t_base=0, cold=False):
     stream = wl.stream
     group = bool(args.group)
 
-    overlap = bool(args.overlap) and hasattr(comm, "run_group_exchange")
-
     def step(t, events=None, grouped=group):
-        if grouped and overlap:  # the variants' flux passes + the one collective, overlapped
-            if events is not None:
-                events[0].record(stream)
-            comm.run_group_exchange(wl.engines, t)
-            if events is not None:
-                events[1].record(stream)
-            return
         if grouped:  # fcx_run_group: the variants' flux passes as one launch
             wl.run_group(t, events)
         else:
@@ -648,8 +634,6 @@ def main():
             traffic = None
 
     mg = multi_gpu_check(wl, world, rank, dist) if la is not None else None
-    if mg is not None and comm is not None and hasattr(comm, "overlapped"):
-        mg["exchanges_overlapped"] = comm.overlapped()  # fcx_run_group_exchange steps that split
 
     out = {
         "metric": METRIC,
@@ -692,8 +676,6 @@ def main():
             "atmos_accumulation": (f"6 fluxes -> {la.n_atmos} atmosphere cells per GPU (1 per ~4 "
                                    f"exchange cells, {args.atmos_map} runs), one all-reduce of the shared "
                                    "boundary cells per step"
-                                   + (", overlapped with the main launch (fcx_run_group_exchange)"
-                                      if comm is not None and args.overlap and args.group else "")
                                    + ((" (libfcx RCCL communicator" + (", FCX_RCCL_LIBRARY stand-in)"
                                                                          if os.environ.get("FCX_RCCL_LIBRARY") else ")"))
                                       if comm is not None else

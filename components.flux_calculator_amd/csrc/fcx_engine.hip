@@ -18,7 +18,6 @@
 #include <cstdlib>
 #include <cstring>
 #include <deque>
-#include <functional>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -308,6 +307,9 @@ struct fcx_engine {
   bool tiled_opt = true;
   int64_t tpad = 0;
   std::vector<void *> tiled_pools;  // the pools of a tiled engine (alloc_tiled)
+  // fcx_plan_check: plans built on the host only (no device memory; bound buffers without a
+  // mirror yet stand in with a non-null tag address), audited, and dropped
+  bool plan_dry = false;
 
   fcx_engine() {
     for (auto &a : slot)
@@ -906,6 +908,129 @@ static int ravg_slot(const fcx_engine *e, const Params &P, uint32_t stages, int 
   return slot;
 }
 
+// Plan audit (the 'zero'-momentum fault loaded a wind the planner had left
+// unbound).  The kernels guard every load by its own pointer, so an unbound input reads
+// nothing; this check, run on every plan before its first launch, names the case where a
+// method the plan computes would need an input the planner did not bind -- the predicates of
+// process() / uv_grid() in fcx_kernels.hip, restated on the parameter block.
+static int plan_audit(const fcx_engine *e, const Params &P) {
+  const uint32_t st = P.stages;
+  auto need = [&](const void *ptr, int s, const char *what, const char *name) -> int {
+    if (ptr) return FCX_OK;
+    return fail(FCX_E_STATE, "plan audit: surface type %d: %s would read the unbound %s (stages 0x%x)", s, what, name,
+                (unsigned)st);
+  };
+#define AUD(ptr, what, name)                                \
+  do {                                                      \
+    if (int r_ = need((ptr), s + 1, (what), (name))) return r_; \
+  } while (0)
+  auto cclm_like = [](int m) { return m == FCX_CCLM || m == FCX_MOM5; };
+  for (int s = 0; s < P.num_types; ++s) {
+    const TypeParams &tp = P.type[s];
+    const TGridPtrs &t = tp.t;
+    const bool q_t = (st & S_QSUR_T) && tp.m_qsur[0] == FCX_CCLM;
+    if ((st & S_RBBR) && t.rbbr && tp.m_rbbr == FCX_STBO) AUD(t.tsur, "RBBR", "TSUR");
+    if (q_t) {
+      AUD(t.fice, "QSUR(t)", "FICE");
+      AUD(t.psur, "QSUR(t)", "PSUR");
+      AUD(t.tsur, "QSUR(t)", "TSUR");
+    }
+    if (st & S_MEVA) {
+      if (cclm_like(tp.m_meva)) {
+        AUD(tp.m_meva == FCX_CCLM ? t.amoi : t.cmoi, "MEVA", tp.m_meva == FCX_CCLM ? "AMOI" : "CMOI");
+        AUD(t.psur, "MEVA", "PSUR");
+        AUD(t.qatm, "MEVA", "QATM");
+        AUD(t.tatm, "MEVA", "TATM");
+        AUD(t.uatm, "MEVA", "UATM");
+        AUD(t.vatm, "MEVA", "VATM");
+        if (!q_t) AUD(t.qsur_in, "MEVA", "QSUR");
+      } else if (tp.m_meva == FCX_RCO) {
+        AUD(t.qatm, "MEVA", "QATM");
+        AUD(t.tsur, "MEVA", "TSUR");
+        AUD(t.uatm, "MEVA", "UATM");
+        AUD(t.vatm, "MEVA", "VATM");
+      }
+    }
+    if ((st & S_HLAT) && t.hlat && (tp.m_hlat == FCX_WATER || tp.m_hlat == FCX_ICE) &&
+        !((st & S_MEVA) && is_compute(tp.m_meva)))
+      AUD(t.meva_in, "HLAT", "MEVA");
+    if ((st & S_HSEN) && t.hsen) {
+      if (cclm_like(tp.m_hsen)) {
+        AUD(tp.m_hsen == FCX_CCLM ? t.amoi : t.chea, "HSEN", tp.m_hsen == FCX_CCLM ? "AMOI" : "CHEA");
+        for (auto pn : {std::make_pair((const void *)t.patm, "PATM"), std::make_pair((const void *)t.psur, "PSUR"),
+                        std::make_pair((const void *)t.qatm, "QATM"), std::make_pair((const void *)t.tatm, "TATM"),
+                        std::make_pair((const void *)t.tsur, "TSUR"), std::make_pair((const void *)t.uatm, "UATM"),
+                        std::make_pair((const void *)t.vatm, "VATM")})
+          AUD(pn.first, "HSEN", pn.second);
+      } else if (tp.m_hsen == FCX_RCO) {
+        AUD(t.tatm, "HSEN", "TATM");
+        AUD(t.tsur, "HSEN", "TSUR");
+        AUD(t.uatm, "HSEN", "UATM");
+        AUD(t.vatm, "HSEN", "VATM");
+      }
+    }
+    if ((st & S_RSDR) && t.rsdr) AUD(P.rsdd0, "RSDR", "RSDD(type 0)");
+    if (P.merged_uv) {
+      bool q_uv = false;
+      for (int k = 0; k < 2; ++k)
+        if ((st & (k == 0 ? S_QSUR_U : S_QSUR_V)) && tp.m_qsur[1 + k] == FCX_CCLM && tp.uv[k].qsur) {
+          q_uv = true;
+          AUD(t.fice, k ? "QSUR(v)" : "QSUR(u)", "FICE");
+          AUD(t.psur, k ? "QSUR(v)" : "QSUR(u)", "PSUR");
+          AUD(t.tsur, k ? "QSUR(v)" : "QSUR(u)", "TSUR");
+        }
+      const bool mom = ((st & S_UMOM) && tp.uv[0].mom) || ((st & S_VMOM) && tp.uv[1].mom);
+      if (mom && cclm_like(tp.m_mom)) {
+        AUD(tp.m_mom == FCX_CCLM ? tp.uv[0].amom : tp.uv[0].cmom, "UMOM/VMOM", tp.m_mom == FCX_CCLM ? "AMOM" : "CMOM");
+        AUD(t.psur, "UMOM/VMOM", "PSUR");
+        AUD(t.tsur, "UMOM/VMOM", "TSUR");
+        AUD(t.uatm, "UMOM/VMOM", "UATM");
+        AUD(t.vatm, "UMOM/VMOM", "VATM");
+        if (!q_t && !q_uv) AUD(t.qsur_in, "UMOM/VMOM", "QSUR");
+      } else if (mom && tp.m_mom == FCX_RCO) {
+        AUD(t.uatm, "UMOM/VMOM", "UATM");
+        AUD(t.vatm, "UMOM/VMOM", "VATM");
+      }
+    } else {
+      for (int k = 0; k < 2; ++k) {
+        const UVGridPtrs &g = tp.uv[k];
+        const char *wq = k ? "QSUR(v)" : "QSUR(u)", *wm = k ? "VMOM" : "UMOM";
+        const bool do_q = (st & (k == 0 ? S_QSUR_U : S_QSUR_V)) && tp.m_qsur[1 + k] == FCX_CCLM && g.qsur;
+        const bool do_m = (st & (k == 0 ? S_UMOM : S_VMOM)) && g.mom;
+        if (do_q) {
+          AUD(g.fice, wq, "FICE");
+          AUD(g.psur, wq, "PSUR");
+          AUD(g.tsur, wq, "TSUR");
+        }
+        if (do_m && cclm_like(tp.m_mom)) {
+          AUD(tp.m_mom == FCX_CCLM ? g.amom : g.cmom, wm, tp.m_mom == FCX_CCLM ? "AMOM" : "CMOM");
+          AUD(g.psur, wm, "PSUR");
+          AUD(g.tsur, wm, "TSUR");
+          AUD(g.uatm, wm, "UATM");
+          AUD(g.vatm, wm, "VATM");
+          if (!do_q) AUD(g.qsur_in, wm, "QSUR");
+        } else if (do_m && tp.m_mom == FCX_RCO) {
+          AUD(g.uatm, wm, "UATM");
+          AUD(g.vatm, wm, "VATM");
+        }
+      }
+    }
+    if (P.ravg_on) {
+      AUD(P.ravg.fare[s], "type-0 average", "FARE");
+      if (P.ravg.out[A_TSUR]) AUD(t.tsur, "type-0 average of TSUR", "TSUR");
+    }
+    for (int a = 0; a < P.num_avg; ++a) {
+      const AvgEntry &ae = P.avg[a];
+      AUD(ae.x0, "type-0 average", "type-0 output");
+      AUD(ae.x[s], "type-0 average", "averaged field");
+      AUD(ae.fare[s], "type-0 average", "FARE");
+    }
+  }
+#undef AUD
+  (void)e;
+  return FCX_OK;
+}
+
 static int build_plan(fcx_engine *e, uint32_t stages, int avg_phases, Plan &pl) {
   Params &P = pl.host;
   std::memset(&P, 0, sizeof P);
@@ -921,17 +1046,26 @@ static int build_plan(fcx_engine *e, uint32_t stages, int avg_phases, Plan &pl) 
   if (stages & (S_QSUR_U | S_UMOM)) n_max = std::max(n_max, e->n[1]);
   if (stages & (S_QSUR_V | S_VMOM)) n_max = std::max(n_max, e->n[2]);
 
+  // a bound buffer's device address (fcx_plan_check before any mirror exists: a tag address)
+  auto dev_of = [&](int b) -> double * {
+    if (e->bufs[b].dev || !e->plan_dry) return e->bufs[b].dev;
+    return reinterpret_cast<double *>((uintptr_t)(b + 1) << 12);
+  };
+  // FCX_TEST_PLAN_UNBIND=<VAR> (tests only, fcx_plan_check): the planner "forgets" that input,
+  // so the audit's named error can be seen
+  const char *unbind = e->plan_dry ? std::getenv("FCX_TEST_PLAN_UNBIND") : nullptr;
   auto in = [&](int s, int g, int var) -> const double * {
     const int b = e->buf(s, g, var);
     if (b < 0) return nullptr;
+    if (e->plan_dry && unbind && std::strcmp(unbind, kVarNames[var0(var)]) == 0) return nullptr;
     reads.insert(b);
-    return e->bufs[b].dev;
+    return dev_of(b);
   };
   auto out = [&](int s, int g, int var) -> double * {
     const int b = e->buf(s, g, var);
     if (b < 0) return nullptr;
     writes.insert(b);
-    return e->bufs[b].dev;
+    return dev_of(b);
   };
 
   for (int s = 1; s <= e->T; ++s) {
@@ -1112,7 +1246,7 @@ static int build_plan(fcx_engine *e, uint32_t stages, int avg_phases, Plan &pl) 
           return fail(FCX_E_MISSING, "average of %s: surface type %d lacks %s or FARE",
                       kVarNames[var0(var)], s, kVarNames[var0(var)]);
         // values produced in this launch are re-read by the same thread (in order)
-        ae.x[s - 1] = e->dptr(s, g, var);
+        ae.x[s - 1] = dev_of(e->buf(s, g, var));
         if (!writes.count(e->buf(s, g, var))) reads.insert(e->buf(s, g, var));
         ae.fare[s - 1] = in(s, g, FCX_FARE);
       }
@@ -1127,11 +1261,44 @@ static int build_plan(fcx_engine *e, uint32_t stages, int avg_phases, Plan &pl) 
   for (int b : pl.reads)
     if (!writes.count(b)) pure.push_back(b);
   pl.reads.swap(pure);
+  if (int r = plan_audit(e, P)) return r;
+  if (e->plan_dry) return FCX_OK;  // fcx_plan_check: host only
   plan_fused_atmos(e, pl, stages, avg_phases);
   if (int r = plan_fused_records(e, pl, stages, avg_phases)) return r;
   HIP_TRY(hipMalloc(&pl.dev, sizeof(Params)));
   HIP_TRY(hipMemcpy(pl.dev, &P, sizeof(Params), hipMemcpyHostToDevice));
   return FCX_OK;
+}
+
+static uint32_t phase_stages(int phase);
+static int staged_sequence(int phase, std::vector<std::pair<uint32_t, int>> &seq);
+
+// Every plan the engine can launch, built on the host and audited (plan_audit), before
+// fcx_commit and without a GPU: the whole phases with their averages, the reference
+// sequence of a regridding engine, each per-call subroutine and each explicit average.
+extern "C" int fcx_plan_check(fcx_engine *e) {
+  if (!e) return fail(FCX_E_ARG, "NULL engine");
+  if (e->committed) return fail(FCX_E_STATE, "fcx_plan_check runs before fcx_commit");
+  if (int r = validate(e)) return r;
+  std::vector<std::pair<uint32_t, int>> sets;
+  for (int ph : {(int)FCX_PHASE_EARLY, (int)FCX_PHASE_NORMAL, (int)(FCX_PHASE_EARLY | FCX_PHASE_NORMAL)}) {
+    sets.push_back({phase_stages(ph), ph});
+    std::vector<std::pair<uint32_t, int>> seq;
+    staged_sequence(ph, seq);
+    for (auto &x : seq) sets.push_back({x.first, 0});
+    sets.push_back({S_AVG, ph});
+  }
+  for (uint32_t st : {S_QSUR_T, S_QSUR_U, S_QSUR_V, S_MEVA, S_HLAT, S_HSEN, S_UMOM, S_VMOM, S_RBBR, S_RSDR})
+    sets.push_back({st, 0});
+  for (auto &a : e->averages) sets.push_back({S_AVG, 1000 + 100 * a.second.first + a.second.second});
+  e->plan_dry = true;
+  int rc = FCX_OK;
+  for (auto &x : sets) {
+    Plan p;
+    if ((rc = build_plan(e, x.first, x.second, p)) != FCX_OK) break;
+  }
+  e->plan_dry = false;
+  return rc;
 }
 
 static int get_plan(fcx_engine *e, uint32_t stages, int avg_phases, Plan **pl) {
@@ -1443,50 +1610,82 @@ static void stage_setup(fcx_engine *e) {
       if (!f.external && heap(f.out_host, rm.n_dst)) f.st = stage_ref(e, f.out_dev);
 }
 
+// A pool whose image cannot be page-locked (a memory-tight node) takes the direct path: its
+// members' StageRefs are dropped, so they are copied one runtime copy per array from the
+// caller's pageable memory, as with FCX_OPT_HOST_STAGING 0.  Applies at commit and at a lazy
+// pool's first transfer alike, so no step and no per-call subroutine ever meets an
+// allocation failure (the lazy path returned FCX_E_NOMEM, which stopped the
+// coupled run through the Fortran drop-in).
+static void stage_disable(fcx_engine *e, size_t i) {
+  StagePool &p = e->spools[i];
+  p.host = nullptr;
+  p.disabled = true;
+  auto drop = [&](StageRef &st) {
+    if (st.sp == (int)i) st.sp = -1;
+  };
+  for (auto &bf : e->bufs) drop(bf.st);
+  for (auto &f : e->atm_fields) drop(f.st);
+  for (auto &rm : e->remaps)
+    for (auto &f : rm.fields) drop(f.st);
+}
+
+// FCX_TEST_PIN_FAIL (tests only): 1 = every image fails at commit, as on a node out of
+// lockable memory; 2 = only the lazy pools' images fail, at their first transfer
+static int pin_fail_mode() {
+  const char *v = std::getenv("FCX_TEST_PIN_FAIL");
+  return v && (*v == '1' || *v == '2') ? *v - '0' : 0;
+}
+
+// page-lock pool i's image now (false: it could not be, and the pool is disabled)
+static bool stage_pin(fcx_engine *e, size_t i, bool lazy) {
+  StagePool &p = e->spools[i];
+  if (p.host) return true;
+  if (p.disabled) return false;
+  const int inject = pin_fail_mode();
+  if (!(inject == 1 || (inject == 2 && lazy)) &&
+      hipHostMalloc((void **)&p.host, std::max<size_t>(p.bytes, 1), hipHostMallocDefault) == hipSuccess)
+    return true;
+  (void)hipGetLastError();
+  stage_disable(e, i);
+  return false;
+}
+
 // at commit: the host image of every staging pool a whole step transfers (page-locked, the
-// pool's size: the pinned footprint is fcx_staging_bytes).  A pool whose image cannot be
-// page-locked (a memory-tight node) falls back to the direct path -- its mirrors are copied
-// one runtime copy per array from the caller's pageable memory, as with
-// FCX_OPT_HOST_STAGING 0 -- so a step never meets an allocation failure.  Pools only other
-// calls transfer (eager[i] == 0: e.g. the tiled layout's pool of arrays no step reads or
-// writes) get their image at their first transfer (page-locking them up front
-// locked ~1 GB per 10M-cell engine that no step uses).
+// pool's size: the pinned footprint is fcx_staging_bytes).  Pools only other calls transfer
+// (eager[i] == 0: e.g. the tiled layout's pool of arrays no step reads or writes) get their
+// image at their first transfer (page-locking them up front locked ~1 GB per
+// 10M-cell engine that no step uses).
 static void stage_alloc_all(fcx_engine *e, const std::vector<char> &eager) {
-  // FCX_TEST_PIN_FAIL=1 (tests only): every image fails, as on a node out of lockable memory
-  const char *inject = std::getenv("FCX_TEST_PIN_FAIL");
-  const bool fail_all = inject && *inject == '1';
+  const bool fail_all = pin_fail_mode() == 1;
   for (size_t i = 0; i < e->spools.size(); ++i) {
-    StagePool &p = e->spools[i];
-    if (p.host) continue;  // (a mapped arena has its image already)
+    if (e->spools[i].host) continue;  // (a mapped arena has its image already)
     if (i < eager.size() && !eager[i] && !fail_all) continue;  // at its first transfer
-    if (!fail_all && hipHostMalloc((void **)&p.host, std::max<size_t>(p.bytes, 1), hipHostMallocDefault) == hipSuccess)
-      continue;
-    (void)hipGetLastError();
-    p.host = nullptr;
-    p.disabled = true;
-    auto drop = [&](StageRef &st) {
-      if (st.sp == (int)i) st.sp = -1;
-    };
-    for (auto &bf : e->bufs) drop(bf.st);
-    for (auto &f : e->atm_fields) drop(f.st);
-    for (auto &rm : e->remaps)
-      for (auto &f : rm.fields) drop(f.st);
+    (void)stage_pin(e, i, false);
   }
 }
 
-// the host images of the pools these transfers use (allocated at commit, or here at the
-// first transfer of a pool no whole step uses)
+// before a transfer of buffers `ids` (and atmosphere / remap outputs) is put together: the
+// lazy pools they use page-locked, or disabled so that those buffers take the direct path
+static void stage_prepare_bufs(fcx_engine *e, const std::vector<int> &ids) {
+  for (int b : ids) {
+    const int sp = e->bufs[(size_t)b].st.sp;
+    if (sp >= 0) (void)stage_pin(e, (size_t)sp, true);
+  }
+}
+static void stage_prepare_outputs(fcx_engine *e) {
+  for (auto &f : e->atm_fields)
+    if (f.st.sp >= 0) (void)stage_pin(e, (size_t)f.st.sp, true);
+  for (auto &rm : e->remaps)
+    for (auto &f : rm.fields)
+      if (f.st.sp >= 0) (void)stage_pin(e, (size_t)f.st.sp, true);
+}
+
+// the host images of the pools these transfers use (stage_prepare_* ran before the transfer
+// list was made, so every pool in it has its image)
 static int stage_alloc(fcx_engine *e, const std::vector<Xfer> &xs) {
   for (const Xfer &x : xs) {
     StagePool &p = e->spools[(size_t)x.sp];
-    if (p.host) continue;
-    if (p.disabled) return fail(FCX_E_STATE, "staging pool %d has no host image", x.sp);
-    if (hipHostMalloc((void **)&p.host, std::max<size_t>(p.bytes, 1), hipHostMallocDefault) != hipSuccess) {
-      (void)hipGetLastError();
-      p.host = nullptr;
-      return fail(FCX_E_NOMEM, "staging pool %d (%zu bytes) could not be page-locked at its first transfer", x.sp,
-                  p.bytes);
-    }
+    if (!p.host) return fail(FCX_E_STATE, "staging pool %d has no host image", x.sp);
   }
   return FCX_OK;
 }
@@ -2007,6 +2206,7 @@ static const double *month_slice(fcx_engine *e, int32_t t, int *rc) {
 // the mirrors of buffers `ids` <-> their host arrays on the engine stream: caller heap arrays
 // through the staging arena, fcx_host_malloc arrays (and staging off) by direct copies
 static int copy_bufs(fcx_engine *e, const std::vector<int> &ids, bool h2d, std::vector<Xfer> *more = nullptr) {
+  stage_prepare_bufs(e, ids);
   std::vector<Xfer> xs;
   if (more) xs.swap(*more);
   for (int b : ids) {
@@ -2142,6 +2342,7 @@ static int upload_one(fcx_engine *e, int b) {
   FieldUploader &u = *e->uploader;
   const Buffer &bf = e->bufs[(size_t)b];
   if (bf.n == 0) return FCX_OK;
+  if (bf.st.sp >= 0) (void)stage_pin(e, (size_t)bf.st.sp, true);  // (else: the direct path below)
   if (bf.st.sp >= 0) {
     if (!u.prepared) {  // stage_in's waits, once per step
       bool mapped = false;
@@ -2203,6 +2404,10 @@ static int uploader_join(fcx_engine *e) {
   if (u.err) {
     const int r = u.err;
     u.err = 0;
+    //  the failed hand-over leaves no field marked as sent: a host that retries
+    // the step moves every input again instead of running on a stale device mirror
+    std::fill(e->field_sent.begin(), e->field_sent.end(), 0);
+    u.prepared = false;
     return fail(r, "fcx_upload_field: %s", u.msg.c_str());
   }
   return FCX_OK;
@@ -2260,6 +2465,7 @@ extern "C" int fcx_download(fcx_engine *e, int phase) {
   if (phase < 1 || phase > 3) return fail(FCX_E_ARG, "phase %d unknown", phase);
   Plan *pl;
   if (int r = get_plan(e, phase_stages(phase), phase, &pl)) return r;
+  stage_prepare_outputs(e);
   std::vector<Xfer> xs;  // every staged download of the phase in one set of DMAs
   std::vector<int> ids = pl->writes;
   for (auto &f : e->atm_fields)
@@ -2619,6 +2825,9 @@ static int step_pipelined(fcx_engine *e, int phase, int32_t t, Plan *pl) {
     e->ev_out.push_back(c);
   }
   // staged (caller heap) and direct (library memory) transfers
+  stage_prepare_bufs(e, pl->reads);
+  stage_prepare_bufs(e, pl->writes);
+  stage_prepare_outputs(e);
   std::vector<Xfer> xin, xout;
   std::vector<int> din, dout;
   for (int b : pl->reads) {
@@ -3342,11 +3551,6 @@ struct fcx_comm {
   double *agree = nullptr;  // 2 * kSigWords doubles (device)
   std::vector<double> agreed;
   bool verify_every = false;  // fcx_comm_verify: the agreement before every exchange
-  // fcx_run_group_exchange: the boundary tiles' launch and the all-reduce run on this stream
-  // beside the engines' main launch
-  hipStream_t side = nullptr;
-  hipEvent_t ev_side = nullptr;
-  int64_t overlapped = 0;  // exchanges that ran beside a main launch (fcx_comm_overlapped)
 };
 
 extern "C" int fcx_comm_unique_id(void *id) {
@@ -3380,9 +3584,6 @@ extern "C" int fcx_comm_create(int device, int nranks, int rank, const void *id,
 extern "C" int fcx_comm_destroy(fcx_comm *c) {
   if (!c) return FCX_OK;
   for (hipEvent_t ev : c->events) (void)hipEventDestroy(ev);
-  if (c->side) (void)hipStreamSynchronize(c->side);
-  if (c->ev_side) (void)hipEventDestroy(c->ev_side);
-  if (c->side) (void)hipStreamDestroy(c->side);
   (void)hipFree(c->scratch);
   (void)hipFree(c->agree);
   if (c->comm) (void)rccl().CommDestroy(c->comm);
@@ -3450,13 +3651,7 @@ extern "C" int fcx_comm_verify(fcx_comm *c, int every_exchange) {
   return FCX_OK;
 }
 
-// s_coll: the stream of the collective (default: the first engine's, joined with the others'
-// before it); given, the slots are already complete in its order (fcx_run_group_exchange) and
-// only the finishes join the engines' streams after it
-// between: work to queue after the collective and before the finishes (the main launch of
-// fcx_run_group_exchange, so that the all-reduce is queued first)
-static int atmos_exchange(fcx_comm *c, fcx_engine *const *es, int n, hipStream_t s_coll = nullptr,
-                          const std::function<int()> &between = nullptr) {
+static int atmos_exchange(fcx_comm *c, fcx_engine *const *es, int n) {
   std::vector<fcx_engine *> v;  // the engines with boundary slots, in list order
   for (int i = 0; i < n; ++i)
     if (es[i]->atm_shared && es[i]->atm_nb > 0 && es[i]->atm_stride > 0) v.push_back(es[i]);
@@ -3466,10 +3661,10 @@ static int atmos_exchange(fcx_comm *c, fcx_engine *const *es, int n, hipStream_t
     total += (size_t)e->atm_nb * e->atm_stride;
     hash = (hash * 1000003ull + (uint64_t)e->atm_nb * 4099ull + (uint64_t)e->atm_stride) & ((1ull << 48) - 1);
   }
-  hipStream_t s0 = s_coll ? s_coll : n > 0 ? es[0]->stream : nullptr;
+  hipStream_t s0 = n > 0 ? es[0]->stream : nullptr;
   if (int r = exchange_agree(c, {(double)v.size(), (double)total, (double)hash}, s0)) return r;
   if (v.empty()) return FCX_OK;
-  if (!s_coll) s0 = v[0]->stream;
+  s0 = v[0]->stream;
   std::vector<char> fresh(v.size());
   int stale = -1;  // first engine with no accumulation since its last exchange
   bool inplace = true;
@@ -3485,18 +3680,16 @@ static int atmos_exchange(fcx_comm *c, fcx_engine *const *es, int n, hipStream_t
   for (auto *e : v)
     if (e->stream != s0 && std::find(others.begin(), others.end(), e->stream) == others.end())
       others.push_back(e->stream);
-  const bool pre_join = s_coll == nullptr;
   while (c->events.size() < 2 * others.size()) {
     hipEvent_t ev;
     HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     c->events.push_back(ev);
   }
   size_t k = 0;
-  if (pre_join)
-    for (hipStream_t so : others) {  // the all-reduce waits for those engines' accumulation
-      HIP_TRY(hipEventRecord(c->events[k], so));
-      HIP_TRY(hipStreamWaitEvent(s0, c->events[k++], 0));
-    }
+  for (hipStream_t so : others) {  // the all-reduce waits for those engines' accumulation
+    HIP_TRY(hipEventRecord(c->events[k], so));
+    HIP_TRY(hipStreamWaitEvent(s0, c->events[k++], 0));
+  }
   if (inplace) {
     RCCL_TRY(rccl().AllReduce(v[0]->atm_shared, v[0]->atm_shared, total, ncclFloat64, ncclSum, c->comm, s0));
   } else {
@@ -3525,8 +3718,6 @@ static int atmos_exchange(fcx_comm *c, fcx_engine *const *es, int n, hipStream_t
       off += cnt;
     }
   }
-  if (between)
-    if (int r = between()) return r;
   for (hipStream_t so : others) {  // the finishes on that stream wait for the all-reduce
     HIP_TRY(hipEventRecord(c->events[k], s0));
     HIP_TRY(hipStreamWaitEvent(so, c->events[k++], 0));
@@ -3561,121 +3752,6 @@ static int atmos_exchange(fcx_comm *c, fcx_engine *const *es, int n, hipStream_t
                 "boundary exchange: engine %d of the list has no accumulation since its last exchange (fcx_run or "
                 "fcx_run_atmos first); it took part with zeros",
                 stale);
-  return FCX_OK;
-}
-
-// fcx_run_group + fcx_atmos_allreduce with the exchange overlapped: the tiles that write
-// boundary slots (the segment of each engine's first and last atmosphere cell) go out first,
-// as their own small group launch on the communicator's side stream, followed there by the
-// all-reduce; the other tiles run meanwhile as the main group launch on the engines' stream,
-// and the finishes wait for both.  The collective sequence is that of fcx_atmos_allreduce
-// (same agreement, same all-reduce), so ranks that take the sequential fallback -- some
-// engine cannot merge, no halo tiles, remaps, an attached communicator -- stay matched.
-static int run_group_exchange(fcx_comm *c, fcx_engine *const *es, int n, int phase, int32_t t) {
-  std::vector<GroupLaunchMember> mem;
-  std::vector<int> member_of;
-  if (int r = select_group(es, n, phase, t, mem, member_of)) return r;
-  bool split = (int)mem.size() == n && n >= 1;
-  for (size_t k = 0; split && k < mem.size(); ++k) {
-    const fcx_engine *e = mem[k].e;
-    split = member_of[k] == (int)k && !e->comm && mem[k].lc.halo > 0 && e->remaps.empty() && e->atm_shared &&
-            e->atm_nb > 0 && e->atm_stride > 0 && e->n_atmos > 0 && (int64_t)e->atm_row.size() > e->n_atmos;
-  }
-  if (!split) {
-    if (int r = fcx_run_group(es, n, phase, t)) return r;
-    return atmos_exchange(c, es, n);
-  }
-  const int nm = (int)mem.size();
-  GroupMember gm[kMaxGroup];
-  group_members(mem.data(), nm, gm);
-  // each member's boundary tiles: tile 0 (its first atmosphere cell's segment starts at cell
-  // 0) when that cell is shared, and the tile where its last atmosphere cell's segment starts
-  int64_t brange[2 * kMaxGroup][3], mrange[3 * kMaxGroup][3];
-  int nb = 0, nmr = 0;
-  for (int k = 0; k < nm; ++k) {
-    const fcx_engine *e = mem[k].e;
-    const int64_t own = (mem[k].lc.f32 ? kF32Cpl : 2) * (64 - mem[k].lc.halo), nt = gm[k].af.n_tiles;
-    int64_t b[2];
-    int cnt = 0;
-    if (e->atm_left >= 0) b[cnt++] = 0;
-    if (e->atm_right >= 0) {
-      const int64_t r = std::min<int64_t>(e->atm_row[(size_t)e->n_atmos - 1] / own, nt - 1);
-      if (!cnt || r != b[0]) b[cnt++] = r;
-    }
-    int64_t at = 0;
-    for (int j = 0; j < cnt; ++j) {
-      brange[nb][0] = k, brange[nb][1] = b[j], brange[nb++][2] = 1;
-      if (b[j] > at) mrange[nmr][0] = k, mrange[nmr][1] = at, mrange[nmr++][2] = b[j] - at;
-      at = b[j] + 1;
-    }
-    if (nt > at) mrange[nmr][0] = k, mrange[nmr][1] = at, mrange[nmr++][2] = nt - at;
-  }
-  hipStream_t s_eng = mem[0].e->stream;
-  if (!c->side) {
-    HIP_TRY(hipSetDevice(c->device));
-    HIP_TRY(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
-    HIP_TRY(hipEventCreateWithFlags(&c->ev_side, hipEventDisableTiming));
-  }
-#ifndef FCX_OVERLAP_BOUNDARY_ON_SIDE
-#define FCX_OVERLAP_BOUNDARY_ON_SIDE 0
-#endif
-  // the boundary tiles go first on the engines' stream (alone on the GPU for the few
-  // microseconds they take), the all-reduce on the side stream after them, then the main
-  // launch: run beside the main launch from the start, the boundary launch measured 55 us
-  // per step slower (profiles/r05/overlap/)
-  hipStream_t s_b = FCX_OVERLAP_BOUNDARY_ON_SIDE ? c->side : s_eng;
-  if (FCX_OVERLAP_BOUNDARY_ON_SIDE) {
-    HIP_TRY(hipEventRecord(c->ev_side, s_eng));  // the engines' earlier work (uploads) first
-    HIP_TRY(hipStreamWaitEvent(c->side, c->ev_side, 0));
-  }
-  if (nb) {
-    const int r = launch_cells_group(gm, nm, mem[0].lc, s_b, brange, nb);
-    if (r) return fail(FCX_E_HIP, "cells_atmos_group_kernel (boundary tiles) launch: %s", hipGetErrorString((hipError_t)r));
-  }
-  if (!FCX_OVERLAP_BOUNDARY_ON_SIDE) {
-    HIP_TRY(hipEventRecord(c->ev_side, s_eng));
-    HIP_TRY(hipStreamWaitEvent(c->side, c->ev_side, 0));
-  }
-  for (int k = 0; k < nm; ++k) {
-    fcx_engine *e = mem[k].e;
-    e->group_members = nm;
-    e->atm_done_fused = true;
-    e->atm_done = true;
-  }
-  // the collective on the side stream (after the boundary tiles) is queued before the main
-  // launch, so that its kernel is dispatched before the main launch fills the CUs; the
-  // finishes go on the engines' stream after both
-  auto main_launch = [&]() -> int {
-    if (nmr) {
-      const int r = launch_cells_group(gm, nm, mem[0].lc, s_eng, mrange, nmr);
-      if (r) return fail(FCX_E_HIP, "cells_atmos_group_kernel launch: %s", hipGetErrorString((hipError_t)r));
-    }
-    for (int k = 0; k < nm; ++k)
-      if (int r = launch_empty_cells(mem[k].e, mem[k].pl, mem[k].lc)) return r;
-    return FCX_OK;
-  };
-  if (int r = atmos_exchange(c, es, n, c->side, main_launch)) return r;
-  ++c->overlapped;
-  for (int k = 0; k < nm; ++k) {
-    fcx_engine *e = mem[k].e;
-    if (e->timing) HIP_TRY(hipEventRecord(e->ev1, e->stream));
-    e->timed = e->timing;
-  }
-  return FCX_OK;
-}
-
-extern "C" int fcx_run_group_exchange(fcx_comm *c, fcx_engine *const *es, int n, int phase, int32_t t) {
-  if (!c) return fail(FCX_E_ARG, "NULL communicator");
-  if (n < 0 || (n > 0 && !es)) return fail(FCX_E_ARG, "bad engine list");
-  if (phase < 1 || phase > 3) return fail(FCX_E_ARG, "phase %d unknown", phase);
-  for (int i = 0; i < n; ++i)
-    if (int r = check(es[i])) return r;
-  return run_group_exchange(c, es, n, phase, t);
-}
-
-extern "C" int fcx_comm_overlapped(fcx_comm *c, int64_t *count) {
-  if (!c || !count) return fail(FCX_E_ARG, "NULL argument");
-  *count = c->overlapped;
   return FCX_OK;
 }
 

@@ -269,10 +269,10 @@ struct GroupMember {
   AtmosFused af;          // its accumulation (af.n_tiles: its tile count)
 };
 // The grid's tiles in ranges: grid tiles [t0, next range's t0) are tiles [first, ...) of member
-// `member`.  A plain group launch has one range per member (all its tiles); the boundary
-// exchange split (fcx_run_group_exchange) launches the tiles that write boundary slots apart
-// from the others, as ranges of the same members.
-constexpr int kMaxGroupRanges = 12;
+// `member`; a group launch has one range per member (all its tiles).  (Round 5 also launched
+// the boundary-slot tiles apart, as ranges of the same members, to overlap the exchange; it
+// measured slower and was removed in round 6.)
+constexpr int kMaxGroupRanges = kMaxGroup;
 struct GroupRange {
   int64_t t0;
   int64_t first;
@@ -287,10 +287,8 @@ struct GroupArgs {
   GroupRange r[kMaxGroupRanges];
 };
 // lc: the members' common launch shape (nontemporal, f32, halo > 0 or not); af.n_tiles of
-// every member is set by the caller.  ranges: n_ranges {member, first tile, tile count}
-// (nullptr: every member's tiles, one range each).  hipError_t as int.
-int launch_cells_group(GroupMember *members, int n, const LaunchConfig &lc, void *stream,
-                       const int64_t (*ranges)[3] = nullptr, int n_ranges = 0);
+// every member is set by the caller.  hipError_t as int.
+int launch_cells_group(GroupMember *members, int n, const LaunchConfig &lc, void *stream);
 
 // the segments carried over a tile boundary: carry of tile t-1 + the head cells of tile t,
 // for every tile of a launch of n_cells (fp32: 256-cell tiles of float fields)

@@ -181,12 +181,15 @@ __device__ __forceinline__ void uv_grid(const TypeParams &tp, int k, uint32_t st
   Vec<C, R> ts = {}, fi = {}, ps = {}, u = {}, v = {}, a = {}, qs = {};
   if (g.tsur) ts = LD(g.tsur, j0, n);
   if (g.psur) ps = LD(g.psur, j0, n);
-  if (do_q) fi = LD(g.fice, j0, n);
+  // every load is guarded by its own pointer, whatever the method says: a method whose input
+  // the planner left unbound reads nothing (plan_audit at plan build names that case as an
+  // error before any launch; round-5 fault: 'zero' momentum loaded unbound winds)
+  if (do_q && g.fice) fi = LD(g.fice, j0, n);
   if (do_m) {  // ('zero' momentum binds no wind: the planner leaves uatm / vatm unset)
     if (g.uatm) u = LD(g.uatm, j0, n);
     if (g.vatm) v = LD(g.vatm, j0, n);
-    if (tp.m_mom == FCX_CCLM) a = LD(g.amom, j0, n);
-    if (tp.m_mom == FCX_MOM5) a = LD(g.cmom, j0, n);
+    if (tp.m_mom == FCX_CCLM && g.amom) a = LD(g.amom, j0, n);
+    if (tp.m_mom == FCX_MOM5 && g.cmom) a = LD(g.cmom, j0, n);
     if (g.qsur_in && !do_q) qs = LD(g.qsur_in, j0, n);
   }
   if (do_q) {
@@ -403,7 +406,7 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
       if (q.uv[0].cmom) n_cmom = LD(q.uv[0].cmom, j0, nt);
     }
     if constexpr (RAVG) {
-      if (P->ravg_on) n_fare = LD(P->ravg.fare[s2], j0, nt);
+      if (P->ravg_on && P->ravg.fare[s2]) n_fare = LD(P->ravg.fare[s2], j0, nt);
     }
   };
   if constexpr (kPrefetch) {
@@ -497,7 +500,7 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
       }
       if constexpr (RAVG) {
         if constexpr (!kPrefetch) {
-          if (P->ravg_on) sink.fare = LD(P->ravg.fare[s], j0, nt);
+          if (P->ravg_on && P->ravg.fare[s]) sink.fare = LD(P->ravg.fare[s], j0, nt);
         }
         sink(A_TSUR, ts);
       }
@@ -648,7 +651,9 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
       const int64_t n = P->n[ae.grid];
       if (j0 >= n) continue;
       Vec<C, R> acc = splat<C, R>(R(0));
+      if (!ae.x0) continue;  // (plan_audit: every entry binds x0, x[s] and fare[s])
       for (int s = 0; s < T; ++s) {
+        if (!ae.x[s] || !ae.fare[s]) continue;
         const Vec<C, R> x = LD(ae.x[s], j0, n);
         const Vec<C, R> f = LD(ae.fare[s], j0, n);
         FOR_C acc.v[i] = acc.v[i] + x.v[i] * f.v[i];
@@ -1668,8 +1673,7 @@ static void launch_group_h(bool halo, bool ravg, int blocks, hipStream_t s, cons
                        g, p[0], p[1], p[2], p[3]);
 }
 
-int launch_cells_group(GroupMember *members, int n, const LaunchConfig &lc, void *stream,
-                       const int64_t (*ranges)[3], int n_ranges) {
+int launch_cells_group(GroupMember *members, int n, const LaunchConfig &lc, void *stream) {
   if (n < 1 || n > kMaxGroup) return (int)hipErrorInvalidValue;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   GroupArgs g{};
@@ -1681,26 +1685,10 @@ int launch_cells_group(GroupMember *members, int n, const LaunchConfig &lc, void
       return (int)hipErrorInvalidValue;
     m.tile0 = total;
     g.m[k] = m;
-    if (!ranges) {
-      g.r[k] = GroupRange{total, 0, k, 0};
-      total += m.af.n_tiles;
-    }
+    g.r[k] = GroupRange{total, 0, k, 0};
+    total += m.af.n_tiles;
   }
-  if (ranges) {  // the caller's ranges, each inside its member's tiles
-    if (n_ranges < 1 || n_ranges > kMaxGroupRanges) return (int)hipErrorInvalidValue;
-    int used = 0;
-    for (int j = 0; j < n_ranges; ++j) {
-      const int64_t mk = ranges[j][0], first = ranges[j][1], cnt = ranges[j][2];
-      if (mk < 0 || mk >= n || first < 0 || cnt < 0 || first + cnt > members[mk].af.n_tiles)
-        return (int)hipErrorInvalidValue;
-      if (cnt == 0) continue;
-      g.r[used++] = GroupRange{total, first, (int32_t)mk, 0};
-      total += cnt;
-    }
-    g.n_ranges = used;
-  } else {
-    g.n_ranges = n;
-  }
+  g.n_ranges = n;
   g.total_tiles = total;
   if (total == 0) return 0;
   const int64_t kw = lc.f32 ? atmos_waves<kF32Cpl>() : atmos_waves<2>();

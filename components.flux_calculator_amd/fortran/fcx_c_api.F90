@@ -364,15 +364,6 @@ MODULE fcx_c_api
       INTEGER(c_int), VALUE :: every_exchange
       INTEGER(c_int) :: fcx_comm_verify
     END FUNCTION
-    ! fcx_run_group + fcx_atmos_allreduce with the exchange overlapped (engines: c_ptr array)
-    FUNCTION fcx_run_group_exchange(comm, engines, n, phase, t) BIND(C, name='fcx_run_group_exchange')
-      IMPORT :: c_int, c_int32_t, c_ptr
-      TYPE(c_ptr), VALUE :: comm
-      TYPE(c_ptr), DIMENSION(*), INTENT(IN) :: engines
-      INTEGER(c_int), VALUE :: n, phase
-      INTEGER(c_int32_t), VALUE :: t
-      INTEGER(c_int) :: fcx_run_group_exchange
-    END FUNCTION
     ! ---- the host's abort routine (oasis_abort, flux_calculator.F90:883-887): a BIND(C)
     ! subroutine taking CHARACTER(kind=c_char), DIMENSION(*) (NUL-terminated), registered
     ! with c_funloc; fcx_abort calls it (fcx_c_string turns the message into a string)

@@ -46,6 +46,7 @@ SIGNATURES = [
     ("fcx_add_average", _I, [_P, _I, _I, _I]),
     ("fcx_set_precision", _I, [_P, _I]),
     ("fcx_commit", _I, [_P]),
+    ("fcx_plan_check", _I, [_P]),
     ("fcx_upload", _I, [_P, _I]),
     ("fcx_run", _I, [_P, _I, _I32]),
     ("fcx_download", _I, [_P, _I]),
@@ -94,8 +95,6 @@ SIGNATURES = [
     ("fcx_last_group_size", _I, [_P, _c.POINTER(_I32)]),
     ("fcx_step_async", _I, [_P, _I, _I32]),
     ("fcx_upload_field", _I, [_P, _I, _I, _I]),
-    ("fcx_run_group_exchange", _I, [_P, _c.POINTER(_P), _I, _I, _I32]),
-    ("fcx_comm_overlapped", _I, [_P, _c.POINTER(_I64)]),
     ("fcx_comm_verify", _I, [_P, _I]),
     ("fcx_set_abort_handler", _I, [_P]),
     ("fcx_abort", _I, [_c.c_char_p]),

@@ -55,19 +55,6 @@ class Comm:
         arr = (ctypes.c_void_p * len(engines))(*[e.h.value for e in engines])
         _lib.check(self.lib.fcx_atmos_allreduce(self.h, arr, len(engines)))
 
-    def run_group_exchange(self, engines, current_step_time=0, phase=3):
-        """fcx_run_group of this rank's engines + the ONE all-reduce of their boundary slots,
-        overlapped: the boundary tiles and the collective on the communicator's stream beside
-        the main launch (fcx_run_group_exchange)."""
-        arr = (ctypes.c_void_p * len(engines))(*[e.h.value for e in engines])
-        _lib.check(self.lib.fcx_run_group_exchange(self.h, arr, len(engines), int(phase), int(current_step_time)))
-
-    def overlapped(self):
-        """Exchanges that ran beside a main launch (fcx_comm_overlapped)."""
-        n = ctypes.c_int64()
-        _lib.check(self.lib.fcx_comm_overlapped(self.h, ctypes.byref(n)))
-        return n.value
-
     def verify(self, every_exchange=True):
         """fcx_comm_verify: the signature agreement before every exchange (hosts that change
         their engine lists at run time) or only before the first of each signature."""

@@ -19,7 +19,7 @@ class Engine:
 
     def __init__(self, lf: LocalFields, num_surface_types, methods, corrections=None,
                  averages=(), regrid=None, device=0, stream=None, atmos=None, options=None, remaps=None,
-                 lib=None):
+                 lib=None, commit=True):
         """atmos: exchange -> atmosphere accumulation, dict with
              local   : fcx.parallel.LocalAtmos of this rank
              fields  : [(phase, surface_type, grid, name, out_array[n_atmos])]
@@ -31,7 +31,8 @@ class Engine:
         remaps: exchange -> model remaps, each {"n_dst", "src", "dst", "w" (0-based links),
                  "fields": [(phase, surface_type, grid, name, out_array[n_dst])]}
         options: {name: value} for fcx_set_option.
-        lib: another libfcx build from _lib.load_path (A/B measurement tools only)."""
+        lib: another libfcx build from _lib.load_path (A/B measurement tools only).
+        commit=False: bind only (no GPU touched); plan_check() then audits the plans on the host."""
         self.lib = lib if lib is not None else _lib.load()
         self.lf = lf
         self.T = int(num_surface_types)
@@ -122,11 +123,19 @@ class Engine:
                                                             ctypes.c_void_p(data_ptr(out)), flags))
             for name, value in (options or {}).items():
                 _lib.check(self.lib.fcx_set_option(h, self._option_id(name), int(value)))
-            _lib.check(self.lib.fcx_commit(h))
+            if commit:
+                _lib.check(self.lib.fcx_commit(h))
         except Exception:
             self.lib.fcx_destroy(h)
             self.h = None
             raise
+
+    def plan_check(self):
+        """fcx_plan_check: every launch plan built on the host and audited (before commit)."""
+        _lib.check(self.lib.fcx_plan_check(self.h))
+
+    def commit(self):
+        _lib.check(self.lib.fcx_commit(self.h))
 
     # ---- fused path
     def upload(self, phase=PHASE_ALL):

@@ -137,6 +137,12 @@ enum fcx_precision { FCX_PRECISION_F64 = 0, FCX_PRECISION_F32 = 1 };
 int fcx_set_precision(fcx_engine *e, int precision);
 /* validate (flux_calculator_prepare.F90 rules), allocate device mirrors, build plans */
 int fcx_commit(fcx_engine *e);
+/* before fcx_commit, host only (no GPU): validate, then build every launch plan the engine can
+ * take -- the whole phases, the per-call subroutines, the regridding sequence, the explicit
+ * averages -- and audit each against the kernels' load predicates: a computed flux whose input
+ * the planner did not bind is a named FCX_E_STATE error (the same audit runs on every plan
+ * fcx_commit and the later calls build, before its first launch) */
+int fcx_plan_check(fcx_engine *e);
 
 /* ---- per coupling step: fused path ---- */
 int fcx_upload(fcx_engine *e, int phase);   /* H2D of host-bound inputs of the phase  */
@@ -172,10 +178,13 @@ int fcx_step_async(fcx_engine *e, int phase, int32_t current_step_time);
  * fcx_upload_field): its host array is copied into the staging arena and DMAed to its
  * mirror by the engine's upload thread while the host goes on to receive the next field
  * (flux_calculator.F90:872-897, 938-966: the reference gets the fields one by one).  The
- * value at the call is what the next run uses; the host may overwrite the array once the
- * next engine call (any but fcx_upload_field) returns -- every call first waits for the
- * handed-over fields.  fcx_upload / fcx_step / fcx_step_async then move only the phase's
- * remaining inputs.  Aliases (one array in several slots) are handed over once. */
+ * upload thread copies the array at some point before the next engine call (any but
+ * fcx_upload_field) returns, so the array must not change until that call returns; from
+ * then on the host may overwrite it -- every call first waits for the handed-over fields.
+ * fcx_upload / fcx_step / fcx_step_async then move only the phase's remaining inputs.
+ * Aliases (one array in several slots) are handed over once.  If a hand-over fails, the
+ * next call returns its error and no field counts as handed over, so a retried step moves
+ * every input again. */
 int fcx_upload_field(fcx_engine *e, int surface_type, int grid, int var);
 
 /* ---- per call: the reference subroutines one by one (exact drop-in semantics; each
@@ -290,21 +299,6 @@ int fcx_atmos_allreduce(fcx_comm *c, fcx_engine *const *engines, int n_engines);
 /* 1: the signature agreement before every exchange of the communicator; 0 (default): before
  * the first exchange of each signature */
 int fcx_comm_verify(fcx_comm *c, int every_exchange);
-/* fcx_run_group of the engines followed by fcx_atmos_allreduce over them, with the exchange
- * overlapped: the wave tiles that write boundary slots (each engine's first and last
- * atmosphere cell) run first as a small launch on the communicator's own stream, the
- * all-reduce follows there while the other tiles run as the main launch on the engines'
- * stream, and the finishes wait for both -- a step costs the flux pass plus the finish
- * instead of the flux pass plus the all-reduce latency.  Results and the collective sequence
- * are those of fcx_run_group + fcx_atmos_allreduce; engines that cannot take the split (not
- * all merged into one T = 1 launch with halo tiles, remaps, an attached communicator) run
- * exactly that way.  Measured on MI355X the split's two cross-stream edges (~10 us each) and
- * its boundary launch cost more than a small all-reduce hides: it pays
- * only where the collective is slow (many ranks, a slow fabric). */
-int fcx_run_group_exchange(fcx_comm *c, fcx_engine *const *engines, int n_engines, int phase,
-                           int32_t current_step_time);
-/* how many exchanges of the communicator ran beside a main launch (the split above) */
-int fcx_comm_overlapped(fcx_comm *c, int64_t *count);
 
 /* ---- exchange-grid -> model remaps ----
  * The SCRIP weight application OASIS3-MCT performs on the 'S' fields sent to a model

@@ -161,6 +161,30 @@ def run_case(case, kind="c", current_step_time=0, phases=(1, 2), regrid=False):
     return o.outputs()
 
 
+def host_threads():
+    """Threads for the oracle on this host: the process's CPU share, capped at 16 (the GPU
+    box's per-GPU share; os.cpu_count() there shows the whole machine)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(16, n, int(os.environ.get("OMP_NUM_THREADS", "16") or 16)))
+
+
+def run_case_threads(case, current_step_time=0, nthreads=None):
+    """run_case over the WHOLE grid with fco_step_threads: APPLE ranges over host threads,
+    bit-identical to fco_step (test_oracle_golden.py::test_oracle_threads_equal_single_thread).
+    No regridding; the type-0 averages follow serially, in the reference put order."""
+    o = OracleState(case, current_step_time)
+    lib, _ = load("c")
+    lib.fco_step_threads(ctypes.byref(o.st), int(nthreads or host_threads()))
+    for ph, g, name in case.averages:
+        lib.fco_average_across_surface_types(ctypes.byref(o.st), g, IDX0[name])
+    out = o.outputs()
+    del o
+    return out
+
+
 class OracleEngine:
     """The fcx.driver engine interface (step / do_regridding) on the C oracle, in place on
     a set-up's LocalFields: the reference time loop with the oracle doing the arithmetic."""

@@ -67,6 +67,42 @@ def norm_error(x, ref):
     return float(np.max(np.abs(x[fin] - ref[fin])) / (top if top > 0 else 1.0))
 
 
+def cell_report(got: dict, ref: dict):
+    """Per field, over every cell: the mixed error (the gate), the plain elementwise max
+    relative error, the counts of cells above 1e-10 by either measure, the bit-identical
+    cells.  {"s:g:NAME": {...}}"""
+    rep = {}
+    for key, r in ref.items():
+        g = np.asarray(got[key], dtype=np.float64)
+        r = np.asarray(r, dtype=np.float64)
+        fin = np.isfinite(r)
+        top = float(np.max(np.abs(r[fin]))) if fin.any() else 0.0
+        d = np.abs(g - r)
+        nz = np.abs(r) > 0
+        rel = np.zeros_like(r)
+        np.divide(d, np.abs(r), out=rel, where=nz)
+        rel[~nz & (d > 0)] = np.inf
+        scale = np.maximum(np.abs(r), 1e-6 * top)
+        mixed = np.divide(d, scale, out=np.zeros_like(r), where=scale > 0)
+        rep["%d:%d:%s" % key] = {
+            "cells": int(r.size), "mixed": mixed_error(g, r), "max_rel": float(rel.max(initial=0.0)),
+            "cells_rel_gt_1e-10": int((rel > FP64_TOL).sum()),
+            "cells_mixed_gt_1e-10": int((mixed > FP64_TOL).sum()),
+            "bit_identical_cells": int((g == r).sum())}
+    return rep
+
+
+def write_report(name, rep):
+    """gpurun_out/<name>.json (copied into profiles/ by the round's evidence scripts)."""
+    import json
+    import os
+
+    out = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out", "parity")
+    os.makedirs(out, exist_ok=True)
+    with open(os.path.join(out, name + ".json"), "w") as f:
+        json.dump(rep, f, indent=1)
+
+
 def error_report(got: dict, ref: dict):
     """{field: (norm-wise error, mixed error, elementwise max relative error)}"""
     out = {}

@@ -49,11 +49,6 @@ SCENARIOS = [
     # the signature agreement before every exchange (fcx_comm_verify): after an agreed
     # exchange, rank 1 passes a shorter engine list -- every rank gets the named error
     ("relisted_after_agreement", "adjacent", "one", "relist"),
-    # fcx_run_group_exchange: boundary tiles + the all-reduce on the communicator's stream
-    # beside the main launch; then with rank 0's last engine capped (it cannot merge, so rank 0
-    # takes the sequential fallback) -- the collective sequence must stay matched
-    ("group_exchange_split", "adjacent", "one", "group_exchange"),
-    ("group_exchange_mixed", "separate", "one", "group_exchange_mixed"),
 ]
 SCENARIOS_3 = [
     ("empty_middle_rank", "adjacent", "one", "empty_middle"),
@@ -128,10 +123,8 @@ def _scenario(rank, world, uid, name, layout, streams, special, log):
             atmos.update(own_boundaries=True, comm=comm)
         else:
             atmos["shared"] = (slots[i], stride)
-        if special in ("attached_group", "group_exchange_mixed"):
+        if special == "attached_group":
             opts = {"max_blocks": 32} if (rank == 0 and i == 2) else None
-        elif special == "group_exchange":
-            opts = None
         else:
             opts = {"atmos_in_run": 0} if i == 1 else None
         e = Engine(case.lf, 1, case.methods, corrections=case.corrections, atmos=atmos,
@@ -152,15 +145,8 @@ def _scenario(rank, world, uid, name, layout, streams, special, log):
         if special == "attached_group":
             run_group(engines, PHASE_ALL, 3600 * step)  # every engine's exchange inside
             group = [e.last_group_size() for e in engines]
-        grouped_exchange = special in ("group_exchange", "group_exchange_mixed")
-        if grouped_exchange:
-            try:
-                comm.run_group_exchange(engines, 3600 * step)  # the step and its one collective
-            except Exception as ex:  # noqa: BLE001 -- reported to the parent
-                err = str(ex)
-            group = [e.last_group_size() for e in engines] + [comm.overlapped()]
         for i, e in enumerate(engines):
-            if special == "attached_group" or grouped_exchange:
+            if special == "attached_group":
                 break
             if special == "stale" and rank == world - 1 and step == 0 and i == 2:
                 continue  # this rank never runs engine 2 before the first exchange
@@ -168,7 +154,7 @@ def _scenario(rank, world, uid, name, layout, streams, special, log):
             if i == 1:
                 e.run_atmos(PHASE_ALL)  # atmos_in_run 0: the accumulation on its own
         try:
-            if layout != "own" and not grouped_exchange:
+            if layout != "own":
                 short = (special == "mismatch" and rank == 1) or (special == "relist" and rank == 1 and step == 1)
                 use = engines[:2] if short else engines
                 comm.atmos_allreduce(use)
@@ -255,13 +241,10 @@ def test_exchange_ranks_through_libfcx(world, tmp_path):
             errs = [p["steps"][1]["error"] for p in per]
             if not all(e and "ranks disagree" in e for e in errs):
                 problems.append(f"{name}: step 1 expected every rank to report the disagreement, got {errs}")
-        if special in ("attached_group", "group_exchange_mixed", "group_exchange"):
+        if special == "attached_group":
             for r, p in enumerate(per):
-                want_g = [2, 2, 0] if (r == 0 and special != "group_exchange") else [3, 3, 3]
-                if special != "attached_group":  # + exchanges overlapped so far (rank 0 mixed: none)
-                    want_g = [want_g + [0 if want_g[2] == 0 else st + 1] for st in range(2)]
-                else:
-                    want_g = [want_g, want_g]
+                want_g = [2, 2, 0] if r == 0 else [3, 3, 3]
+                want_g = [want_g, want_g]
                 if [st["group"] for st in p["steps"]] != want_g:
                     problems.append(f"{name} rank {r}: group sizes {[st['group'] for st in p['steps']]}, want {want_g}")
         for step in range(1 if special == "relist" else 2):

@@ -526,3 +526,71 @@ def test_staging_pins_only_what_a_step_transfers():
     eng.close()
     ref = oracle_lib.run_case(case, "c", current_step_time=STEP_T)
     assert_parity(got, ref, label="lazy staging pools")
+
+
+def test_lazy_pool_pin_failure_takes_the_direct_path(monkeypatch):
+    """a lazy staging pool (page-locked at its first transfer) whose image cannot
+    be page-locked is disabled and its arrays take the direct path (one runtime copy each),
+    as at commit -- no FCX_E_NOMEM reaches the caller.  FCX_TEST_PIN_FAIL=2 fails only the
+    lazy pools; CMOI of a CCLM case lives in one (no whole step reads it) and is handed over
+    with fcx_upload_field, then a step and the per-call subroutines run."""
+    from fcx import flux_calculator_calculate as fcc  # noqa: F401  (the module loads the ABI)
+
+    n = 200_000
+    case = build_case("CCLM", n=n, T=1, bias=False, seed=4)
+    eng = Engine(case.lf, 1, case.methods, options={"zero_copy": 0})
+    pinned = eng.staging_bytes()
+    monkeypatch.setenv("FCX_TEST_PIN_FAIL", "2")
+    eng.upload_field(1, 1, "CMOI")  # the lazy pool: its pin fails, the direct copy runs
+    for k in case.outputs:
+        case.lf.field[k][:] = np.nan
+    eng.step(PHASE_ALL, STEP_T)
+    got = {k: np.array(case.lf.field[k], copy=True) for k in case.outputs}
+    assert eng.staging_bytes() == pinned  # the failed pool holds no image
+    lib = eng.lib
+    for k in case.outputs:
+        case.lf.field[k][:] = np.nan
+    for g in (1, 2, 3):
+        assert lib.fcx_calc_spec_vapor_surface(eng.h, g) == 0, lib.fcx_last_error()
+    assert lib.fcx_calc_flux_mass_evap(eng.h, STEP_T) == 0, lib.fcx_last_error()
+    assert lib.fcx_calc_flux_heat_latent(eng.h) == 0
+    assert lib.fcx_calc_flux_heat_sensible(eng.h) == 0
+    assert lib.fcx_calc_flux_momentum_east(eng.h, 2) == 0
+    assert lib.fcx_calc_flux_momentum_north(eng.h, 3) == 0
+    assert lib.fcx_calc_flux_radiation_blackbody(eng.h) == 0
+    per_call = {k: np.array(case.lf.field[k], copy=True) for k in case.outputs}
+    eng.close()
+    ref = oracle_lib.run_case(case, "c", current_step_time=STEP_T)
+    assert_parity(got, ref, label="lazy pool pin failure, step")
+    assert_parity(per_call, ref, label="lazy pool pin failure, per call")
+
+
+def test_handed_over_arrays_may_change_after_the_next_call():
+    """fcx_upload_field's contract (include/fcx.h): the array must not change
+    until the next engine call returns; after that the host may overwrite it and the run uses
+    the value handed over.  Every input handed over, fcx_synchronize returns, the inputs are
+    overwritten with garbage, then the step: bit-identical to a step on the original inputs."""
+    case = build_case("MOM5", n=32_768, T=1, bias=True, seed=12)
+    outs = {id(case.lf.field[k]) for k in case.outputs}
+    slots, seen = [], set()
+    for (s, g, name), a in case.lf.field.items():
+        if id(a) not in outs and id(a) not in seen:
+            seen.add(id(a))
+            slots.append(((s, g, name), a))
+    orig = [a.copy() for _, a in slots]
+    eng = Engine(case.lf, 1, case.methods, corrections=case.corrections)
+    eng.step(PHASE_ALL, STEP_T)
+    want = {k: np.array(case.lf.field[k], copy=True) for k in case.outputs}
+    for key, _ in slots:
+        eng.upload_field(*key)
+    eng.synchronize()  # the next engine call: the handed-over arrays are the engine's now
+    for _, a in slots:
+        a[:] = -1.0e30
+    for k in case.outputs:
+        case.lf.field[k][:] = np.nan
+    eng.step(PHASE_ALL, STEP_T)
+    got = {k: np.array(case.lf.field[k], copy=True) for k in case.outputs}
+    eng.close()
+    for (_, a), o in zip(slots, orig):
+        a[:] = o
+    same_bits(got, want)
