@@ -190,6 +190,35 @@ def multi_gpu_check(wl, world, rank, dist, samples=2000):
                     "(relative error); sampled interior cells bit-identical to the rank's own sequential sum"}
 
 
+def allreduce_cost(comm, wl, world, dist, iters=100):
+    """N > 1: the step's one collective alone -- an all-reduce (sum, fp64) of as many doubles
+    as the step's boundary slots (every variant's, wl.shared), through the same libfcx
+    communicator on the workload's stream, timed with one HIP event pair around `iters` of
+    them after a barrier; max over ranks.  None at N = 1 or without the libfcx communicator."""
+    import torch
+
+    if world <= 1 or comm is None or not hasattr(comm, "allreduce_sum"):
+        return None
+    buf = torch.zeros(wl.shared.numel(), dtype=torch.float64, device=wl.dev)
+    s = wl.stream
+    for _ in range(10):
+        comm.allreduce_sum(buf, s.cuda_stream)
+    torch.cuda.synchronize()
+    dist.barrier()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(s)
+    for _ in range(iters):
+        comm.allreduce_sum(buf, s.cuda_stream)
+    b.record(s)
+    torch.cuda.synchronize()
+    us = a.elapsed_time(b) * 1e3 / iters
+    t = torch.tensor([us], dtype=torch.float64, device=wl.dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return {"us_per_allreduce": round(float(t.item()), 2), "doubles": int(buf.numel()), "iters": iters,
+            "rule": "the step's boundary all-reduce alone (same count, same communicator, the workload's stream): "
+                    "one HIP event pair around the iterations, max over ranks"}
+
+
 def e2e_host(args, variants, sizes=(10_000_000, 32_768)):
     """SURVEY.md 8d end-to-end rate (never `value`): the fields in caller heap arrays (numpy,
     as a Fortran host's ALLOCATEd local_field arrays), every coupling step fcx_step = inputs
@@ -333,10 +362,13 @@ def e2e_async(args, variants, n=32_768, steps=500):
 def e2e_library_memory(args, variants, n=32_768, steps=500):
     """The Baltic-size step with the fields in fcx_host_malloc memory -- a host that allocates
     its local_field arrays from the library (c_f_pointer) instead of
-    its own heap: the default transport then reads and writes them in place over the link
-    (zero-copy), with no host copies and no DMA calls.  Median wall time per step of the
-    variants one after the other (fcx_step) and started together (fcx_step_async from one
-    thread, each engine on its own stream, then fcx_synchronize of each)."""
+    its own heap, inputs first and outputs after them as the reference allocates them
+    (flux_calculator.F90:436-560, then prepare:36-42).  Two transports: the span transport
+    (the default: device mirrors laid out like the host memory, ONE upload and ONE download per
+    engine and step) and zero-copy (FCX_OPT_ZERO_COPY 1: the kernels read and write the arrays
+    in place over the link).  Median wall time per step of the variants one after the other
+    (fcx_step) and started together (fcx_step_async from one thread, each engine on its own
+    stream, then fcx_synchronize of each)."""
     import torch
     from fcx.basic import PHASE_ALL
     from fcx.engine import Engine
@@ -344,37 +376,44 @@ def e2e_library_memory(args, variants, n=32_768, steps=500):
     from fcx.synthetic import build_case, inputs_for_bench
 
     data = inputs_for_bench(n)
-    streams = [torch.cuda.Stream() for _ in variants]
-    cases = [build_case(v, n=n, T=args.types, bias=args.bias, data=data if args.types == 1 else None)
-             for v in variants]
     res = {}
-    with Arena() as arena:
-        for c in cases:
-            arena.adopt(c.lf)
-        engines = [Engine(c.lf, c.num_surface_types, c.methods, corrections=c.corrections, averages=c.averages,
-                          stream=st.cuda_stream) for c, st in zip(cases, streams)]
-        for mode in ("sequential", "async"):
-            ts = []
-            for k in range(50 + steps):
-                t0 = time.perf_counter()
-                if mode == "sequential":
-                    for e in engines:
-                        e.step(PHASE_ALL, k * 3600)
-                else:
-                    for e in engines:
-                        e.step_async(PHASE_ALL, k * 3600)
-                    for e in engines:
-                        e.synchronize()
-                if k >= 50:
-                    ts.append(time.perf_counter() - t0)
-            res[f"{mode}_us_per_step_median"] = round(float(np.median(ts)) * 1e6, 1)
-            res[f"{mode}_us_per_step_p90"] = round(float(np.percentile(ts, 90)) * 1e6, 1)
-        for e in engines:
-            e.close()
-    res.update(steps=steps, engines=len(cases), transport="fcx_host_malloc arrays, default options (zero-copy "
-               "in place at this size)", rule="sequential: fcx_step of each variant in turn; async: fcx_step_async "
-               "of each from one host thread, then fcx_synchronize of each; a step = first start to the last "
-               "engine done")
+    for transport, opts in (("spans", {}), ("zero_copy", {"zero_copy": 1})):
+        streams = [torch.cuda.Stream() for _ in variants]
+        cases = [build_case(v, n=n, T=args.types, bias=args.bias, data=data if args.types == 1 else None)
+                 for v in variants]
+        with Arena() as arena:
+            for c in cases:
+                arena.adopt(c.lf)
+            engines = [Engine(c.lf, c.num_surface_types, c.methods, corrections=c.corrections, averages=c.averages,
+                              stream=st.cuda_stream, options=opts) for c, st in zip(cases, streams)]
+            out = {}
+            if transport == "spans":
+                out["copies_per_step"] = [list(e.span_runs()) for e in engines]
+            for mode in ("sequential", "async"):
+                ts = []
+                for k in range(50 + steps):
+                    t0 = time.perf_counter()
+                    if mode == "sequential":
+                        for e in engines:
+                            e.step(PHASE_ALL, k * 3600)
+                    else:
+                        for e in engines:
+                            e.step_async(PHASE_ALL, k * 3600)
+                        for e in engines:
+                            e.synchronize()
+                    if k >= 50:
+                        ts.append(time.perf_counter() - t0)
+                out[f"{mode}_us_per_step_median"] = round(float(np.median(ts)) * 1e6, 1)
+                out[f"{mode}_us_per_step_p90"] = round(float(np.percentile(ts, 90)) * 1e6, 1)
+            for e in engines:
+                e.close()
+        res[transport] = out
+    res.update(steps=steps, engines=len(variants),
+               transports="spans: device mirrors laid out like the host memory, one copy per run of adjacent arrays "
+                          "(the default for fcx_host_malloc arrays); zero_copy: the kernels use the arrays in place "
+                          "(FCX_OPT_ZERO_COPY 1)",
+               rule="sequential: fcx_step of each variant in turn; async: fcx_step_async of each from one host "
+                    "thread, then fcx_synchronize of each; a step = first start to the last engine done")
     return res
 
 
@@ -634,6 +673,7 @@ def main():
             traffic = None
 
     mg = multi_gpu_check(wl, world, rank, dist) if la is not None else None
+    ar = allreduce_cost(comm, wl, world, dist)
 
     out = {
         "metric": METRIC,
@@ -714,6 +754,8 @@ def main():
     }
     if mg is not None:
         out["multi_gpu_check"] = mg
+    if ar is not None:
+        out["allreduce"] = ar
     wl.close()
     del wl
     torch.cuda.synchronize()
@@ -752,7 +794,12 @@ def main():
         m4 = measure(w4, args, world, dist, coll if comm is None else comm, args.steps, args.warmup)
         k4 = m4["kern_mean"]
         d4 = m4["dom"]
+        mg4 = multi_gpu_check(w4, world, rank, dist) if w4.la is not None else None
+        ar4 = allreduce_cost(comm, w4, world, dist)
         out["config4"] = {
+            "baseline_config": "BASELINE.json configs[3]: the 40M-cell grid sharded 8 ways by decomp_def ranges -- "
+                               "THE 1/2/4/8-GPU strong-scaling curve (this object at N = 1, 2, 4, 8); the line's own "
+                               "`value` is weak scaling (10M cells per GPU)",
             "workload": "config 4: fixed synthetic grid sharded by APPLE ranges over the ranks (strong scaling), "
                         "CCLM+MOM5+RCO fused kernels + accumulation, one all-reduce of the boundary slots per step, "
                         f"{args.atmos_map} atmosphere map",
@@ -770,6 +817,11 @@ def main():
         if m4["group_ms"] is not None:
             out["config4"]["group_kernel_ms"] = round(m4["group_ms"], 4)
             out["config4"]["group_frac"] = round(sum(w4.alg_bytes) / (m4["group_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+        out["config4"]["ranks_seen"] = mg4["ranks_seen"] if mg4 is not None else world
+        if mg4 is not None:
+            out["config4"]["multi_gpu_check"] = mg4
+        if ar4 is not None:
+            out["config4"]["allreduce_us_per_step"] = ar4["us_per_allreduce"]
         w4.close()
         del w4, wl
         torch.cuda.synchronize()
@@ -816,8 +868,10 @@ def main():
             out["baltic_size"]["gpu_async_vs_all_cores"] = round(cp["us_per_step"] / asy["us_per_step_median"], 2)
             lib = e2e_library_memory(args, variants)
             out["baltic_size"]["gpu_dropin_library_memory"] = lib
-            out["baltic_size"]["gpu_library_memory_vs_all_cores"] = round(
-                cp["us_per_step"] / min(lib["sequential_us_per_step_median"], lib["async_us_per_step_median"]), 2)
+            # one ratio per transport and mode (no best-of-two after the fact)
+            out["baltic_size"]["gpu_library_memory_vs_all_cores"] = {
+                f"{tr}_{mode}": round(cp["us_per_step"] / lib[tr][f"{mode}_us_per_step_median"], 2)
+                for tr in ("spans", "zero_copy") for mode in ("sequential", "async")}
             # the host link's bound: the step's fields must cross it once
             # each way; measured both directions at once on this box
             from link_probe import link_rates
@@ -842,6 +896,11 @@ def main():
                                                             "overlap (the engines' own copies do overlap them in part, "
                                                             "DESIGN.md section 7); the host copies between the caller's "
                                                             "arrays and page-locked memory come on top of either")
+                # the library-memory step against the link's duplex floor (VERDICT r05 item 2:
+                # the span transport's target is <= 1.2 x bound_duplex_us)
+                out["baltic_size"]["gpu_library_memory_vs_duplex_floor"] = {
+                    f"spans_{mode}": round(lib["spans"][f"{mode}_us_per_step_median"] / max(duplex, 1e-9), 3)
+                    for mode in ("sequential", "async")}
     if rank == 0:
         print(json.dumps(out), flush=True)
     if comm is not None:

@@ -75,6 +75,16 @@ struct Buffer {
   bool external = false;   // caller-owned device memory (or a host array used in place)
   bool in_place = false;   // a host array the kernels use through its mapped address
   StageRef st;
+  int span = -1;           // fcx_host_malloc array moved by the span transport: its Span
+};
+
+// The span transport (FCX_OPT_LIB_SPANS) of fcx_host_malloc arrays: one device buffer per
+// host slab the engine's arrays sit in, laid out like the host memory from `lo` on, so that
+// arrays adjacent in host memory are adjacent on the device and move as ONE copy.
+struct Span {
+  uintptr_t lo = 0;  // host address of the device buffer's first byte
+  char *dev = nullptr;
+  size_t bytes = 0;
 };
 
 // A device pool with host-bound mirrors and its page-locked host image: the same bytes at
@@ -310,6 +320,10 @@ struct fcx_engine {
   // fcx_plan_check: plans built on the host only (no device memory; bound buffers without a
   // mirror yet stand in with a non-null tag address), audited, and dropped
   bool plan_dry = false;
+  // the span transport of fcx_host_malloc arrays (FCX_OPT_LIB_SPANS, default on)
+  bool lib_spans = true;
+  std::vector<Span> spans;
+  std::vector<char> written;  // per buffer: some plan writes it (never part of an upload run)
 
   fcx_engine() {
     for (auto &a : slot)
@@ -446,6 +460,7 @@ extern "C" int fcx_destroy(fcx_engine *e) {
   (void)hipFree(e->d_rec);
   (void)hipFree(e->pool);
   for (void *p : e->tiled_pools) (void)hipFree(p);
+  for (auto &sp : e->spans) (void)hipFree(sp.dev);
   if (e->ev0) (void)hipEventDestroy(e->ev0);
   if (e->ev1) (void)hipEventDestroy(e->ev1);
   for (hipEvent_t ev : e->ev_in) (void)hipEventDestroy(ev);
@@ -915,6 +930,7 @@ static int ravg_slot(const fcx_engine *e, const Params &P, uint32_t stages, int 
 // process() / uv_grid() in fcx_kernels.hip, restated on the parameter block.
 static int plan_audit(const fcx_engine *e, const Params &P) {
   const uint32_t st = P.stages;
+  if (P.n_max <= 0) return FCX_OK;  // nothing is launched (a rank with an empty task)
   auto need = [&](const void *ptr, int s, const char *what, const char *name) -> int {
     if (ptr) return FCX_OK;
     return fail(FCX_E_STATE, "plan audit: surface type %d: %s would read the unbound %s (stages 0x%x)", s, what, name,
@@ -925,7 +941,7 @@ static int plan_audit(const fcx_engine *e, const Params &P) {
     if (int r_ = need((ptr), s + 1, (what), (name))) return r_; \
   } while (0)
   auto cclm_like = [](int m) { return m == FCX_CCLM || m == FCX_MOM5; };
-  for (int s = 0; s < P.num_types; ++s) {
+  for (int s = 0; s < P.num_types && P.n[0] > 0; ++s) {
     const TypeParams &tp = P.type[s];
     const TGridPtrs &t = tp.t;
     const bool q_t = (st & S_QSUR_T) && tp.m_qsur[0] == FCX_CCLM;
@@ -993,6 +1009,7 @@ static int plan_audit(const fcx_engine *e, const Params &P) {
       }
     } else {
       for (int k = 0; k < 2; ++k) {
+        if (P.n[1 + k] <= 0) continue;
         const UVGridPtrs &g = tp.uv[k];
         const char *wq = k ? "QSUR(v)" : "QSUR(u)", *wm = k ? "VMOM" : "UMOM";
         const bool do_q = (st & (k == 0 ? S_QSUR_U : S_QSUR_V)) && tp.m_qsur[1 + k] == FCX_CCLM && g.qsur;
@@ -1316,26 +1333,66 @@ static int get_plan(fcx_engine *e, uint32_t stages, int avg_phases, Plan **pl) {
 // Library-owned page-locked host memory (fcx_host_malloc).  A host that allocates its
 // local_field arrays here hands the engine memory the library itself locked and mapped at
 // allocation, page-exclusive by construction and alive until fcx_host_free: the kernels can
-// use it in place (zero-copy, the default for small grids) and the copies of large grids
-// DMA from it directly, with no registration of caller memory at all.
+// use it in place (zero-copy) and the copies DMA from it directly, with no registration of
+// caller memory at all.
+//
+// Round 6: the blocks are carved from large page-locked slabs, 256-B aligned, one after the
+// other in call order.  A host that allocates its fields the way the reference does --
+// every input array first (flux_calculator.F90:436-560, allocate_localvar, basic:288-309),
+// then the outputs (do_prepare_calculation, prepare:36-42) -- thereby lays out each phase's
+// inputs as one span and its outputs as another, and an engine moves each span with ONE
+// copy per direction (the span transport, FCX_OPT_LIB_SPANS) instead of one per array.
 namespace {
 
+constexpr size_t kSlabBytes = size_t(32) << 20;  // smallest slab (one Baltic-size engine: ~9 MB)
+constexpr size_t kBlockAlign = 256;
+
+struct HostSlab {
+  char *host = nullptr, *dev = nullptr;  // page-locked, mapped for the device at allocation
+  size_t bytes = 0, used = 0;            // blocks go at `used`, in call order
+  int live = 0;
+};
 struct HostBlock {
-  size_t bytes;
-  void *dev;  // device-visible address of the block
+  size_t bytes;  // as requested
+  uintptr_t slab;
 };
 std::mutex g_blk_mu;
+std::map<uintptr_t, HostSlab> g_slabs;    // keyed by the slab's host address
 std::map<uintptr_t, HostBlock> g_blocks;  // keyed by the block's host address
+uintptr_t g_cur_slab = 0;                 // the slab new blocks go to (0: none)
+
+size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// the block holding [h, h + bytes), under g_blk_mu; end() if none
+std::map<uintptr_t, HostBlock>::const_iterator block_of(uintptr_t a, size_t bytes) {
+  auto it = g_blocks.upper_bound(a);
+  if (it == g_blocks.begin()) return g_blocks.end();
+  --it;
+  if (a + bytes > it->first + it->second.bytes) return g_blocks.end();
+  return it;
+}
 
 // device-visible address of [h, h + bytes) if it lies inside one fcx_host_malloc block
 void *lib_block_device_ptr(const void *h, size_t bytes) {
   const uintptr_t a = reinterpret_cast<uintptr_t>(h);
   std::lock_guard<std::mutex> lk(g_blk_mu);
-  auto it = g_blocks.upper_bound(a);
-  if (it == g_blocks.begin()) return nullptr;
-  --it;
-  if (a + bytes > it->first + it->second.bytes) return nullptr;
-  return reinterpret_cast<char *>(it->second.dev) + (a - it->first);
+  auto it = block_of(a, bytes);
+  if (it == g_blocks.end()) return nullptr;
+  const HostSlab &sl = g_slabs.at(it->second.slab);
+  return sl.dev + (a - reinterpret_cast<uintptr_t>(sl.host));
+}
+
+// the fcx_host_malloc block and slab holding [h, h + bytes): false if none
+struct LibBlock {
+  uintptr_t start = 0, end = 0, slab = 0;  // block [start, end) as requested, its slab
+};
+bool lib_block_of(const void *h, size_t bytes, LibBlock *out) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(h);
+  std::lock_guard<std::mutex> lk(g_blk_mu);
+  auto it = block_of(a, bytes);
+  if (it == g_blocks.end()) return false;
+  *out = LibBlock{it->first, it->first + it->second.bytes, it->second.slab};
+  return true;
 }
 
 }  // namespace
@@ -1343,31 +1400,52 @@ void *lib_block_device_ptr(const void *h, size_t bytes) {
 extern "C" int fcx_host_malloc(size_t bytes, void **ptr) {
   if (!ptr) return fail(FCX_E_ARG, "ptr is NULL");
   *ptr = nullptr;
-  void *h = nullptr, *d = nullptr;
-  hipError_t err = hipHostMalloc(&h, bytes ? bytes : 1, hipHostMallocMapped);
-  if (err != hipSuccess) return fail(FCX_E_NOMEM, "hipHostMalloc(%zu): %s", bytes, hipGetErrorString(err));
-  err = hipHostGetDevicePointer(&d, h, 0);
-  if (err != hipSuccess || !d) {
-    (void)hipHostFree(h);
-    return fail(FCX_E_HIP, "hipHostGetDevicePointer: %s", hipGetErrorString(err));
+  const size_t want = bytes ? bytes : 1, need = round_up(want, kBlockAlign);
+  std::lock_guard<std::mutex> lk(g_blk_mu);
+  HostSlab *sl = g_cur_slab ? &g_slabs.at(g_cur_slab) : nullptr;
+  if (!sl || sl->used + need > sl->bytes) {  // a new slab, the current one from now on
+    HostSlab ns;
+    ns.bytes = std::max(kSlabBytes, round_up(need, size_t(2) << 20));
+    void *h = nullptr, *d = nullptr;
+    hipError_t err = hipHostMalloc(&h, ns.bytes, hipHostMallocMapped);
+    if (err != hipSuccess) return fail(FCX_E_NOMEM, "hipHostMalloc(%zu): %s", ns.bytes, hipGetErrorString(err));
+    err = hipHostGetDevicePointer(&d, h, 0);
+    if (err != hipSuccess || !d) {
+      (void)hipHostFree(h);
+      return fail(FCX_E_HIP, "hipHostGetDevicePointer: %s", hipGetErrorString(err));
+    }
+    ns.host = static_cast<char *>(h);
+    ns.dev = static_cast<char *>(d);
+    g_cur_slab = reinterpret_cast<uintptr_t>(h);
+    sl = &(g_slabs[g_cur_slab] = ns);
   }
-  {
-    std::lock_guard<std::mutex> lk(g_blk_mu);
-    g_blocks[reinterpret_cast<uintptr_t>(h)] = HostBlock{bytes ? bytes : 1, d};
-  }
-  *ptr = h;
+  char *p = sl->host + sl->used;
+  sl->used += need;
+  ++sl->live;
+  g_blocks[reinterpret_cast<uintptr_t>(p)] = HostBlock{want, reinterpret_cast<uintptr_t>(sl->host)};
+  *ptr = p;
   return FCX_OK;
 }
 
 extern "C" int fcx_host_free(void *ptr) {
   if (!ptr) return FCX_OK;
+  void *slab_host = nullptr;
   {
     std::lock_guard<std::mutex> lk(g_blk_mu);
     auto it = g_blocks.find(reinterpret_cast<uintptr_t>(ptr));
     if (it == g_blocks.end()) return fail(FCX_E_ARG, "%p was not allocated by fcx_host_malloc", ptr);
+    HostSlab &sl = g_slabs.at(it->second.slab);
+    const uintptr_t a = it->first, end = a + round_up(it->second.bytes, kBlockAlign);
+    if (end == reinterpret_cast<uintptr_t>(sl.host) + sl.used) sl.used = a - reinterpret_cast<uintptr_t>(sl.host);
+    const uintptr_t key = it->second.slab;
     g_blocks.erase(it);
+    if (--sl.live == 0) {  // the slab's last block: the slab goes back
+      slab_host = sl.host;
+      g_slabs.erase(key);
+      if (g_cur_slab == key) g_cur_slab = 0;
+    }
   }
-  HIP_TRY(hipHostFree(ptr));
+  if (slab_host) HIP_TRY(hipHostFree(slab_host));
   return FCX_OK;
 }
 
@@ -1414,6 +1492,123 @@ static int map_host_arrays(fcx_engine *e) {
   return count;
 }
 
+// The span transport: every fcx_host_malloc array not used in place gets its mirror in the
+// device buffer of its slab's span (Span), at its host offset.  Returns the arrays mapped.
+static int map_lib_spans(fcx_engine *e, int *count) {
+  *count = 0;
+  const size_t es = e->esize;
+  std::map<uintptr_t, std::vector<int>> by_slab;
+  for (size_t b = 0; b < e->bufs.size(); ++b) {
+    const Buffer &bf = e->bufs[b];
+    if (bf.external || !bf.host || bf.n <= 0) continue;
+    LibBlock lb;
+    if (lib_block_of(bf.host, (size_t)bf.n * es, &lb)) by_slab[lb.slab].push_back((int)b);
+  }
+  for (auto &kv : by_slab) {
+    uintptr_t lo = UINTPTR_MAX, hi = 0;
+    for (int b : kv.second) {
+      const uintptr_t h = reinterpret_cast<uintptr_t>(e->bufs[(size_t)b].host);
+      lo = std::min(lo, h);
+      hi = std::max(hi, h + (size_t)e->bufs[(size_t)b].n * es);
+    }
+    lo &= ~uintptr_t(kBlockAlign - 1);  // (device offsets keep the host's alignment mod 256)
+    Span sp;
+    sp.lo = lo;
+    sp.bytes = hi - lo;
+    hipError_t err = hipMalloc((void **)&sp.dev, sp.bytes);
+    if (err != hipSuccess)
+      return fail(FCX_E_NOMEM, "hipMalloc(%zu) for a span of fcx_host_malloc arrays: %s", sp.bytes,
+                  hipGetErrorString(err));
+    const int id = (int)e->spans.size();
+    e->spans.push_back(sp);
+    for (int b : kv.second) {
+      Buffer &bf = e->bufs[(size_t)b];
+      bf.dev = reinterpret_cast<double *>(sp.dev + (reinterpret_cast<uintptr_t>(bf.host) - lo));
+      bf.external = true;  // not in the engine's pools (the tiled layout is off for it)
+      bf.span = id;
+      if (reinterpret_cast<uintptr_t>(bf.dev) % 16) e->aligned16 = false;
+      ++*count;
+    }
+  }
+  return FCX_OK;
+}
+
+// per buffer: written by some plan (a flux output, a type-0 average, a regrid destination)
+static void classify_written(fcx_engine *e) {
+  static const int kOut[] = {FCX_QSUR, FCX_MEVA, FCX_HLAT, FCX_HSEN, FCX_RBBR, FCX_UMOM, FCX_VMOM, FCX_RSDR};
+  e->written.assign(e->bufs.size(), 0);
+  for (int s = 0; s <= e->T; ++s)
+    for (int g = 1; g <= 3; ++g) {
+      for (int v : kOut)
+        if (e->buf(s, g, v) >= 0) e->written[(size_t)e->buf(s, g, v)] = 1;
+      for (int v = 1; v <= kNumVars; ++v)
+        for (int k = 0; k < 3; ++k)
+          if (((e->put_to[s][g - 1][v - 1] >> k) & 1) && e->buf(s, k + 1, v) >= 0)
+            e->written[(size_t)e->buf(s, k + 1, v)] = 1;
+    }
+  for (auto &a : e->averages)
+    if (e->buf(0, a.second.first, a.second.second) >= 0) e->written[(size_t)e->buf(0, a.second.first, a.second.second)] = 1;
+}
+
+// May a copy run continue from host address r1 (one array's end) over the gap to b0 (the next
+// array's start)?  Downloads write the host bytes: only over the 256-B padding between two
+// consecutive fcx_host_malloc blocks, where no block can ever lie.  Uploads write device bytes
+// only: over any gap up to kUploadGap that holds none of the engine's written arrays (whose
+// mirrors may hold results not yet downloaded); the rest of the gap -- other inputs, free
+// slab, other engines' arrays -- lands in span bytes no mirror of this engine uses or in
+// mirrors of inputs, with the host's own values.
+constexpr size_t kUploadGap = size_t(256) << 10;
+static bool span_gap_ok(const fcx_engine *e, int span, uintptr_t r1, uintptr_t b0, bool h2d) {
+  if (b0 <= r1) return true;
+  if (h2d) {
+    if (b0 - r1 > kUploadGap) return false;
+    for (size_t b = 0; b < e->bufs.size(); ++b) {
+      const Buffer &bf = e->bufs[b];
+      if (bf.span != span || !e->written[b]) continue;
+      const uintptr_t h = reinterpret_cast<uintptr_t>(bf.host), z = h + (size_t)bf.n * e->esize;
+      if (h < b0 && z > r1) return false;
+    }
+    return true;
+  }
+  if (b0 - r1 >= kBlockAlign) return false;
+  LibBlock a, b;
+  if (!lib_block_of(reinterpret_cast<const void *>(r1 - 1), 1, &a) || !lib_block_of(reinterpret_cast<const void *>(b0), 1, &b))
+    return false;
+  return a.end == r1 && b.start == b0 && a.slab == b.slab && round_up(a.end, kBlockAlign) == b0;
+}
+
+// the span copies of buffers `ids` (span arrays only): sorted by host address, every run of
+// arrays the gap rule joins as ONE hipMemcpyAsync.  runs: the number of copies (queued only
+// when s is not null)
+static int span_copy(fcx_engine *e, std::vector<int> ids, bool h2d, hipStream_t s, int *runs = nullptr) {
+  const size_t es = e->esize;
+  std::sort(ids.begin(), ids.end(), [&](int x, int y) { return e->bufs[(size_t)x].host < e->bufs[(size_t)y].host; });
+  int nr = 0;
+  for (size_t i = 0; i < ids.size();) {
+    const Buffer &a = e->bufs[(size_t)ids[i]];
+    const int sp = a.span;
+    const uintptr_t r0 = reinterpret_cast<uintptr_t>(a.host);
+    uintptr_t r1 = r0 + (size_t)a.n * es;
+    size_t j = i + 1;
+    for (; j < ids.size(); ++j) {
+      const Buffer &b = e->bufs[(size_t)ids[j]];
+      const uintptr_t b0 = reinterpret_cast<uintptr_t>(b.host);
+      if (b.span != sp || !span_gap_ok(e, sp, r1, b0, h2d)) break;
+      r1 = std::max(r1, b0 + (size_t)b.n * es);
+    }
+    ++nr;
+    if (s) {
+      const Span &p = e->spans[(size_t)sp];
+      char *d = p.dev + (r0 - p.lo);
+      char *h = reinterpret_cast<char *>(r0);
+      HIP_TRY(h2d ? hipMemcpyAsync(d, h, r1 - r0, hipMemcpyDefault, s) : hipMemcpyAsync(h, d, r1 - r0, hipMemcpyDefault, s));
+    }
+    i = j;
+  }
+  if (runs) *runs = nr;
+  return FCX_OK;
+}
+
 // Tile-blocked mirrors (FCX_OPT_TILED_LAYOUT).  Every field array is cut into tiles of
 // kLayoutTile cells; tile t of all arrays of one pool sits together: array k of the pool at
 // element t * S * kLayoutTile + k * kLayoutTile, S = slots per tile, the same S for every
@@ -1433,16 +1628,18 @@ static int alloc_tiled(fcx_engine *e) {
   static const int kOut[] = {FCX_QSUR, FCX_MEVA, FCX_HLAT, FCX_HSEN, FCX_RBBR, FCX_UMOM, FCX_VMOM, FCX_RSDR};
   enum { kRead = 0, kWrite = 1, kCold = 2 };
   std::vector<int> cls(e->bufs.size(), kCold);
-  {  // the whole-step plan's read and write sets (pointers are not assigned yet: dropped)
+  {  // the whole-step plan's read and write sets: built on the host only (plan_dry: the
+     // mirrors do not exist yet, tag addresses stand in for them), then dropped
     Plan p;
     const std::string saved = g_err;
+    e->plan_dry = true;
     if (build_plan(e, phase_stages(FCX_PHASE_EARLY | FCX_PHASE_NORMAL), FCX_PHASE_EARLY | FCX_PHASE_NORMAL, p) ==
         FCX_OK) {
       for (int b : p.reads) cls[b] = kRead;
       for (int b : p.writes) cls[b] = kWrite;
     }
+    e->plan_dry = false;
     g_err = saved;
-    (void)hipFree(p.dev);
   }
   for (int s = 0; s <= e->T; ++s)  // outputs of other phases / staged launches
     for (int g = 1; g <= 3; ++g)
@@ -1959,12 +2156,20 @@ extern "C" int fcx_commit(fcx_engine *e) {
   const int64_t n_big = std::max(e->n[0], std::max(e->n[1], e->n[2]));
   const bool small = n_big < 2 * e->min_chunk;
   if (e->zero_copy == 1 || (e->zero_copy == 2 && small)) {
-    e->zc_active = map_host_arrays(e) > 0;
+    // fcx_host_malloc arrays: in place when asked for (1); in auto mode the span transport
+    // takes them when it is on (one copy per direction beats the kernels' own reads over the
+    // link, whose two directions do not overlap: DESIGN.md section 7)
+    if (!(e->lib_spans && e->zero_copy == 2)) e->zc_active = map_host_arrays(e) > 0;
     int staged = 0;
     if (e->staging)
       if (int r = map_staged(e, &staged)) return r;
     e->zc_active = e->zc_active || staged > 0;
   }
+  if (e->lib_spans) {
+    int spanned = 0;
+    if (int r = map_lib_spans(e, &spanned)) return r;
+  }
+  classify_written(e);
   bool any_external = false;
   for (auto &bf : e->bufs) any_external = any_external || bf.external;
   if (e->tiled_opt && !any_external && !e->bufs.empty()) {
@@ -2209,6 +2414,8 @@ static int copy_bufs(fcx_engine *e, const std::vector<int> &ids, bool h2d, std::
   stage_prepare_bufs(e, ids);
   std::vector<Xfer> xs;
   if (more) xs.swap(*more);
+  std::vector<int> spanned;
+  bool direct = false;
   for (int b : ids) {
     const Buffer &bf = e->bufs[b];
     if (bf.n == 0) continue;
@@ -2217,10 +2424,24 @@ static int copy_bufs(fcx_engine *e, const std::vector<int> &ids, bool h2d, std::
       xs.push_back(xfer_of(bf.st, bf.host, bf.n));
       continue;
     }
+    if (bf.span >= 0) {
+      spanned.push_back(b);
+      continue;
+    }
     if (bf.external) continue;
     HIP_TRY(copy_cells(e, bf, 0, bf.n, h2d, e->stream));
+    direct = true;
   }
-  return h2d ? stage_in(e, xs, e->stream) : stage_out(e, xs, e->stream);
+  if (!spanned.empty()) {
+    if (int r = span_copy(e, spanned, h2d, e->stream)) return r;
+    direct = true;
+  }
+  if (h2d) return stage_in(e, xs, e->stream);
+  if (xs.empty() && direct && !e->deferred_scatter) {  // the outputs in the arrays on return
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    return stage_flush(e);
+  }
+  return stage_out(e, xs, e->stream);
 }
 
 #ifndef FCX_ZC_ONE_CELL  // A/B builds: 0 keeps 16-B (2-cell) lanes in zero-copy launches
@@ -2361,7 +2582,7 @@ static int upload_one(fcx_engine *e, int b) {
       HIP_TRY(stage_dma(e, xs, 0, -1, true, e->stream));
       u.dma = true;
     }
-  } else if (!bf.external) {
+  } else if (!bf.external || bf.span >= 0) {
     HIP_TRY(copy_cells(e, bf, 0, bf.n, true, e->stream));
   }
   return FCX_OK;
@@ -2785,7 +3006,7 @@ static int launch_group(const GroupLaunchMember *mem, int nm) {
 // copy the part [lo, hi) of a host-bound buffer (the last chunk also takes the array tail)
 static int copy_slice(fcx_engine *e, const Buffer &bf, int64_t lo, int64_t hi, bool last, bool h2d,
                       hipStream_t s) {
-  if (bf.external || bf.n == 0) return FCX_OK;
+  if ((bf.external && bf.span < 0) || bf.n == 0) return FCX_OK;
   const int64_t a = std::min(lo, bf.n), z = last ? bf.n : std::min(hi, bf.n);
   if (z <= a) return FCX_OK;
   HIP_TRY(copy_cells(e, bf, a, z, h2d, s));
@@ -2834,13 +3055,13 @@ static int step_pipelined(fcx_engine *e, int phase, int32_t t, Plan *pl) {
     const Buffer &bf = e->bufs[b];
     if (bf.n == 0) continue;
     if (bf.st.sp >= 0) xin.push_back(xfer_of(bf.st, bf.host, bf.n));
-    else if (!bf.external) din.push_back(b);
+    else if (!bf.external || bf.span >= 0) din.push_back(b);
   }
   for (int b : pl->writes) {
     const Buffer &bf = e->bufs[b];
     if (bf.n == 0) continue;
     if (bf.st.sp >= 0) xout.push_back(xfer_of(bf.st, bf.host, bf.n));
-    else if (!bf.external) dout.push_back(b);
+    else if (!bf.external || bf.span >= 0) dout.push_back(b);
   }
   if (!xin.empty() || !xout.empty()) {
     if (int r = stage_alloc(e, xin)) return r;
@@ -2927,9 +3148,9 @@ static int step_pipelined(fcx_engine *e, int phase, int32_t t, Plan *pl) {
 
 static bool host_bound(const fcx_engine *e, const Plan *pl) {
   for (int b : pl->reads)
-    if (!e->bufs[b].external || e->bufs[b].st.sp >= 0) return true;
+    if (!e->bufs[b].external || e->bufs[b].st.sp >= 0 || e->bufs[b].span >= 0) return true;
   for (int b : pl->writes)
-    if (!e->bufs[b].external || e->bufs[b].st.sp >= 0) return true;
+    if (!e->bufs[b].external || e->bufs[b].st.sp >= 0 || e->bufs[b].span >= 0) return true;
   return false;
 }
 
@@ -3118,6 +3339,23 @@ extern "C" int fcx_handoff_recoveries(fcx_engine *e, int64_t *count) {
   return FCX_OK;
 }
 
+extern "C" int fcx_span_runs(fcx_engine *e, int phase, int32_t *h2d_copies, int32_t *d2h_copies) {
+  if (int r = check(e)) return r;
+  if (phase < 1 || phase > 3 || !h2d_copies || !d2h_copies) return fail(FCX_E_ARG, "bad arguments");
+  Plan *pl;
+  if (int r = get_plan(e, phase_stages(phase), phase, &pl)) return r;
+  int n[2] = {0, 0};
+  for (int k = 0; k < 2; ++k) {
+    std::vector<int> ids;
+    for (int b : k ? pl->writes : pl->reads)
+      if (e->bufs[(size_t)b].span >= 0 && e->bufs[(size_t)b].n > 0) ids.push_back(b);
+    if (int r = span_copy(e, ids, k == 0, nullptr, &n[k])) return r;
+  }
+  *h2d_copies = n[0];
+  *d2h_copies = n[1];
+  return FCX_OK;
+}
+
 extern "C" int fcx_zero_copy_bytes(fcx_engine *e, int64_t *bytes) {
   if (int r = check(e)) return r;
   if (!bytes) return fail(FCX_E_ARG, "NULL argument");
@@ -3222,6 +3460,11 @@ extern "C" int fcx_set_option(fcx_engine *e, int option, int64_t value) {
     case FCX_OPT_TIMING:
       e->timing = value != 0;
       if (!e->timing) e->timed = false;
+      return FCX_OK;
+    case FCX_OPT_LIB_SPANS:
+      if (e->committed) return fail(FCX_E_STATE, "lib_spans is applied at fcx_commit");
+      if (value < 0 || value > 1) return fail(FCX_E_ARG, "lib_spans: 0 or 1");
+      e->lib_spans = value != 0;
       return FCX_OK;
     case FCX_OPT_ZERO_COPY:
       if (e->committed) return fail(FCX_E_STATE, "zero_copy is applied at fcx_commit");

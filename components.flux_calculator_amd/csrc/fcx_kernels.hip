@@ -384,7 +384,10 @@ __device__ __forceinline__ void process(const Params *__restrict__ P, const doub
   // SIMD, no spills.  In one process over the same arrays (profiles/r03/ab_t2_prefetch.json,
   // random map): T = 2 step 1.672 -> 1.625 ms, CCLM 5.14 -> 5.26 TB/s, MOM5 5.54 -> 5.67,
   // RCO 5.26 -> 5.50.
-  constexpr bool kPrefetch = kReload;
+#ifndef FCX_T2_PREFETCH  // A/B builds: 0 = no next-type prefetch (24 fewer VGPRs)
+#define FCX_T2_PREFETCH 1
+#endif
+  constexpr bool kPrefetch = kReload && FCX_T2_PREFETCH;
   // Multi-type CCLM / MOM5 kernels: the atmosphere-only terms of the formulas are formed once
   // per cell, when the type's atmosphere fields are (re)loaded, instead of once per type:
   // T_a * EF (HSEN's pow, ta_exner) and, for CCLM, whose coefficients AMOI / AMOM are

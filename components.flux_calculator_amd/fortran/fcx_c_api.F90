@@ -24,7 +24,8 @@ MODULE fcx_c_api
                                FCX_OPT_PIPELINE_CHUNKS = 7, FCX_OPT_ZERO_COPY = 9, FCX_OPT_TIMING = 10, &
                                FCX_OPT_TILED_LAYOUT = 11, FCX_OPT_REMAP_PACK = 13, &
                                FCX_OPT_HOST_STAGING = 15, FCX_OPT_HOST_THREADS = 16, &
-                               FCX_OPT_ATMOS_HALO = 17, FCX_OPT_DEFERRED_SCATTER = 18
+                               FCX_OPT_ATMOS_HALO = 17, FCX_OPT_DEFERRED_SCATTER = 18, &
+                               FCX_OPT_LIB_SPANS = 19
   ! retired in version 3: accepted by fcx_set_option and ignored
   INTEGER(c_int), PARAMETER :: FCX_OPT_PIN_HOST = 6, FCX_OPT_CARRY_HANDOFF = 14
   ! the RCCL unique id travels between the ranks as these many bytes (MPI_Bcast)

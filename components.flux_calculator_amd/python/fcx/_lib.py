@@ -67,6 +67,7 @@ SIGNATURES = [
     ("fcx_last_kernel_ms", _I, [_P, _c.POINTER(_c.c_float)]),
     ("fcx_staging_bytes", _I, [_P, _c.POINTER(_I64)]),
     ("fcx_algorithmic_bytes", _I, [_P, _I, _c.POINTER(_I64)]),
+    ("fcx_span_runs", _I, [_P, _I, _c.POINTER(_I32), _c.POINTER(_I32)]),
     ("fcx_zero_copy_bytes", _I, [_P, _c.POINTER(_I64)]),
     ("fcx_run_group", _I, [_P, _I, _I, _I32]),
     ("fcx_pinned_bytes", _I, [_P, _c.POINTER(_I64)]),

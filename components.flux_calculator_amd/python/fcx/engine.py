@@ -192,13 +192,20 @@ class Engine:
         _lib.check(self.lib.fcx_zero_copy_bytes(self.h, ctypes.byref(b)))
         return b.value
 
+    def span_runs(self, phase=PHASE_ALL):
+        """(uploads, downloads) one step of the phase makes of the fcx_host_malloc arrays with
+        the span transport (fcx_span_runs)"""
+        a, b = ctypes.c_int32(), ctypes.c_int32()
+        _lib.check(self.lib.fcx_span_runs(self.h, phase, ctypes.byref(a), ctypes.byref(b)))
+        return a.value, b.value
+
     def zero_copy_active(self):
         return self.zero_copy_bytes() > 0
 
     OPTIONS = {"cells_per_thread": 1, "max_blocks": 2, "nontemporal": 3, "specialize": 4,
                "atmos_in_run": 5, "pipeline_chunks": 7, "pipeline_min_chunk": 8, "zero_copy": 9,
                "timing": 10, "tiled_layout": 11, "remap_pack": 13, "host_staging": 15, "host_threads": 16,
-               "atmos_halo": 17, "deferred_scatter": 18}
+               "atmos_halo": 17, "deferred_scatter": 18, "lib_spans": 19}
 
     def run_atmos(self, phase=PHASE_ALL):
         _lib.check(self.lib.fcx_run_atmos(self.h, phase))

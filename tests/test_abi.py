@@ -178,7 +178,10 @@ def test_remap_and_staging_options_before_commit():
     for gone in (6, 12, 14):
         _lib.check(lib.fcx_set_option(h, gone, 1))
         _lib.check(lib.fcx_set_option(h, gone, 0))
-    assert lib.fcx_set_option(h, 19, 1) == 1  # FCX_E_ARG: unknown
+    for v in (0, 1):
+        _lib.check(lib.fcx_set_option(h, 19, v))  # FCX_OPT_LIB_SPANS
+    assert lib.fcx_set_option(h, 19, 2) == 1
+    assert lib.fcx_set_option(h, 20, 1) == 1  # FCX_E_ARG: unknown
     for v in (0, 1):
         _lib.check(lib.fcx_set_option(h, 18, v))  # FCX_OPT_DEFERRED_SCATTER
     b = ctypes.c_int64(7)

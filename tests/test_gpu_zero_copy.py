@@ -185,14 +185,20 @@ def test_library_arrays_per_call_chain():
 
 @pytest.mark.parametrize("variant", ["CCLM", "MOM5", "RCO"])
 @pytest.mark.parametrize("n", [4097, 32_768])
-def test_library_pinned_arrays_zero_copy(variant, n):
-    """Arrays allocated by fcx_host_malloc are used in place by default (auto zero-copy:
-    page-locked and mapped by the library itself, no registration of caller memory)."""
+@pytest.mark.parametrize("transport", ["spans", "zero_copy"])
+def test_library_pinned_arrays(variant, n, transport):
+    """Arrays allocated by fcx_host_malloc (page-locked and mapped by the library itself, no
+    registration of caller memory): by default the span transport moves them (device mirrors
+    laid out like the host memory, one copy per run of adjacent arrays); FCX_OPT_ZERO_COPY 1
+    uses them in place."""
     c = build_case(variant, n=n, T=2, bias=True)
     with host_alloc.Arena() as arena:
         arena.adopt(c.lf)
-        e = engine_for(c)
-        assert e.zero_copy_active()
+        e = engine_for(c) if transport == "spans" else engine_for(c, zero_copy=1)
+        assert e.zero_copy_active() == (transport == "zero_copy")
+        if transport == "spans":
+            up, down = e.span_runs()
+            assert 1 <= up <= 2 and down == 1, (up, down)
         assert e.staging_bytes() == 0  # library memory: no staging arena either
         for k in range(3):
             reset_outputs(c)
@@ -276,3 +282,111 @@ def test_recycled_virtual_address_between_engines(variant):
         eb.close()
     finally:
         libc.munmap(addr, size)
+
+
+SPAN_MODES = ["step", "step_async", "per_call", "upload_field"]
+
+
+def _run_mode(case, eng, mode, t):
+    lib, h = eng.lib, eng.h
+    if mode == "step":
+        eng.step(PHASE_ALL, t)
+    elif mode == "step_async":
+        eng.step_async(PHASE_ALL, t)
+        eng.synchronize()
+    elif mode == "upload_field":
+        outs = {id(case.lf.field[k]) for k in case.outputs}
+        seen = set()
+        for key, a in case.lf.field.items():
+            if id(a) not in outs and id(a) not in seen and key[0] >= 1:
+                seen.add(id(a))
+                eng.upload_field(*key)
+        eng.step(PHASE_ALL, t)
+    else:
+        from fcx.basic import IDX
+
+        assert lib.fcx_calc_flux_radiation_blackbody(h) == 0, lib.fcx_last_error()
+        for g in (1, 2, 3):
+            assert lib.fcx_calc_spec_vapor_surface(h, g) == 0
+        assert lib.fcx_calc_flux_mass_evap(h, t) == 0
+        assert lib.fcx_calc_flux_heat_latent(h) == 0
+        assert lib.fcx_calc_flux_heat_sensible(h) == 0
+        assert lib.fcx_calc_flux_momentum_east(h, 2) == 0
+        assert lib.fcx_calc_flux_momentum_north(h, 3) == 0
+        for ph, g, name in case.averages:
+            assert lib.fcx_average_across_surface_types(h, g, IDX[name]) == 0
+
+
+@pytest.mark.parametrize("mode", SPAN_MODES)
+@pytest.mark.parametrize("variant,T,n", [("CCLM", 1, 32_768), ("MOM5", 2, 4_099), ("RCO", 3, 1_001),
+                                         ("CCLM", 2, 600_000)])
+def test_span_transport_bit_identical_to_heap_arrays(variant, T, n, mode):
+    """the span transport of fcx_host_malloc arrays (one upload and one
+    download per run of adjacent arrays; the chunk pipeline at 600,000 cells) gives outputs
+    bit-identical to the same case from caller heap arrays, in every way a host drives the
+    engine: fcx_step, fcx_step_async + fcx_synchronize, the per-call subroutines, fields
+    handed over one by one -- over two steps with the inputs changed in between."""
+    t = 3600 * 24 * 31
+    heap = build_case(variant, n=n, T=T, bias=True, seed=17)
+    lib_case = build_case(variant, n=n, T=T, bias=True, seed=17)
+    with host_alloc.Arena() as arena:
+        arena.adopt(lib_case.lf)
+        e_heap = engine_for(heap)
+        e_lib = engine_for(lib_case)
+        assert not e_lib.zero_copy_active() and e_lib.staging_bytes() == 0
+        for step in range(2):
+            for c in (heap, lib_case):
+                reset_outputs(c)
+                if step:
+                    for key in ("TSUR", "TATM", "UATM"):
+                        for s in range(0, T + 1):
+                            if (s, 1, key) in c.lf.field:
+                                a = c.lf.field[(s, 1, key)]
+                                a[:] = a * (1.0 + 1e-4)
+            _run_mode(heap, e_heap, mode, t)
+            _run_mode(lib_case, e_lib, mode, t)
+            for k in heap.outputs:
+                a, b = np.asarray(heap.lf.field[k]), np.asarray(lib_case.lf.field[k])
+                assert np.array_equal(a, b, equal_nan=True), (k, mode, step)
+        check(lib_case, f"spans {variant} T={T} {mode}")
+        e_heap.close()
+        e_lib.close()
+
+
+def test_span_runs_follow_the_allocation_order():
+    """Arrays allocated inputs first, then outputs (the reference's order: allocate_localvar
+    for every input, flux_calculator.F90:436-560, then do_prepare_calculation for the outputs,
+    prepare:36-42) move as ONE upload and ONE download per step; the same arrays allocated
+    with the outputs interleaved between the inputs take more copies, and unbound gaps between
+    outputs are never written by a download."""
+    c = build_case("CCLM", n=32_768, T=1, bias=False, seed=3)
+    outs = {id(c.lf.field[k]) for k in c.outputs}
+    with host_alloc.Arena() as arena:
+        arena.adopt(c.lf)  # dict order: inputs, then outputs
+        e = engine_for(c)
+        assert e.span_runs() == (1, 1)
+        e.close()
+    c2 = build_case("CCLM", n=32_768, T=1, bias=False, seed=3)
+    with host_alloc.Arena() as arena:
+        moved, guards = {}, []
+        for key, a in list(c2.lf.field.items()):  # interleaved: a guard block after every output
+            if id(a) in moved:
+                c2.lf.field[key] = moved[id(a)]
+                continue
+            v = arena.empty(a.shape[0], a.dtype)
+            v[:] = a
+            moved[id(a)] = v
+            c2.lf.field[key] = v
+            if id(a) in outs:
+                g = arena.empty(64)
+                g[:] = 12345.0
+                guards.append(g)
+        e = engine_for(c2)
+        up, down = e.span_runs()
+        assert down > 1, (up, down)
+        reset_outputs(c2)
+        e.step(PHASE_ALL, T_STEP)
+        check(c2, "spans with guards between the outputs")
+        for g in guards:
+            assert np.all(g == 12345.0)
+        e.close()
