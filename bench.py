@@ -69,6 +69,9 @@ def parse():
     p.add_argument("--collective", choices=("rccl", "torch"), default="rccl",
                    help="N > 1: the boundary all-reduce through libfcx's RCCL communicator (default) or "
                         "torch.distributed (rehearsals)")
+    p.add_argument("--config5", type=int, default=1,
+                   help="N = 1, fp64 line: also time the fp32 variant of the same workload (BASELINE config 5's "
+                        "fp32 kernels, a 'config5_fp32' sub-object; never the `value`)")
     p.add_argument("--config4", type=int, default=40_000_000,
                    help="also time config 4's fixed grid of this many cells sharded over the ranks "
                         "(strong scaling, a 'config4' sub-object); 0 = off")
@@ -363,10 +366,10 @@ def e2e_library_memory(args, variants, n=32_768, steps=500):
     """The Baltic-size step with the fields in fcx_host_malloc memory -- a host that allocates
     its local_field arrays from the library (c_f_pointer) instead of
     its own heap, inputs first and outputs after them as the reference allocates them
-    (flux_calculator.F90:436-560, then prepare:36-42).  Two transports: the span transport
-    (the default: device mirrors laid out like the host memory, ONE upload and ONE download per
-    engine and step) and zero-copy (FCX_OPT_ZERO_COPY 1: the kernels read and write the arrays
-    in place over the link).  Median wall time per step of the variants one after the other
+    (flux_calculator.F90:436-560, then prepare:36-42).  Two transports: zero-copy (the default
+    at this size: the kernels read and write the arrays in place over the link) and the span
+    transport (FCX_OPT_ZERO_COPY 0: device mirrors laid out like the host memory, one or two
+    uploads and ONE download per engine and step).  Median wall time per step of the variants one after the other
     (fcx_step) and started together (fcx_step_async from one thread, each engine on its own
     stream, then fcx_synchronize of each)."""
     import torch
@@ -377,7 +380,7 @@ def e2e_library_memory(args, variants, n=32_768, steps=500):
 
     data = inputs_for_bench(n)
     res = {}
-    for transport, opts in (("spans", {}), ("zero_copy", {"zero_copy": 1})):
+    for transport, opts in (("zero_copy", {}), ("spans", {"zero_copy": 0})):
         streams = [torch.cuda.Stream() for _ in variants]
         cases = [build_case(v, n=n, T=args.types, bias=args.bias, data=data if args.types == 1 else None)
                  for v in variants]
@@ -409,9 +412,9 @@ def e2e_library_memory(args, variants, n=32_768, steps=500):
                 e.close()
         res[transport] = out
     res.update(steps=steps, engines=len(variants),
-               transports="spans: device mirrors laid out like the host memory, one copy per run of adjacent arrays "
-                          "(the default for fcx_host_malloc arrays); zero_copy: the kernels use the arrays in place "
-                          "(FCX_OPT_ZERO_COPY 1)",
+               transports="zero_copy: the kernels use the arrays in place (the default at this size); spans: "
+                          "device mirrors laid out like the host memory, one copy per run of adjacent arrays "
+                          "(FCX_OPT_ZERO_COPY 0)",
                rule="sequential: fcx_step of each variant in turn; async: fcx_step_async of each from one host "
                     "thread, then fcx_synchronize of each; a step = first start to the last engine done")
     return res
@@ -785,6 +788,34 @@ def main():
         del wo, wl
         torch.cuda.synchronize()
 
+    # config 5's fp32 kernels on the same workload (N = 1): Mcells/s and the roofline fraction
+    # of the step's one launch, next to the fp64 line
+    if args.config5 and world == 1 and not f32 and args.atmos:
+        w5 = Workload(n_global, rank, world, variants, types=args.types, bias=args.bias, precision="f32",
+                      atmos=True, caller_device=args.caller_device, device=gpu, atmos_map=args.atmos_map,
+                      stream=torch.cuda.current_stream(dev), engine_options=engine_options)
+        wl = w5
+        m5 = measure(w5, args, world, dist, None, args.steps, args.warmup)
+        k5, d5 = m5["kern_mean"], m5["dom"]
+        g5 = m5["group_ms"]
+        out["config5_fp32"] = {
+            "workload": "the same synthetic grid and variants in the fp32 engine (BASELINE configs[4]'s fp32 kernel "
+                        "variant): fp32 fields and arithmetic, the accumulation's weights, products and sums in fp64",
+            "value": round(n_global * len(variants) * args.steps / m5["t_max"] / 1e6, 1),
+            "unit": "Mcells/s",
+            "ms_per_step": round(m5["t_max"] / args.steps * 1e3, 4),
+            "alg_bytes_per_step": int(sum(w5.alg_bytes)),
+            "frac": round(sum(w5.alg_bytes) / ((g5 if g5 is not None else float(k5[d5])) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "kernel_ms": round(g5 if g5 is not None else float(k5[d5]), 4),
+            "dtype": "f32",
+            "tolerance": "tests/test_gpu_fp32.py: the kernel's arithmetic within 64 fp32 ulps of the fp64 oracle on "
+                         "the same rounded inputs, or 4x the oracle's movement under 16-ulp perturbations "
+                         "(profiles/r06/.../fp32_error_*.json)",
+        }
+        w5.close()
+        del w5, wl
+        torch.cuda.synchronize()
+
     # config 4 at this N: the fixed 40M-cell grid over the same ranks (strong scaling)
     if args.config4 and not args.global_cells:
         w4 = Workload(args.config4, rank, world, variants, types=1, precision=args.precision,
@@ -896,11 +927,10 @@ def main():
                                                             "overlap (the engines' own copies do overlap them in part, "
                                                             "DESIGN.md section 7); the host copies between the caller's "
                                                             "arrays and page-locked memory come on top of either")
-                # the library-memory step against the link's duplex floor (VERDICT r05 item 2:
-                # the span transport's target is <= 1.2 x bound_duplex_us)
+                # the library-memory step against the link's duplex floor
                 out["baltic_size"]["gpu_library_memory_vs_duplex_floor"] = {
-                    f"spans_{mode}": round(lib["spans"][f"{mode}_us_per_step_median"] / max(duplex, 1e-9), 3)
-                    for mode in ("sequential", "async")}
+                    f"{tr}_{mode}": round(lib[tr][f"{mode}_us_per_step_median"] / max(duplex, 1e-9), 3)
+                    for tr in ("zero_copy", "spans") for mode in ("sequential", "async")}
     if rank == 0:
         print(json.dumps(out), flush=True)
     if comm is not None:

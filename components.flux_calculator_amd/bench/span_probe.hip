@@ -15,8 +15,9 @@
 //   duplex_k   as duplex, the kernels on stream A after each upload (no cross-stream wait
 //              before a kernel; B waits for the kernel's event before the download)
 //   one_span   all three engines' inputs as ONE copy, the kernels, ONE download
-// argv: cells (32768), reps (300), host flags ("mapped": hipHostMallocMapped as fcx_host_malloc
-// slabs, else hipHostMallocDefault).
+// argv: cells (32768), reps (300), host flags: default | mapped | portable | mapped_portable
+// (hipHostMalloc flags; round 6: device->host copies into default or mapped memory run at
+// ~23 GB/s, into portable memory at ~52 GB/s -- bench/d2h_flags_probe.hip).
 //
 //   hipcc --offload-arch=gfx950 -O2 span_probe.hip -o span_probe && ./span_probe 32768 300 mapped
 #include <hip/hip_runtime.h>
@@ -61,7 +62,11 @@ struct Eng {
 int main(int argc, char **argv) {
   const int n = argc > 1 ? std::atoi(argv[1]) : 32768;
   const int reps = argc > 2 ? std::atoi(argv[2]) : 300;
-  const bool mapped = argc > 3 && std::string(argv[3]) == "mapped";
+  const std::string hf = argc > 3 ? argv[3] : "default";
+  const unsigned hflags = hf == "mapped" ? hipHostMallocMapped
+                          : hf == "portable" ? hipHostMallocPortable
+                          : hf == "mapped_portable" ? (hipHostMallocMapped | hipHostMallocPortable)
+                                                    : hipHostMallocDefault;
   const int shape[3][2] = {{10, 7}, {11, 7}, {5, 6}};
   std::vector<Eng> es(3);
   hipStream_t sa, sb;
@@ -79,8 +84,9 @@ int main(int argc, char **argv) {
     tout += es[i].b_out;
   }
   char *h, *d;
-  CHECK(hipHostMalloc((void **)&h, tin + tout, mapped ? hipHostMallocMapped : hipHostMallocDefault));
+  CHECK(hipHostMalloc((void **)&h, tin + tout, hflags));
   CHECK(hipMalloc((void **)&d, tin + tout));
+  CHECK(hipMemset(d, 0, tin + tout));  // (D2H out of never-written device pages runs ~5x slower)
   size_t oi = 0, oo = tin;
   for (Eng &e : es) {
     e.h_in = h + oi, e.d_in = d + oi, oi += e.b_in;
@@ -102,8 +108,11 @@ int main(int argc, char **argv) {
   const int ns = sizeof(names) / sizeof(names[0]);
   std::printf("{\"tool\": \"span_probe.hip\", \"cells\": %d, \"reps\": %d, \"host\": \"%s\", \"in_bytes\": %zu, "
               "\"out_bytes\": %zu, \"schedules\": {",
-              n, reps, mapped ? "hipHostMallocMapped" : "hipHostMallocDefault", tin, tout);
+              n, reps, hf.c_str(), tin, tout);
+  const std::string only = argc > 4 ? argv[4] : "";  // a comma list of schedules (default: all)
+  bool first = true;
   for (int sc = 0; sc < ns; ++sc) {
+    if (!only.empty() && ("," + only + ",").find("," + std::string(names[sc]) + ",") == std::string::npos) continue;
     std::vector<double> t;
     for (int r = 0; r < reps + 20; ++r) {
       const double t0 = now_us();
@@ -163,8 +172,9 @@ int main(int argc, char **argv) {
       if (r >= 20) t.push_back(now_us() - t0);
     }
     std::sort(t.begin(), t.end());
-    std::printf("%s\"%s\": {\"median_us\": %.1f, \"p10_us\": %.1f, \"p90_us\": %.1f}", sc ? ", " : "", names[sc],
+    std::printf("%s\"%s\": {\"median_us\": %.1f, \"p10_us\": %.1f, \"p90_us\": %.1f}", first ? "" : ", ", names[sc],
                 t[t.size() / 2], t[t.size() / 10], t[t.size() * 9 / 10]);
+    first = false;
   }
   bool ok = true;
   for (Eng &e : es)

@@ -1345,6 +1345,16 @@ static int get_plan(fcx_engine *e, uint32_t stages, int avg_phases, Plan **pl) {
 namespace {
 
 constexpr size_t kSlabBytes = size_t(32) << 20;  // smallest slab (one Baltic-size engine: ~9 MB)
+// Page-locked host memory of the library (slabs, staging images) is allocated PORTABLE: in the
+// ROCm 7.2 runtime a device->host copy into hipHostMallocDefault or hipHostMallocMapped memory
+// runs at ~23 GB/s (5.2 MB in 225 us, and 491 us as three copies), into portable (or coherent,
+// or non-coherent) memory at ~52 GB/s (101 us), and only then do the two directions overlap
+// (6.8 MB up + 5.2 MB down at once: 130 against 349 us; bench/d2h_flags_probe.hip,
+// profiles/r06/).
+#ifndef FCX_PIN_PORTABLE  // A/B builds: 0 = the pre-round-6 flags (hipHostMallocDefault / Mapped)
+#define FCX_PIN_PORTABLE 1
+#endif
+constexpr unsigned kHostPinFlags = FCX_PIN_PORTABLE ? hipHostMallocPortable : hipHostMallocDefault;
 constexpr size_t kBlockAlign = 256;
 
 struct HostSlab {
@@ -1407,7 +1417,7 @@ extern "C" int fcx_host_malloc(size_t bytes, void **ptr) {
     HostSlab ns;
     ns.bytes = std::max(kSlabBytes, round_up(need, size_t(2) << 20));
     void *h = nullptr, *d = nullptr;
-    hipError_t err = hipHostMalloc(&h, ns.bytes, hipHostMallocMapped);
+    hipError_t err = hipHostMalloc(&h, ns.bytes, hipHostMallocMapped | kHostPinFlags);
     if (err != hipSuccess) return fail(FCX_E_NOMEM, "hipHostMalloc(%zu): %s", ns.bytes, hipGetErrorString(err));
     err = hipHostGetDevicePointer(&d, h, 0);
     if (err != hipSuccess || !d) {
@@ -1557,7 +1567,7 @@ static void classify_written(fcx_engine *e) {
 // mirrors may hold results not yet downloaded); the rest of the gap -- other inputs, free
 // slab, other engines' arrays -- lands in span bytes no mirror of this engine uses or in
 // mirrors of inputs, with the host's own values.
-constexpr size_t kUploadGap = size_t(256) << 10;
+constexpr size_t kUploadGap = size_t(448) << 10;  // ~9 us at the link's ~50 GB/s: one copy call's cost
 static bool span_gap_ok(const fcx_engine *e, int span, uintptr_t r1, uintptr_t b0, bool h2d) {
   if (b0 <= r1) return true;
   if (h2d) {
@@ -1840,7 +1850,7 @@ static bool stage_pin(fcx_engine *e, size_t i, bool lazy) {
   if (p.disabled) return false;
   const int inject = pin_fail_mode();
   if (!(inject == 1 || (inject == 2 && lazy)) &&
-      hipHostMalloc((void **)&p.host, std::max<size_t>(p.bytes, 1), hipHostMallocDefault) == hipSuccess)
+      hipHostMalloc((void **)&p.host, std::max<size_t>(p.bytes, 1), kHostPinFlags) == hipSuccess)
     return true;
   (void)hipGetLastError();
   stage_disable(e, i);
@@ -2067,7 +2077,7 @@ static int map_staged(fcx_engine *e, int *count) {
   if (items.empty()) return FCX_OK;
   StagePool p;
   void *h = nullptr, *d = nullptr;
-  hipError_t err = hipHostMalloc(&h, total, hipHostMallocMapped);
+  hipError_t err = hipHostMalloc(&h, total, hipHostMallocMapped | kHostPinFlags);
   if (err != hipSuccess) return fail(FCX_E_NOMEM, "hipHostMalloc(%zu) for the mapped staging arena: %s", total, hipGetErrorString(err));
   err = hipHostGetDevicePointer(&d, h, 0);
   if (err != hipSuccess || !d) {
@@ -2156,10 +2166,11 @@ extern "C" int fcx_commit(fcx_engine *e) {
   const int64_t n_big = std::max(e->n[0], std::max(e->n[1], e->n[2]));
   const bool small = n_big < 2 * e->min_chunk;
   if (e->zero_copy == 1 || (e->zero_copy == 2 && small)) {
-    // fcx_host_malloc arrays: in place when asked for (1); in auto mode the span transport
-    // takes them when it is on (one copy per direction beats the kernels' own reads over the
-    // link, whose two directions do not overlap: DESIGN.md section 7)
-    if (!(e->lib_spans && e->zero_copy == 2)) e->zc_active = map_host_arrays(e) > 0;
+    // fcx_host_malloc arrays in place.  (Round 6 measured the span transport against it at
+    // the Baltic size: 335-338 against 213-233 us for the three variants -- every copy and
+    // launch on a stream costs ~10-17 us of dispatch latency in this runtime, which the
+    // copy engines' duplex does not win back at 1-3 MB per engine)
+    e->zc_active = map_host_arrays(e) > 0;
     int staged = 0;
     if (e->staging)
       if (int r = map_staged(e, &staged)) return r;

@@ -42,6 +42,7 @@ MODULE flux_calculator_calculate
     PUBLIC average_across_surface_types
     PUBLIC fcx_attach, fcx_register_average, fcx_commit_engine, fcx_run_phase, fcx_detach
     PUBLIC fcx_register_abort, fcx_start_phase, fcx_finish_phase, fcx_hand_over_field
+    PUBLIC fcx_allocate_field, fcx_free_field
 
     TYPE(c_ptr), SAVE :: engine = c_null_ptr
     ! What fcx_attach bound.  The reference subroutines take the bottom model, the type count,
@@ -62,6 +63,29 @@ CONTAINS
         INTEGER(c_int) :: r
         r = fcx_set_abort_handler(handler)
     END SUBROUTINE fcx_register_abort
+
+    ! Library memory for one local_field array (INTEGRATION.md section 3): the host calls this
+    ! where the reference ALLOCATEs the array -- allocate_localvar (basic:288-309) for every
+    ! input, do_prepare_calculation (prepare:36-42) for every output -- and frees it with
+    ! fcx_free_field after fcx_detach.  fcx_host_malloc hands out consecutive blocks, so in
+    ! the reference's order the inputs form one span and the outputs another, and each phase
+    ! moves them with one copy per direction (FCX_OPT_LIB_SPANS).
+    SUBROUTINE fcx_allocate_field(field, length)
+        REAL(wp), POINTER, INTENT(INOUT) :: field(:)
+        INTEGER,           INTENT(IN)    :: length
+        TYPE(c_ptr) :: blk
+        INTEGER(c_size_t) :: bytes
+        bytes = INT(MAX(length, 1), c_size_t) * INT(STORAGE_SIZE(1.0_wp) / 8, c_size_t)
+        CALL check(fcx_host_malloc(bytes, blk), 'fcx_allocate_field')
+        CALL C_F_POINTER(blk, field, [length])
+    END SUBROUTINE fcx_allocate_field
+
+    SUBROUTINE fcx_free_field(field)
+        REAL(wp), POINTER, INTENT(INOUT) :: field(:)
+        IF (.NOT. ASSOCIATED(field)) RETURN
+        IF (SIZE(field) > 0) CALL check(fcx_host_free(C_LOC(field(1))), 'fcx_free_field')
+        NULLIFY (field)
+    END SUBROUTINE fcx_free_field
 
     ! the end of the rank on an error: message to w_unit, the host's abort routine, stop
     SUBROUTINE stop_run(msg)

@@ -337,19 +337,17 @@ enum fcx_option {
   FCX_OPT_PIPELINE_MIN_CHUNK = 8, /* ... of at least this many cells (multiple of 1024;
                                    default 262144: smaller grids take the sequential step) */
   FCX_OPT_ZERO_COPY = 9,        /* fields used by the kernels in place through the host link:
-                                   no mirrors, no copy calls.  2 auto (default): caller heap
-                                   arrays through the mapped staging arena when every grid is
-                                   below 2 x PIPELINE_MIN_CHUNK cells; fcx_host_malloc arrays
-                                   take the span transport instead (FCX_OPT_LIB_SPANS) unless
-                                   it is off.  1: in place at any size, fcx_host_malloc arrays
-                                   included; 0: never */
+                                   no mirrors, no copy calls (fcx_host_malloc arrays directly,
+                                   caller heap arrays through the mapped staging arena).
+                                   2 auto (default): when every grid is below
+                                   2 x PIPELINE_MIN_CHUNK cells; 1: at any size; 0: never */
   FCX_OPT_LIB_SPANS = 19,       /* fcx_host_malloc arrays not used in place: device mirrors
                                    laid out like the host memory (one buffer per slab span), so
                                    arrays adjacent in host memory move as ONE copy per
                                    direction -- a host allocating its inputs, then its outputs,
-                                   in the reference's order (INTEGRATION.md section 4) makes
-                                   one upload and one download per phase.  1 (default); 0: one
-                                   copy per array.  Applied at fcx_commit                  */
+                                   in the reference's order (INTEGRATION.md section 3) makes
+                                   one or two uploads and one download per phase.  1 (default);
+                                   0: one copy per array.  Applied at fcx_commit           */
   FCX_OPT_TIMING = 10,          /* record the events behind fcx_last_kernel_ms (default 0:
                                    two event records per run cost ~8 us on small grids) */
   FCX_OPT_HOST_STAGING = 15,    /* caller heap arrays (not fcx_host_malloc memory) reach

@@ -8,7 +8,11 @@
 ! No regridding matrices are set, so the reference's do_regridding calls between the
 ! calc_* calls would be no-ops and are left out.
 !
-!   dropin_host <dir> percall|fused|async|handover|noattach|badtable|badgrid|badtypes[+abort]
+!   dropin_host <dir> percall|fused|async|handover|libmem|libmem_async|noattach|badtable|badgrid|badtypes[+abort]
+!
+! libmem / libmem_async: every buffer allocated with fcx_allocate_field (library memory,
+! INTEGRATION.md section 3) in manifest order -- inputs, then outputs, as the reference
+! allocates them -- and the fused phases (started and finished) run on the span transport.
 !
 ! handover: before each fused phase every bound input field is handed over one by one
 ! (fcx_hand_over_field, as after each oasis_get), then the phase runs.
@@ -85,7 +89,12 @@ PROGRAM dropin_host
             ALLOCATE (bufs(nbufs))
         CASE ('A')
             READ (line, *) tag, k, n, path
-            ALLOCATE (bufs(k)%p(n), tmp(n))
+            IF (INDEX(mode, 'libmem') == 1) THEN
+                CALL fcx_allocate_field(bufs(k)%p, n)
+                ALLOCATE (tmp(n))
+            ELSE
+                ALLOCATE (bufs(k)%p(n), tmp(n))
+            ENDIF
             CALL read_raw(TRIM(dir)//'/'//TRIM(path), tmp)
             bufs(k)%p = REAL(tmp, wp)
             DEALLOCATE (tmp)
@@ -144,7 +153,8 @@ PROGRAM dropin_host
         CALL average_across_surface_types(1, 22, nsurf + 1, grid_size, local_field)
     ENDIF
 
-    IF (TRIM(mode) == 'fused' .OR. TRIM(mode) == 'async' .OR. TRIM(mode) == 'handover') THEN
+    IF (TRIM(mode) == 'fused' .OR. TRIM(mode) == 'async' .OR. TRIM(mode) == 'handover' .OR. &
+        INDEX(mode, 'libmem') == 1) THEN
         ! INTEGRATION.md: two phases replace :902-918 and :972-1008
         DO i = 1, nav
             CALL fcx_register_average(av(1, i) == 1, av(2, i), av(3, i))
@@ -155,7 +165,7 @@ PROGRAM dropin_host
             CALL fcx_run_phase(FCX_PHASE_EARLY)
             CALL hand_over_inputs()
             CALL fcx_run_phase(FCX_PHASE_NORMAL)
-        ELSE IF (TRIM(mode) == 'async') THEN
+        ELSE IF (TRIM(mode) == 'async' .OR. TRIM(mode) == 'libmem_async') THEN
             ! each phase started, then finished; the early phase's outputs are complete
             ! before the normal phase starts (its oasis_put precedes the normal oasis_get)
             CALL fcx_start_phase(FCX_PHASE_EARLY)
@@ -192,6 +202,11 @@ PROGRAM dropin_host
         v = outs(3, i)
         CALL write_raw(TRIM(dir)//'/'//TRIM(outpath(i)), REAL(local_field(s, g)%var(v)%field, 8))
     ENDDO
+    IF (INDEX(mode, 'libmem') == 1) THEN
+        DO k = 1, nbufs
+            CALL fcx_free_field(bufs(k)%p)
+        ENDDO
+    ENDIF
     WRITE (*, '(A)') 'DROPIN_HOST OK'
 
 CONTAINS

@@ -78,7 +78,7 @@ def write_manifest(case, d, step_time):
 
 @pytest.mark.gpu
 @pytest.mark.skipif(not os.path.exists(DROPIN), reason="Fortran drop-in host not built")
-@pytest.mark.parametrize("mode", ["percall", "fused", "async", "handover"])
+@pytest.mark.parametrize("mode", ["percall", "fused", "async", "handover", "libmem", "libmem_async"])
 @pytest.mark.parametrize("variant,T", [("CCLM", 2), ("MOM5", 3), ("RCO", 1)])
 def test_dropin_module_in_a_fortran_host(tmp_path, mode, variant, T):
     """The drop-in module flux_calculator_calculate driven by a Fortran host whose
