@@ -9,6 +9,7 @@ export TMPDIR=/tmp
 O=${1:-gpurun_out/r06/t2counters}; mkdir -p $O
 A="--types 2 --rounds 2 --steps 10"
 for b in ref t2nopf4 t2pf4; do
+  mkdir -p $O/$b
   if [ $b = ref ]; then L=""; else L="$PWD/ab/$b/libfcx.so"; fi
   FCX_LIBRARY=$L timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $O/$b/trace -o run -- \
     python3 components.flux_calculator_amd/bench/group_ab.py $A > $O/$b/group_ab.json

@@ -1345,12 +1345,14 @@ static int get_plan(fcx_engine *e, uint32_t stages, int avg_phases, Plan **pl) {
 namespace {
 
 constexpr size_t kSlabBytes = size_t(32) << 20;  // smallest slab (one Baltic-size engine: ~9 MB)
-// Page-locked host memory of the library (slabs, staging images) is allocated PORTABLE: in the
-// ROCm 7.2 runtime a device->host copy into hipHostMallocDefault or hipHostMallocMapped memory
-// runs at ~23 GB/s (5.2 MB in 225 us, and 491 us as three copies), into portable (or coherent,
-// or non-coherent) memory at ~52 GB/s (101 us), and only then do the two directions overlap
-// (6.8 MB up + 5.2 MB down at once: 130 against 349 us; bench/d2h_flags_probe.hip,
-// profiles/r06/).
+// Page-locked host memory of the library (slabs, staging images) is allocated PORTABLE.  On
+// the shared MI355X boxes a device->host copy of the Baltic step's 5.2 MB ran at ~23 GB/s in
+// some allocations and at ~52 GB/s in others, with the host->device rate moving too (128 to
+// 172 us for 6.8 MB) from one allocation to the next in one process; neither the allocation
+// flags nor the NUMA node of the pages (bound to either node of the box) explained it -- the
+// link is shared with the machine's other GPUs' jobs (bench/d2h_flags_probe.hip,
+// zc_flags_probe.hip, numa_probe.hip, profiles/r06/probes/).  Portable memory never measured
+// slower and is what a multi-device host needs.
 #ifndef FCX_PIN_PORTABLE  // A/B builds: 0 = the pre-round-6 flags (hipHostMallocDefault / Mapped)
 #define FCX_PIN_PORTABLE 1
 #endif
