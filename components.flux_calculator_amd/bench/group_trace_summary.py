@@ -3,7 +3,7 @@
 trace of `bench.py --no-cpu --e2e 0` (measurement tool).
 
 The bench's workloads run one after the other: main (random map, 10M cells), other_map
-(periodic), config4 (40M cells), each as build + cold + warm-up + event-timed per-engine
+(periodic), config5_fp32 (the fp32 engine, round 6), config4 (40M cells), each as build + cold + warm-up + event-timed per-engine
 block + one more block + the timed steps, the timed ones being the LAST `steps` group
 launches of the workload.  A workload's group launches are the run of consecutive
 cells_atmos_group_kernel dispatches of one kernel name and grid size (the 0.5-s idle gap before the cold step
@@ -33,7 +33,7 @@ def main():
         segs[-1]["durs"].append(dur)
         segs[-1]["end"] = int(r["End_Timestamp"])
     bench = json.loads([x for x in open(line) if x.startswith("{")][-1])
-    names = ["main", "other_map", "config4"]
+    names = ["main"] + [k for k in ("other_map", "config5_fp32", "config4") if k in bench]
     out = {"source": trace, "rule": f"mean of the last {steps} group launches of each workload (its timed steps)",
            "workloads": []}
     for i, s in enumerate(segs):

@@ -1569,7 +1569,7 @@ static void classify_written(fcx_engine *e) {
 // mirrors may hold results not yet downloaded); the rest of the gap -- other inputs, free
 // slab, other engines' arrays -- lands in span bytes no mirror of this engine uses or in
 // mirrors of inputs, with the host's own values.
-constexpr size_t kUploadGap = size_t(448) << 10;  // ~9 us at the link's ~50 GB/s: one copy call's cost
+constexpr size_t kUploadGap = size_t(512) << 10;  // ~9.9 us at ~53 GB/s: about what one more copy costs (9.4 us)
 static bool span_gap_ok(const fcx_engine *e, int span, uintptr_t r1, uintptr_t b0, bool h2d) {
   if (b0 <= r1) return true;
   if (h2d) {
