@@ -1356,7 +1356,11 @@ constexpr size_t kSlabBytes = size_t(32) << 20;  // smallest slab (one Baltic-si
 #ifndef FCX_PIN_PORTABLE  // A/B builds: 0 = the pre-round-6 flags (hipHostMallocDefault / Mapped)
 #define FCX_PIN_PORTABLE 1
 #endif
-constexpr unsigned kHostPinFlags = FCX_PIN_PORTABLE ? hipHostMallocPortable : hipHostMallocDefault;
+#ifndef FCX_PIN_NONCOHERENT  // A/B builds: 1 = mapped non-coherently (the GPU's L2 may hold host lines
+#define FCX_PIN_NONCOHERENT 0  // within a kernel; made visible at the kernel boundaries)
+#endif
+constexpr unsigned kHostPinFlags = (FCX_PIN_PORTABLE ? hipHostMallocPortable : hipHostMallocDefault) |
+                                   (FCX_PIN_NONCOHERENT ? hipHostMallocNonCoherent : 0u);
 constexpr size_t kBlockAlign = 256;
 
 struct HostSlab {
