@@ -27,11 +27,12 @@ class Workload:
 
     caller_device: bind contiguous torch device arrays shared by the variants instead of
     host arrays whose engine-owned device mirrors are uploaded once.
-    engine_options: extra fcx_set_option values for every engine (A/B tools)."""
+    engine_options: extra fcx_set_option values for every engine (A/B tools).
+    inputs: this rank's input arrays (inputs_for_bench's keys) instead of drawing them."""
 
     def __init__(self, n_global, rank=0, world=1, variants=VARIANTS, types=1, bias=False,
                  precision="f64", atmos=True, caller_device=False, device=0, stream=None,
-                 engine_options=None, atmos_map="periodic"):
+                 engine_options=None, atmos_map="periodic", inputs=None):
         import torch
 
         self.n_global, self.rank, self.world = int(n_global), int(rank), int(world)
@@ -42,7 +43,7 @@ class Workload:
         dev = torch.device("cuda", device)
         self.dev = dev
         self.stream = stream if stream is not None else torch.cuda.current_stream(dev)
-        host = inputs_for_bench(self.n, seed=BASE_SEED + self.offset)
+        host = inputs if inputs is not None else inputs_for_bench(self.n, seed=BASE_SEED + self.offset)
         if caller_device:
             data = {k: torch.as_tensor(v).to(dev) for k, v in host.items()}
             if f32:  # inputs rounded once; every variant's case shares them
