@@ -56,9 +56,9 @@ def perturbation_movement(c64, t, ulps=PERTURB_ULPS, trials=8):
     """max over seeded trials of |oracle(inputs * (1 +- ulps * eps32)) - oracle(inputs)| per cell"""
     base = oracle_lib.run_case(c64, "c", current_step_time=t)
     move = {k: np.zeros(np.shape(v)) for k, v in base.items()}
-    outs = {id(c64.lf.field[k]) for k in c64.outputs}
     for trial in range(trials):
         c = as_dtype(as_dtype(c64, "float32"), "float64")  # a fresh copy (the inputs are fp32 values)
+        outs = {id(c.lf.field[k]) for k in c.outputs}  # (the copy's own output arrays stay unperturbed)
         rng = np.random.default_rng([trial, 32])
         seen = set()
         for a in c.lf.field.values():

@@ -362,13 +362,13 @@ def test_span_runs_follow_the_allocation_order():
     with the outputs interleaved between the inputs take more copies, and unbound gaps between
     outputs are never written by a download."""
     c = build_case("CCLM", n=32_768, T=1, bias=False, seed=3)
-    outs = {id(c.lf.field[k]) for k in c.outputs}
     with host_alloc.Arena() as arena:
         arena.adopt(c.lf)  # dict order: inputs, then outputs
         e = engine_for(c, zero_copy=0)
         assert e.span_runs() == (1, 1)
         e.close()
     c2 = build_case("CCLM", n=32_768, T=1, bias=False, seed=3)
+    outs = {id(c2.lf.field[k]) for k in c2.outputs}  # (this case's own arrays: ids of c's may be reused)
     with host_alloc.Arena() as arena:
         moved, guards = {}, []
         for key, a in list(c2.lf.field.items()):  # interleaved: a guard block after every output
@@ -385,7 +385,7 @@ def test_span_runs_follow_the_allocation_order():
                 guards.append(g)
         e = engine_for(c2, zero_copy=0)
         up, down = e.span_runs()
-        assert down > 1, (up, down)
+        assert len(guards) == len(outs) and down > 1, (len(guards), up, down)
         reset_outputs(c2)
         e.step(PHASE_ALL, T_STEP)
         check(c2, "spans with guards between the outputs")
