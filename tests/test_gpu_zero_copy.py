@@ -392,3 +392,46 @@ def test_span_runs_follow_the_allocation_order():
         for g in guards:
             assert np.all(g == 12345.0)
         e.close()
+
+
+def test_host_malloc_blocks_follow_the_call_order():
+    """fcx_host_malloc carves 256-B aligned blocks from page-locked slabs in call order (what
+    lets the span transport move adjacent arrays as one copy): consecutive blocks are
+    adjacent, freeing the last block lets the next call take its place, a freed block in the
+    middle is not handed out again while its slab lives, a block that does not fit opens a new
+    slab, and fcx_host_free names a pointer it does not own."""
+    import ctypes
+
+    from fcx import _lib
+
+    lib = _lib.load()
+    MB = 1 << 20
+
+    def malloc(n):
+        p = ctypes.c_void_p()
+        _lib.check(lib.fcx_host_malloc(n, ctypes.byref(p)))
+        assert p.value and p.value % 256 == 0
+        ctypes.memset(p.value, 0x5A, max(n, 1))  # page-locked host memory the caller may write
+        return p.value
+
+    def free(p):
+        _lib.check(lib.fcx_host_free(ctypes.c_void_p(p)))
+
+    big = malloc(33 * MB)  # fits no partly used 32-MB slab: a fresh 34-MB slab, current from now on
+    p1 = malloc(1000)
+    p2 = malloc(5000)
+    assert p1 == big + 33 * MB and p2 == p1 + 1024
+    free(p2)
+    p3 = malloc(100)
+    assert p3 == p2  # the tail block's place is reused
+    free(p1)
+    p4 = malloc(100)
+    assert p4 == p3 + 256  # the hole p1 left is not
+    p5 = malloc(2 * MB)  # ~1 MB left in the slab: a new one
+    assert not (big <= p5 < big + 34 * MB)
+    for p in (big, p3, p4, p5):
+        free(p)
+    free(None)  # NULL is a no-op, as free(3)
+    foreign = ctypes.create_string_buffer(64)
+    assert lib.fcx_host_free(ctypes.cast(foreign, ctypes.c_void_p)) != 0
+    assert b"fcx_host_malloc" in lib.fcx_last_error()
