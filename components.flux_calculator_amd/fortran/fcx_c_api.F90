@@ -378,6 +378,90 @@ MODULE fcx_c_api
       CHARACTER(kind=c_char), DIMENSION(*), INTENT(IN) :: message
       INTEGER(c_int) :: fcx_abort
     END FUNCTION
+    ! -- the rest of include/fcx.h: plan audit, streams, device memory, diagnostics --------
+    FUNCTION fcx_plan_check(engine) BIND(C, name='fcx_plan_check')
+      IMPORT :: c_int, c_ptr
+      TYPE(c_ptr), VALUE :: engine
+      INTEGER(c_int) :: fcx_plan_check
+    END FUNCTION
+    FUNCTION fcx_set_stream(engine, hip_stream) BIND(C, name='fcx_set_stream')
+      IMPORT :: c_int, c_ptr
+      TYPE(c_ptr), VALUE :: engine, hip_stream
+      INTEGER(c_int) :: fcx_set_stream
+    END FUNCTION
+    FUNCTION fcx_device_ptr(engine, surface_type, grid, var, dptr) BIND(C, name='fcx_device_ptr')
+      IMPORT :: c_int, c_ptr
+      TYPE(c_ptr), VALUE :: engine
+      INTEGER(c_int), VALUE :: surface_type, grid, var
+      TYPE(c_ptr), INTENT(OUT) :: dptr
+      INTEGER(c_int) :: fcx_device_ptr
+    END FUNCTION
+    FUNCTION fcx_device_layout(engine, tile, tile_stride) BIND(C, name='fcx_device_layout')
+      IMPORT :: c_int, c_int64_t, c_ptr
+      TYPE(c_ptr), VALUE :: engine
+      INTEGER(c_int64_t), INTENT(OUT) :: tile, tile_stride
+      INTEGER(c_int) :: fcx_device_layout
+    END FUNCTION
+    FUNCTION fcx_last_kernel_ms(engine, ms) BIND(C, name='fcx_last_kernel_ms')
+      IMPORT :: c_int, c_float, c_ptr
+      TYPE(c_ptr), VALUE :: engine
+      REAL(c_float), INTENT(OUT) :: ms
+      INTEGER(c_int) :: fcx_last_kernel_ms
+    END FUNCTION
+    FUNCTION fcx_span_runs(engine, phase, h2d_copies, d2h_copies) BIND(C, name='fcx_span_runs')
+      IMPORT :: c_int, c_int32_t, c_ptr
+      TYPE(c_ptr), VALUE :: engine
+      INTEGER(c_int), VALUE :: phase
+      INTEGER(c_int32_t), INTENT(OUT) :: h2d_copies, d2h_copies
+      INTEGER(c_int) :: fcx_span_runs
+    END FUNCTION
+    FUNCTION fcx_algorithmic_bytes(engine, phase, bytes) BIND(C, name='fcx_algorithmic_bytes')
+      IMPORT :: c_int, c_int64_t, c_ptr
+      TYPE(c_ptr), VALUE :: engine
+      INTEGER(c_int), VALUE :: phase
+      INTEGER(c_int64_t), INTENT(OUT) :: bytes
+      INTEGER(c_int) :: fcx_algorithmic_bytes
+    END FUNCTION
+    FUNCTION fcx_set_atmos_shared(engine, shared, n_boundaries, stride, left, right) &
+        BIND(C, name='fcx_set_atmos_shared')
+      IMPORT :: c_int, c_int32_t, c_ptr
+      TYPE(c_ptr), VALUE :: engine, shared
+      INTEGER(c_int32_t), VALUE :: n_boundaries, stride, left, right
+      INTEGER(c_int) :: fcx_set_atmos_shared
+    END FUNCTION
+    FUNCTION fcx_comm_allreduce_sum(comm, buf, count, hip_stream) BIND(C, name='fcx_comm_allreduce_sum')
+      IMPORT :: c_int, c_size_t, c_ptr
+      TYPE(c_ptr), VALUE :: comm, buf, hip_stream
+      INTEGER(c_size_t), VALUE :: count
+      INTEGER(c_int) :: fcx_comm_allreduce_sum
+    END FUNCTION
+    FUNCTION fcx_atmos_allreduce(comm, engines, n_engines) BIND(C, name='fcx_atmos_allreduce')
+      IMPORT :: c_int, c_ptr
+      TYPE(c_ptr), VALUE :: comm
+      TYPE(c_ptr), DIMENSION(*), INTENT(IN) :: engines
+      INTEGER(c_int), VALUE :: n_engines
+      INTEGER(c_int) :: fcx_atmos_allreduce
+    END FUNCTION
+    FUNCTION fcx_device_malloc(device, bytes, ptr) BIND(C, name='fcx_device_malloc')
+      IMPORT :: c_int, c_size_t, c_ptr
+      INTEGER(c_int), VALUE :: device
+      INTEGER(c_size_t), VALUE :: bytes
+      TYPE(c_ptr), INTENT(OUT) :: ptr
+      INTEGER(c_int) :: fcx_device_malloc
+    END FUNCTION
+    FUNCTION fcx_device_free(ptr) BIND(C, name='fcx_device_free')
+      IMPORT :: c_int, c_ptr
+      TYPE(c_ptr), VALUE :: ptr
+      INTEGER(c_int) :: fcx_device_free
+    END FUNCTION
+    ! kind: 1 host->device, 2 device->host, 3 device->device (synchronous)
+    FUNCTION fcx_memcpy(dst, src, bytes, kind) BIND(C, name='fcx_memcpy')
+      IMPORT :: c_int, c_size_t, c_ptr
+      TYPE(c_ptr), VALUE :: dst, src
+      INTEGER(c_size_t), VALUE :: bytes
+      INTEGER(c_int), VALUE :: kind
+      INTEGER(c_int) :: fcx_memcpy
+    END FUNCTION
   END INTERFACE
 
 CONTAINS

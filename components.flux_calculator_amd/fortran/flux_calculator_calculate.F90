@@ -279,7 +279,11 @@ CONTAINS
                    'fcx_add_average')
     END SUBROUTINE fcx_register_average
 
+    ! every plan the engine can launch audited on the host first (fcx_plan_check: a method
+    ! that would read an input the set-up left unbound stops here with a named error, before
+    ! any device memory is taken), then validation and the device mirrors
     SUBROUTINE fcx_commit_engine()
+        CALL check(fcx_plan_check(engine), 'fcx_plan_check')
         CALL check(fcx_commit(engine), 'fcx_commit')
     END SUBROUTINE fcx_commit_engine
 

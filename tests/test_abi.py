@@ -37,6 +37,14 @@ def test_library_exports_every_declared_symbol():
     assert set(declared_symbols()) == bound, set(declared_symbols()) ^ bound
 
 
+def test_fortran_module_binds_every_declared_symbol():
+    """fortran/fcx_c_api.F90 carries one BIND(C) interface per entry point of include/fcx.h
+    (a Fortran host reaches the whole ABI), and nothing the header no longer declares."""
+    f90 = open(os.path.join(ROOT, "components.flux_calculator_amd", "fortran", "fcx_c_api.F90")).read()
+    bound = set(re.findall(r"BIND\(C,\s*name='(fcx_\w+)'\)", f90))
+    assert bound == set(declared_symbols()), set(declared_symbols()) ^ bound
+
+
 def test_library_is_gfx950_only_and_unversioned_hip():
     data = open(_lib.LIB_PATH, "rb").read()
     assert b"gfx950" in data
